@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident FASTA header-index scan (BASELINE.json configs[1]) on 1..N MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--no-cpu-baseline]
+
+One step = one whole co.preprocess(chunk_size=size/4) equivalent over one synthetic 4 GiB FASTA object
+that is already resident in HBM: chunk-plan upload, the single-pass scan kernel, the split-header
+resolve kernel and the read-back of the pair count / per-chunk state (the index itself stays in HBM;
+the H2D/D2H-inclusive end-to-end rate is reported separately).
+
+Multi-GPU (``torch.distributed.run --nproc-per-node N``): one process per GPU, each indexing its own
+object (independent objects/chunks, no collective on the data path; weak scaling).  Barrier + device
+sync bracket the K timed steps; the max time over ranks is reported.
+
+Also measured inside this run: the scan kernel's average duration from HIP events on its own stream
+(-> roofline), and, on rank 0 at N = 1, the reference algorithm on the host cores (cpu_baseline).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK = 8.0e12   # B/s, MI355X spec (MI355X_MICROARCH.md §Chip-level parameters)
+GiB = float(1 << 30)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--size", type=int, default=4 << 30)
+    p.add_argument("--chunks", type=int, default=4, help="chunk_size = ceil(size / chunks) (fasta_example.py)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--traffic-bytes", type=float, default=None,
+                   help="HBM bytes per scan launch from a rocprofv3 --pmc pass (profiles/), if measured")
+    return p.parse_args()
+
+
+def init_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = dist_mod
+    return world, rank, local, dist
+
+
+def barrier(dist, local):
+    if dist is not None:
+        import torch
+        dist.barrier()
+        torch.cuda.synchronize(local)
+
+
+def max_over_ranks(dist, local, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, local, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def _regex_chunk(args):
+    """cpu_baseline worker: the reference's per-chunk scan (fasta.py:36-56), restated in oracle/cpu_ref."""
+    from oracle import cpu_ref
+    c0, c1 = args
+    return len(cpu_ref.fasta_chunk_pairs(_CPU_OBJ, c0, c1))
+
+
+_CPU_OBJ = b""
+
+
+def cpu_baseline(host: np.ndarray, chunk_size: int):
+    """The reference algorithm (re.finditer per chunk + fix-up) on the host cores, bounded sample."""
+    import multiprocessing as mp
+    global _CPU_OBJ
+    sample = min(len(host), 1 << 30)                 # bounded sample: the object's first GiB
+    _CPU_OBJ = host[:sample].tobytes()
+    cs = max(1, min(chunk_size, sample // 64))       # fan chunks out over a fork pool
+    plan = [(i * cs, (i + 1) * cs) for i in range(sample // cs)]
+    cores = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(cores) as pool:
+        pool.map(_regex_chunk, plan, chunksize=1)
+    t_pool = time.perf_counter() - t0
+    one = _CPU_OBJ[: 256 << 20]
+    t0 = time.perf_counter()
+    from oracle import cpu_ref
+    cpu_ref.fasta_chunk_pairs(one, 0, len(one))
+    t_one = time.perf_counter() - t0
+    scanned = len(plan) * cs
+    return {"value": round(scanned / t_pool / GiB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"first {scanned / GiB:.2f} GiB of the object, {len(plan)} chunks of {cs} B, "
+                      f"re.finditer(rb'>.+(\\n)?') + fix-up per chunk (fasta.py:36-56) over a fork pool",
+            "value_1core": round(len(one) / t_one / GiB, 3)}
+
+
+def main():
+    args = parse()
+    world, rank, local, dist = init_dist(args)
+    from dataplug_amd import synth
+    from dataplug_amd.scan import ScanContext
+
+    ctx = ScanContext(local)
+    size = args.size
+    chunk_size = math.ceil(size / args.chunks)
+    plan = [(i * chunk_size, size if chunk_size == size // chunk_size - 1 else (i + 1) * chunk_size)
+            for i in range(size // chunk_size)]
+    chunks = np.ascontiguousarray(np.asarray(plan, np.uint64).reshape(-1))
+
+    # synthetic object for this rank (seeded; repeated non-power-of-two base block), resident in HBM
+    t0 = time.perf_counter()
+    host = synth.tiled_fasta_host(size, seed=1 + rank)
+    gen_s = time.perf_counter() - t0
+    d_in = ctx.workspace("bench_in", size + 64)
+    ctx.h2d(d_in.ptr, host)
+    cap = size // 256 + 1024
+    d_out = ctx.workspace("bench_out", 8 * cap)
+
+    def step():
+        ctx.fasta_index_async(d_in.ptr, size, 0, size, chunks, d_out.ptr, False, cap)
+        return ctx.fasta_result(len(plan))
+
+    for _ in range(args.warmup):
+        n_pairs, pending, cend = step()
+    ctx.timing(True)
+    ctx.timing_read()
+    barrier(dist, local)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        n_pairs, pending, cend = step()
+    ctx.sync()
+    barrier(dist, local)
+    dt = time.perf_counter() - t0
+    kern_ms, launches = ctx.timing_read()
+    ctx.timing(False)
+
+    dt_max = max_over_ranks(dist, local, dt)
+    total_bytes = sum_over_ranks(dist, local, float(size) * args.steps)
+    total_offsets = sum_over_ranks(dist, local, 2.0 * n_pairs * args.steps)
+    kern_avg_s = kern_ms / 1e3 / max(1, launches)
+    kern_avg_max = max_over_ranks(dist, local, kern_avg_s)
+
+    verified = None
+    if not args.no_verify and rank == 0:
+        from oracle import dpref
+        exp = dpref.fasta_pairs(host, plan)
+        got = np.empty((n_pairs, 2), np.uint32)
+        ctx.d2h(got, d_out.ptr)
+        verified = bool(np.array_equal(got.astype(np.uint64), exp))
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(host, chunk_size)
+
+    if rank == 0:
+        alg_bytes = size + 8.0 * n_pairs            # N input bytes read once + 8 B per (start, end) pair
+        achieved = alg_bytes / kern_avg_max
+        value = total_bytes / dt_max / GiB
+        out = {
+            "metric": "fasta_index_scan_GiB_per_s_device_resident",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": f"FASTA '>' header index, {size / GiB:g} GiB synthetic object per GPU, "
+                                   f"chunk_size=size/{args.chunks} (BASELINE configs[1])",
+                       "object_bytes": size, "chunks": len(plan), "pairs": int(n_pairs),
+                       "parallelism": f"independent objects x{world}, no collective"},
+            "offsets_per_s": round(total_offsets / dt_max, 1),
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+                         "traffic": args.traffic_bytes,
+                         "kernel": "scan_kernel<FASTA>", "kernel_avg_us": round(kern_avg_max * 1e6, 2),
+                         "alg_bytes_per_launch": int(alg_bytes)},
+            "cpu_baseline": cpu,
+            "verified_bit_exact": verified,
+            "gen_s": round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

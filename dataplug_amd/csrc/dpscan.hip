@@ -1,0 +1,1000 @@
+// dpscan.hip — MI355X (gfx950, CDNA4) record-boundary scan kernels + the C ABI of libdpscan.so.
+//
+// What runs here:
+//   * scan_kernel<FASTA>: the FASTA header index of dataplug/formats/genomics/fasta.py:24-63 for a whole
+//     chunk plan in ONE pass over HBM; emits (start, end) offset pairs bit-exact to the reference.
+//   * scan_kernel<DELIM>: sorted offsets of a delimiter byte (CSV/VCF newline index, FASTQ read ends).
+//   * fasta_resolve_kernel / find_kernel: the "header cut by the chunk end" fix-up (fasta.py:45-56).
+//
+// Single-pass structure (memory-bound byte scan, no MFMA):
+//   * persistent grid, workgroup = 4 waves; a workgroup owns a 32 KiB "unit" per iteration (each wave a
+//     contiguous 8 KiB, 8 rows of 1 KiB = 64 lanes x 16 B global_load_dwordx4, all issued up front and
+//     kept in VGPRs).
+//   * per 16-byte lane: SWAR exact byte-match masks ('>' and '\n'), a carry trick that marks the first
+//     valid '>' of every line segment, and 64-lane ballot scans for the carried line state and the
+//     emit counts (bit-sliced ballots + mbcnt) — no LDS traffic in the row loop.
+//   * phase A computes the unit's summary as a FUNCTION of the incoming line state (count / out-state
+//     if the unit starts inside a line that already emitted a header, or not); units chain their
+//     summaries with a decoupled look-back over 8-byte {status, value} descriptors (agent-scope relaxed
+//     atomics = sc1, one store per descriptor, see cdna_hip_programming.md G16 R2); phase B replays the
+//     registers with the true prefix and writes the offsets.  Input bytes are read from HBM exactly once.
+//   * all waits on other workgroups are bounded (DP_ERR_TIMEOUT) — units are statically strided over a
+//     grid sized to be fully resident, so a unit only ever waits on lower units already running.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/dpscan.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWaves = 4;                          // waves per workgroup
+constexpr int kThreads = kWave * kWaves;
+constexpr int kRowBytes = kWave * 16;              // one dwordx4 per lane
+constexpr int kRows = 8;                           // rows per wave per unit
+constexpr int kWaveBytes = kRowBytes * kRows;      // 8 KiB
+constexpr int kUnitBytes = kWaveBytes * kWaves;    // 32 KiB look-back unit
+constexpr uint32_t kGT = 0x3E3E3E3Eu;              // '>'
+constexpr uint32_t kNL = 0x0A0A0A0Au;              // '\n'
+
+constexpr uint32_t kErrTimeout = 1u;
+constexpr uint32_t kErrOverflow = 2u;
+
+constexpr uint64_t kStatAgg = 1ull << 62;
+constexpr uint64_t kStatPrefix = 2ull << 62;
+constexpr uint64_t kStatMask = 3ull << 62;
+constexpr uint32_t kSpinLimit = 1u << 22;          // x s_sleep(2) per poll: well above any legal wait
+
+enum Mode { kFasta = 0, kDelim = 1 };
+
+struct ScanArgs {
+  const uint8_t* base;         // 16-byte aligned base; coordinates below are relative to it
+  uint64_t shift;              // buffer start - base (0..15)
+  uint64_t obj_base;           // object offset of buffer byte 0
+  const uint64_t* chunk_lo;    // [nchunks] aligned coords
+  const uint64_t* chunk_hi;    // [nchunks]
+  const uint64_t* chunk_u0;    // [nchunks + 1] first unit of each chunk
+  uint64_t nchunks;
+  uint64_t nunits;
+  unsigned long long* desc;    // [nunits] look-back descriptors (zeroed per launch)
+  void* out;
+  uint64_t cap;                // entries (FASTA: pairs)
+  int out_u64;
+  uint32_t delim;              // DELIM: byte replicated x4
+  uint32_t every_k;
+  uint32_t emit_add;
+  uint32_t* err;
+  unsigned long long* total;   // [2] inclusive count of the last unit; (DELIM) number of delimiters
+  long long* pending;          // FASTA: [nchunks] pair index whose end is unresolved at chunk end, or -1
+  unsigned long long* chunk_end;  // [nchunks] inclusive count at the end of each (non-empty) chunk
+};
+
+// ------------------------------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t pat) {
+  // exact: bit 8j+7 set iff byte j of w equals the pattern byte
+  const uint32_t x = w ^ pat;
+  const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(t | x) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t pack4(uint32_t e) {
+  // bits 7,15,23,31 -> bits 0..3 (mul_u32_u24 gather)
+  const uint32_t f = e >> 7;
+  return ((((f & 0x10101u) * 0x4081u) >> 14) & 7u) | (f >> 21);
+}
+__device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t pat) {
+  return pack4(eq4(v.x, pat)) | (pack4(eq4(v.y, pat)) << 4) | (pack4(eq4(v.z, pat)) << 8) |
+         (pack4(eq4(v.w, pat)) << 12);
+}
+__device__ __forceinline__ bool maybe_has(const uint4& v, uint32_t pat) {
+  // no false negatives (classic haszero); false positives only make the exact path run
+  auto hz = [](uint32_t x) { return (x - 0x01010101u) & ~x; };
+  return ((hz(v.x ^ pat) | hz(v.y ^ pat) | hz(v.z ^ pat) | hz(v.w ^ pat)) & 0x80808080u) != 0;
+}
+__device__ __forceinline__ uint32_t clip16(uint64_t pos0, uint64_t lo, uint64_t hi) {
+  uint32_t m = 0xFFFFu;
+  if (pos0 < lo) m = (lo - pos0 >= 16) ? 0u : (m << (uint32_t)(lo - pos0)) & 0xFFFFu;
+  if (pos0 + 16 > hi) m = (hi <= pos0) ? 0u : m & ((1u << (uint32_t)(hi - pos0)) - 1u);
+  return m;
+}
+__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+__device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+// exclusive wave prefix + total of small per-lane counts (< 2^BITS), bit-sliced ballots
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& total) {
+  uint32_t ex = 0, tot = 0;
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) {
+    const uint64_t m = __ballot((c >> b) & 1u);
+    ex += mbcnt(m) << b;
+    tot += (uint32_t)__popcll(m) << b;
+  }
+  total = tot;
+  return ex;
+}
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_total(uint32_t c) {
+  uint32_t tot = 0;
+#pragma unroll
+  for (int b = 0; b < BITS; ++b) tot += (uint32_t)__popcll(__ballot((c >> b) & 1u)) << b;
+  return tot;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, l);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t ld_desc(unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_desc(unsigned long long* p, uint64_t v) {
+  __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Summary of a byte range as a function of the incoming line state S (does the current line already
+// hold an emitted header?): count and outgoing state for S = false (F) and S = true (T).
+struct Func {
+  uint64_t cF, cT;
+  uint32_t sF, sT;
+};
+__device__ __forceinline__ Func f_identity() { return Func{0, 0, 0u, 1u}; }
+__device__ __forceinline__ Func f_then(const Func& a, const Func& b) {   // a, then b
+  Func r;
+  r.cF = a.cF + (a.sF ? b.cT : b.cF);
+  r.sF = a.sF ? b.sT : b.sF;
+  r.cT = a.cT + (a.sT ? b.cT : b.cF);
+  r.sT = a.sT ? b.sT : b.sF;
+  return r;
+}
+__device__ __forceinline__ uint64_t pack_agg(const Func& f) {
+  return kStatAgg | ((uint64_t)f.sT << 49) | ((uint64_t)f.sF << 48) | ((f.cT & 0xFFFFFFull) << 24) |
+         (f.cF & 0xFFFFFFull);
+}
+__device__ __forceinline__ Func unpack_agg(uint64_t d) {
+  return Func{d & 0xFFFFFFull, (d >> 24) & 0xFFFFFFull, (uint32_t)(d >> 48) & 1u, (uint32_t)(d >> 49) & 1u};
+}
+__device__ __forceinline__ uint64_t pack_prefix(uint64_t count, uint32_t s) {
+  return kStatPrefix | ((uint64_t)s << 48) | (count & 0xFFFFFFFFFFFFull);
+}
+
+// One 16-byte lane of a FASTA row.  Inputs: lane's bytes, clip mask, next-byte-is-'\n' for bit 15,
+// whether the chunk's last byte (p = c1-1, never a header: needs p+1 < c1) is in this lane, and the
+// wave-uniform incoming state S.  See DESIGN.md §3.2 for the derivation of the carry trick.
+struct FRow {
+  uint32_t V, nl, emits, ends;
+  uint32_t s_before_nl;   // line state just before this lane's first '\n'
+  uint64_t H;             // ballot: lanes holding a '\n'
+  uint32_t S_out;         // wave-uniform state after the row
+};
+__device__ __forceinline__ FRow fasta_row(const uint4& v, uint32_t valid, uint32_t nxt_nl, int last_bit,
+                                          uint32_t S, int lane) {
+  FRow f;
+  const uint32_t gt = mask16(v, kGT) & valid;
+  const uint32_t nl = mask16(v, kNL) & valid;
+  const uint32_t nb = (__shfl_down((int)nl, 1) & 1);
+  const uint32_t nxt = (lane == kWave - 1) ? nxt_nl : nb;
+  uint32_t V = gt & ~((nl >> 1) | (nxt << 15));      // '>' followed by a non-'\n' byte
+  if (last_bit >= 0) V &= ~(1u << last_bit);          // p + 1 < c1
+  const uint32_t X = V | nl;
+  const uint32_t R = ((~X) & 0xFFFFu) + ((nl << 1) | 1u);   // first X bit at/after each line start
+  const uint32_t low = nl & (0u - nl);
+  const uint32_t fs = low ? low - 1u : 0xFFFFu;       // bits before the lane's first '\n'
+  const uint32_t s_last = ((R >> 16) & 1u) ^ 1u;      // a valid '>' after the lane's last '\n'
+  const uint64_t H = __ballot(nl != 0u);
+  const uint64_t SB = __ballot(s_last);
+  const uint64_t lt = lanemask_lt(lane);
+  const uint64_t prior = H & lt;
+  uint32_t S_lane;
+  if (prior) S_lane = ((SB & lt) >> (63 - __clzll(prior))) != 0ull;
+  else S_lane = S || ((SB & lt) != 0ull);
+  f.V = V;
+  f.nl = nl;
+  f.emits = V & R & (S_lane ? ~fs : 0xFFFFu);
+  f.ends = nl & (~R | (S_lane ? low : 0u));
+  f.s_before_nl = S_lane || ((V & fs) != 0u);
+  f.H = H;
+  f.S_out = H ? ((SB >> (63 - __clzll(H))) != 0ull) : (S || SB != 0ull);
+  return f;
+}
+
+template <typename T>
+__device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
+  reinterpret_cast<T*>(out)[i] = (T)v;
+}
+
+// ------------------------------------------------------------------------------------------ scan kernel
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A) {
+  const int lane = __lane_id();
+  const int wave = threadIdx.x >> 6;
+  __shared__ uint64_t s_cF[kWaves], s_cT[kWaves], s_P[kWaves];
+  __shared__ uint32_t s_sF[kWaves], s_sT[kWaves], s_S[kWaves];
+
+  for (uint64_t u = blockIdx.x; u < A.nunits; u += gridDim.x) {
+    // ---- unit -> chunk (uniform binary search over chunk_u0)
+    uint64_t c = 0, cn = A.nchunks;
+    while (cn - c > 1) {
+      const uint64_t m = (c + cn) >> 1;
+      if (A.chunk_u0[m] <= u) c = m; else cn = m;
+    }
+    const uint64_t lo = A.chunk_lo[c], hi = A.chunk_hi[c];
+    const uint64_t cu0 = A.chunk_u0[c];
+    const bool chunk_first = (u == cu0);
+    const bool chunk_last = (u + 1 == A.chunk_u0[c + 1]);
+    const uint64_t wbase = (lo & ~15ull) + (u - cu0) * (uint64_t)kUnitBytes + (uint64_t)wave * kWaveBytes;
+
+    uint4 v[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const uint64_t a = wbase + (uint64_t)r * kRowBytes + (uint64_t)lane * 16;
+      v[r] = (a < hi) ? *reinterpret_cast<const uint4*>(A.base + a) : make_uint4(0, 0, 0, 0);
+    }
+
+    // ---------------- phase A: summary of this wave's 8 KiB as a function of the incoming state
+    Func ws;
+    uint32_t dmask[kRows];
+    if constexpr (MODE == kFasta) {
+      uint32_t S = 0, nlseen = 0, fV = 0;
+      uint64_t cnt = 0;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const uint64_t row0 = wbase + (uint64_t)r * kRowBytes;
+        if (row0 >= hi) break;
+        const bool need = S || !nlseen || (__ballot(maybe_has(v[r], kGT)) != 0ull);
+        if (!need) continue;
+        const uint64_t pos0 = row0 + (uint64_t)lane * 16;
+        uint32_t nxt = 0;
+        const uint64_t rend = row0 + kRowBytes;
+        if (rend < hi) {
+          if (r + 1 < kRows) nxt = ((uint32_t)__builtin_amdgcn_readlane((int)v[(r + 1) & (kRows - 1)].x, 0) & 0xFFu) == 10u;
+          else nxt = A.base[rend] == 10;
+        }
+        const int64_t lb = (int64_t)hi - 1 - (int64_t)pos0;
+        const FRow f = fasta_row(v[r], clip16(pos0, lo, hi), nxt, (lb >= 0 && lb < 16) ? (int)lb : -1, S, lane);
+        if (!nlseen && f.H) {
+          fV = __builtin_amdgcn_readlane((int)f.s_before_nl, (int)__builtin_ctzll(f.H));
+          nlseen = 1;
+        }
+        cnt += wave_total<3>((uint32_t)__popc(f.emits));
+        S = f.S_out;
+      }
+      if (!nlseen) fV = S;
+      ws.cF = cnt;
+      ws.cT = cnt - fV;
+      ws.sF = S;
+      ws.sT = nlseen ? S : 1u;
+      if (chunk_first && wave == 0) { ws.cT = ws.cF; ws.sT = ws.sF; }
+    } else {
+      uint64_t cnt = 0;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const uint64_t pos0 = wbase + (uint64_t)r * kRowBytes + (uint64_t)lane * 16;
+        dmask[r] = mask16(v[r], A.delim) & clip16(pos0, lo, hi);
+        cnt += wave_total<5>((uint32_t)__popc(dmask[r]));
+      }
+      ws = Func{cnt, cnt, 0u, 0u};
+    }
+    if (lane == 0) {
+      s_cF[wave] = ws.cF; s_cT[wave] = ws.cT; s_sF[wave] = ws.sF; s_sT[wave] = ws.sT;
+    }
+    __syncthreads();
+
+    // ---------------- look-back (wave 0): prefix count + line state entering this unit
+    if (wave == 0) {
+      Func w[kWaves];
+#pragma unroll
+      for (int i = 0; i < kWaves; ++i) w[i] = Func{s_cF[i], s_cT[i], s_sF[i], s_sT[i]};
+      Func unit = w[0];
+#pragma unroll
+      for (int i = 1; i < kWaves; ++i) unit = f_then(unit, w[i]);
+
+      uint64_t P = 0;
+      uint32_t S_in = 0;
+      if (u > 0) {
+        if (lane == 0) st_desc(&A.desc[u], pack_agg(unit));
+        Func acc = f_identity();
+        int64_t j = (int64_t)u - 1;
+        for (;;) {
+          const int64_t t = j - lane;
+          uint64_t d;
+          uint64_t pref;
+          uint32_t spins = 0;
+          for (;;) {
+            d = (t >= 0) ? ld_desc(&A.desc[t]) : pack_prefix(0, 0);
+            const uint64_t inval = __ballot((d & kStatMask) == 0ull);
+            pref = __ballot((d & kStatMask) == kStatPrefix);
+            const uint64_t nearer = pref ? ((pref & (0ull - pref)) - 1ull) : ~0ull;
+            if ((inval & nearer) == 0ull) break;
+            if (++spins > kSpinLimit) {
+              if (lane == 0) atomicOr(A.err, kErrTimeout);
+              pref = 1ull;            // give up: pretend the nearest is a prefix of 0
+              d = pack_prefix(0, 0);
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+          }
+          const int k = pref ? (int)__builtin_ctzll(pref) : kWave;
+          Func win = f_identity();
+          for (int l = k - 1; l >= 0; --l) win = f_then(win, unpack_agg(readlane64(d, l)));
+          acc = f_then(win, acc);
+          if (k < kWave) {
+            const uint64_t pd = readlane64(d, k);
+            const uint64_t pc = pd & 0xFFFFFFFFFFFFull;
+            const uint32_t ps = (uint32_t)(pd >> 48) & 1u;
+            P = pc + (ps ? acc.cT : acc.cF);
+            S_in = ps ? acc.sT : acc.sF;
+            break;
+          }
+          j -= kWave;
+        }
+      }
+      const uint64_t P_incl = P + (S_in ? unit.cT : unit.cF);
+      const uint32_t S_out = S_in ? unit.sT : unit.sF;
+      if (lane == 0) {
+        st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
+        uint64_t p = P;
+        uint32_t s = chunk_first ? 0u : S_in;
+#pragma unroll
+        for (int i = 0; i < kWaves; ++i) {
+          s_P[i] = p;
+          s_S[i] = s;
+          p += s ? w[i].cT : w[i].cF;
+          s = s ? w[i].sT : w[i].sF;
+        }
+        if (u + 1 == A.nunits) A.total[0] = P_incl;
+        if (chunk_last) {
+          A.chunk_end[c] = P_incl;
+          if constexpr (MODE == kFasta) A.pending[c] = S_out ? (long long)P_incl - 1 : -1ll;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---------------- phase B: replay the registers with the true prefix and write offsets
+    uint64_t count = s_P[wave];
+    const uint64_t obase = A.obj_base - A.shift;   // object offset = obase + aligned coordinate
+    if constexpr (MODE == kFasta) {
+      uint32_t S = s_S[wave];
+      bool ovf = false;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const uint64_t row0 = wbase + (uint64_t)r * kRowBytes;
+        if (row0 >= hi) break;
+        const bool need = S || (__ballot(maybe_has(v[r], kGT)) != 0ull);
+        if (!need) continue;
+        const uint64_t pos0 = row0 + (uint64_t)lane * 16;
+        uint32_t nxt = 0;
+        const uint64_t rend = row0 + kRowBytes;
+        if (rend < hi) {
+          if (r + 1 < kRows) nxt = ((uint32_t)__builtin_amdgcn_readlane((int)v[(r + 1) & (kRows - 1)].x, 0) & 0xFFu) == 10u;
+          else nxt = A.base[rend] == 10;
+        }
+        const int64_t lb = (int64_t)hi - 1 - (int64_t)pos0;
+        const FRow f = fasta_row(v[r], clip16(pos0, lo, hi), nxt, (lb >= 0 && lb < 16) ? (int)lb : -1, S, lane);
+        uint32_t tot;
+        const uint32_t ex = wave_excl<3>((uint32_t)__popc(f.emits), tot);
+        const uint64_t i0 = count + ex;
+        const uint64_t ob = obase + pos0;
+        for (uint32_t e = f.emits; e; e &= e - 1u) {
+          const int b = __builtin_ctz(e);
+          const uint64_t i = i0 + (uint32_t)__popc(f.emits & ((1u << b) - 1u));
+          const uint64_t val = ob + (uint64_t)b;
+          if (i < A.cap) {
+            if (A.out_u64) put<uint64_t>(A.out, 2 * i, val);
+            else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, 2 * i, val); }
+          }
+        }
+        for (uint32_t e = f.ends; e; e &= e - 1u) {
+          const int b = __builtin_ctz(e);
+          const uint64_t i = i0 + (uint32_t)__popc(f.emits & ((1u << b) - 1u)) - 1u;
+          const uint64_t val = ob + (uint64_t)b + 1u;
+          if (i < A.cap) {
+            if (A.out_u64) put<uint64_t>(A.out, 2 * i + 1, val);
+            else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, 2 * i + 1, val); }
+          }
+        }
+        count += tot;
+        S = f.S_out;
+      }
+      if (ovf) atomicOr(A.err, kErrOverflow);
+    } else {
+      const uint32_t k = A.every_k;
+      bool ovf = false;
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) {
+        const uint32_t m = dmask[r];
+        uint32_t tot;
+        const uint32_t ex = wave_excl<5>((uint32_t)__popc(m), tot);
+        if (tot == 0) continue;
+        const uint64_t pos0 = wbase + (uint64_t)r * kRowBytes + (uint64_t)lane * 16;
+        const uint64_t i0 = count + ex;
+        const uint64_t ob = obase + pos0 + A.emit_add;
+        for (uint32_t e = m; e; e &= e - 1u) {
+          const int b = __builtin_ctz(e);
+          uint64_t g = i0 + (uint32_t)__popc(m & ((1u << b) - 1u));
+          if (k != 1) {
+            if (g % k != k - 1) continue;
+            g /= k;
+          }
+          const uint64_t val = ob + (uint64_t)b;
+          if (g < A.cap) {
+            if (A.out_u64) put<uint64_t>(A.out, g, val);
+            else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, g, val); }
+          }
+        }
+        count += tot;
+      }
+      if (ovf) atomicOr(A.err, kErrOverflow);
+    }
+  }
+}
+
+// first position >= from (aligned coords) holding the delimiter, inside [from, end); -1 if none.  One wave.
+__device__ uint64_t wave_find(const uint8_t* base, uint64_t from, uint64_t end, uint32_t pat, int lane, bool& found) {
+  for (uint64_t a = from & ~15ull; a < end; a += kRowBytes) {
+    const uint64_t pa = a + (uint64_t)lane * 16;
+    uint32_t m = 0;
+    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), pat) & clip16(pa, from, end);
+    const uint64_t bal = __ballot(m != 0u);
+    if (bal) {
+      const int l = (int)__builtin_ctzll(bal);
+      const uint64_t p = pa + (m ? (uint64_t)__builtin_ctz(m) : 0ull);
+      found = true;
+      return readlane64(p, l);
+    }
+  }
+  found = false;
+  return 0;
+}
+
+struct ResolveArgs {
+  const uint8_t* base;
+  uint64_t shift, obj_base, buf_end, obj_size;   // buf_end in aligned coords
+  int at_obj_end;
+  const uint64_t* chunk_hi;
+  uint64_t nchunks;
+  long long* pending;
+  void* out;
+  uint64_t cap;
+  int out_u64;
+  uint32_t* err;
+};
+
+__global__ void __launch_bounds__(kWave) fasta_resolve_kernel(ResolveArgs R) {
+  const int lane = __lane_id();
+  for (uint64_t c = blockIdx.x; c < R.nchunks; c += gridDim.x) {
+    const long long idx = R.pending[c];
+    if (idx < 0) continue;
+    bool found;
+    const uint64_t p = wave_find(R.base, R.chunk_hi[c], R.buf_end, kNL, lane, found);
+    uint64_t val;
+    if (found) val = R.obj_base - R.shift + p + 1;
+    else if (R.at_obj_end) val = R.obj_size;
+    else continue;   // unresolved: the host extends the buffer
+    if (lane == 0) {
+      if ((uint64_t)idx < R.cap) {
+        if (R.out_u64) put<uint64_t>(R.out, 2 * (uint64_t)idx + 1, val);
+        else {
+          if (val > 0xFFFFFFFFull) atomicOr(R.err, kErrOverflow);
+          put<uint32_t>(R.out, 2 * (uint64_t)idx + 1, val);
+        }
+      }
+      R.pending[c] = -1;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kWave) find_kernel(const uint8_t* base, uint64_t from, uint64_t end, uint32_t pat,
+                                                    long long* res) {
+  bool found;
+  const uint64_t p = wave_find(base, from, end, pat, __lane_id(), found);
+  if (__lane_id() == 0) *res = found ? (long long)p : -1ll;
+}
+
+// ------------------------------------------------------------------------------------------ host side
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(expr)                                                                       \
+  do {                                                                                     \
+    hipError_t _e = (expr);                                                                \
+    if (_e != hipSuccess)                                                                  \
+      return fail(DP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));          \
+  } while (0)
+
+}  // namespace
+
+struct dp_ctx {
+  int device = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  int cus = 0;
+  int grid = 0;                       // persistent scan grid
+  // device workspace
+  unsigned long long* d_desc = nullptr;
+  uint64_t desc_cap = 0;
+  uint64_t* d_tab = nullptr;          // chunk_lo | chunk_hi | chunk_u0 | pending | ctrl
+  uint64_t tab_cap = 0;               // in u64 words
+  uint64_t* h_tab = nullptr;          // pinned mirror
+  uint64_t h_cap = 0;
+  std::vector<uint64_t> last_tab;     // last uploaded table (skip identical re-uploads)
+  uint64_t* d_tab_uploaded = nullptr;
+  // async call state
+  int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
+  uint64_t nchunks = 0, cap = 0;
+  int out_u64 = 0;
+  uint32_t every_k = 1;
+  uint64_t pend_off = 0, ctrl_off = 0;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  double ms_acc = 0.0;
+  uint64_t launches = 0;
+};
+
+namespace {
+
+int ensure_tab(dp_ctx* c, uint64_t words) {
+  if (words > c->tab_cap) {
+    if (c->d_tab) HIPCHK(hipFree(c->d_tab));
+    uint64_t cap = words + words / 2 + 64;
+    HIPCHK(hipMalloc(&c->d_tab, cap * 8));
+    c->tab_cap = cap;
+    c->last_tab.clear();
+  }
+  if (words > c->h_cap) {
+    if (c->h_tab) HIPCHK(hipHostFree(c->h_tab));
+    uint64_t cap = words + words / 2 + 64;
+    HIPCHK(hipHostMalloc(&c->h_tab, cap * 8, hipHostMallocDefault));
+    c->h_cap = cap;
+  }
+  return DP_OK;
+}
+int ensure_desc(dp_ctx* c, uint64_t n) {
+  if (n > c->desc_cap) {
+    if (c->d_desc) HIPCHK(hipFree(c->d_desc));
+    uint64_t cap = ((n + n / 4 + 1023) / 1024) * 1024;
+    HIPCHK(hipMalloc(&c->d_desc, cap * 8));
+    c->desc_cap = cap;
+  }
+  return DP_OK;
+}
+int ev_begin(dp_ctx* c, hipEvent_t* e0) {
+  if (!c->timing) return DP_OK;
+  while (c->ev_pool.size() < c->ev_used + 2) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->ev_pool.push_back(e);
+  }
+  *e0 = c->ev_pool[c->ev_used];
+  HIPCHK(hipEventRecord(*e0, c->stream));
+  return DP_OK;
+}
+int ev_end(dp_ctx* c) {
+  if (!c->timing) return DP_OK;
+  HIPCHK(hipEventRecord(c->ev_pool[c->ev_used + 1], c->stream));
+  c->ev_used += 2;
+  return DP_OK;
+}
+int harvest_events(dp_ctx* c) {
+  for (size_t i = 0; i + 1 < c->ev_used; i += 2) {
+    HIPCHK(hipEventSynchronize(c->ev_pool[i + 1]));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev_pool[i], c->ev_pool[i + 1]));
+    c->ms_acc += ms;
+    c->launches += 1;
+  }
+  c->ev_used = 0;
+  return DP_OK;
+}
+
+// Lay out the chunk table in aligned coordinates and enqueue its upload + the control-block reset.
+// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[4] (err | total | spare x2).
+int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, const uint64_t* chunks,
+                 uint64_t n, uint64_t* nunits_out) {
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  std::vector<uint64_t> tab(3 * n + 1);
+  uint64_t units = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint64_t c0 = chunks[2 * i], c1 = chunks[2 * i + 1];
+    if (c1 < c0 || c0 < buf_base || c1 > buf_base + buf_len)
+      return fail(DP_ERR_INVALID, "chunk " + std::to_string(i) + " [" + std::to_string(c0) + "," +
+                                      std::to_string(c1) + ") outside the buffer");
+    const uint64_t lo = c0 - buf_base + shift, hi = c1 - buf_base + shift;
+    tab[i] = lo;
+    tab[n + i] = hi;
+    tab[2 * n + i] = units;
+    if (hi > lo) units += (hi - (lo & ~15ull) + kUnitBytes - 1) / kUnitBytes;
+  }
+  tab[3 * n] = units;
+  const uint64_t words = 5 * n + 1 + 4;
+  int rc = ensure_tab(c, words);
+  if (rc) return rc;
+  c->pend_off = 3 * n + 1;
+  c->ctrl_off = 5 * n + 1;
+  if (tab != c->last_tab) {
+    // the pinned mirror may still feed an earlier async copy: wait for the stream before rewriting it
+    HIPCHK(hipStreamSynchronize(c->stream));
+    memcpy(c->h_tab, tab.data(), tab.size() * 8);
+    HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
+    c->last_tab.swap(tab);
+  }
+  HIPCHK(hipMemsetAsync(c->d_tab + c->pend_off, 0xFF, 2 * n * 8, c->stream));
+  HIPCHK(hipMemsetAsync(c->d_tab + c->ctrl_off, 0, 4 * 8, c->stream));
+  *nunits_out = units;
+  return DP_OK;
+}
+
+int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t units,
+                void* d_out, int out_u64, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add) {
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  ScanArgs a;
+  a.base = d_buf - shift;
+  a.shift = shift;
+  a.obj_base = buf_base;
+  a.chunk_lo = c->d_tab;
+  a.chunk_hi = c->d_tab + n;
+  a.chunk_u0 = c->d_tab + 2 * n;
+  a.nchunks = n;
+  a.nunits = units;
+  a.desc = c->d_desc;
+  a.out = d_out;
+  a.cap = cap;
+  a.out_u64 = out_u64;
+  a.delim = delim * 0x01010101u;
+  a.every_k = every_k;
+  a.emit_add = emit_add;
+  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
+  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
+  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
+  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  if (units == 0) return DP_OK;
+  int rc = ensure_desc(c, units);
+  if (rc) return rc;
+  a.desc = c->d_desc;
+  HIPCHK(hipMemsetAsync(c->d_desc, 0, ((units * 8 + 15) / 16) * 16, c->stream));
+  const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
+  hipEvent_t e0;
+  rc = ev_begin(c, &e0);
+  if (rc) return rc;
+  if (mode == kFasta)
+    hipLaunchKernelGGL(scan_kernel<kFasta>, dim3(grid), dim3(kThreads), 0, c->stream, a);
+  else
+    hipLaunchKernelGGL(scan_kernel<kDelim>, dim3(grid), dim3(kThreads), 0, c->stream, a);
+  HIPCHK(hipGetLastError());
+  return ev_end(c);
+}
+
+int check_ctx(dp_ctx* c) {
+  if (!c) return fail(DP_ERR_INVALID, "null dp_ctx");
+  HIPCHK(hipSetDevice(c->device));
+  return DP_OK;
+}
+
+int collect_ctrl(dp_ctx* c, uint64_t extra_words) {
+  // D2H of [pending (nchunks) | ctrl(4)] and wait
+  const uint64_t off = c->pend_off;
+  const uint64_t words = c->ctrl_off + 4 - off + extra_words;
+  HIPCHK(hipMemcpyAsync(c->h_tab + off, c->d_tab + off, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  int rc = harvest_events(c);
+  if (rc) return rc;
+  return DP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dp_abi_version(void) { return 1; }
+
+const char* dp_last_error(void) { return g_err.c_str(); }
+
+int dp_device_count(int* n) {
+  if (!n) return fail(DP_ERR_INVALID, "null");
+  HIPCHK(hipGetDeviceCount(n));
+  return DP_OK;
+}
+
+int dp_ctx_create(int device, dp_ctx** out) {
+  if (!out) return fail(DP_ERR_INVALID, "null out");
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(DP_ERR_INVALID, "device " + std::to_string(device) + " out of range");
+  HIPCHK(hipSetDevice(device));
+  dp_ctx* c = new dp_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete c;
+    return fail(DP_ERR_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+  }
+  c->stream = c->own;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  c->cus = prop.multiProcessorCount;
+  int occ = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, scan_kernel<kFasta>, kThreads, 0));
+  int occ2 = 0;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, scan_kernel<kDelim>, kThreads, 0));
+  if (occ2 < occ) occ = occ2;
+  // every workgroup of the persistent grid must be resident (look-back waits on lower units): stay one
+  // block per CU under the occupancy answer (it can over-report by one, MI355X_MICROARCH.md §Residency)
+  int per_cu = occ - 1;
+  const char* env = getenv("DP_BLOCKS_PER_CU");
+  if (env) per_cu = atoi(env);
+  if (per_cu > 4) per_cu = 4;
+  if (per_cu < 1) per_cu = 1;
+  c->grid = c->cus * per_cu;
+  *out = c;
+  return DP_OK;
+}
+
+int dp_ctx_destroy(dp_ctx* c) {
+  if (!c) return DP_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->d_desc) (void)hipFree(c->d_desc);
+  if (c->d_tab) (void)hipFree(c->d_tab);
+  if (c->h_tab) (void)hipHostFree(c->h_tab);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+  return DP_OK;
+}
+
+int dp_ctx_get_stream(dp_ctx* c, void** s) {
+  if (!c || !s) return fail(DP_ERR_INVALID, "null");
+  *s = (void*)c->stream;
+  return DP_OK;
+}
+
+int dp_ctx_set_stream(dp_ctx* c, void* s) {
+  if (!c) return fail(DP_ERR_INVALID, "null");
+  c->stream = s ? (hipStream_t)s : c->own;
+  return DP_OK;
+}
+
+int dp_ctx_device(dp_ctx* c, int* d) {
+  if (!c || !d) return fail(DP_ERR_INVALID, "null");
+  *d = c->device;
+  return DP_OK;
+}
+
+int dp_malloc(dp_ctx* c, uint64_t bytes, void** p) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (!p) return fail(DP_ERR_INVALID, "null");
+  HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+  return DP_OK;
+}
+
+int dp_free(dp_ctx* c, void* p) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (p) HIPCHK(hipFree(p));
+  return DP_OK;
+}
+
+int dp_host_alloc(uint64_t bytes, void** p) {
+  if (!p) return fail(DP_ERR_INVALID, "null");
+  HIPCHK(hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocDefault));
+  return DP_OK;
+}
+
+int dp_host_free(void* p) {
+  if (p) HIPCHK(hipHostFree(p));
+  return DP_OK;
+}
+
+int dp_h2d(dp_ctx* c, void* dst, const void* src, uint64_t n) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, c->stream));
+  return DP_OK;
+}
+
+int dp_d2h(dp_ctx* c, void* dst, const void* src, uint64_t n) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (n) HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream));
+  return DP_OK;
+}
+
+int dp_sync(dp_ctx* c) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return DP_OK;
+}
+
+int dp_fasta_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t obj_size,
+                         const uint64_t* chunks, uint64_t nchunks, void* d_out, int out_u64, uint64_t cap_pairs) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is already in flight on this ctx");
+  if (nchunks && (!d_buf || !chunks)) return fail(DP_ERR_INVALID, "null buffer/chunks");
+  if (cap_pairs && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
+  if (buf_base + buf_len > obj_size) return fail(DP_ERR_INVALID, "buffer extends beyond the object");
+  uint64_t units = 0;
+  rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units);
+  if (rc) return rc;
+  rc = launch_scan(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0);
+  if (rc) return rc;
+  if (nchunks) {
+    const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+    ResolveArgs r;
+    r.base = d_buf - shift;
+    r.shift = shift;
+    r.obj_base = buf_base;
+    r.buf_end = shift + buf_len;
+    r.obj_size = obj_size;
+    r.at_obj_end = (buf_base + buf_len == obj_size);
+    r.chunk_hi = c->d_tab + nchunks;
+    r.nchunks = nchunks;
+    r.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
+    r.out = d_out;
+    r.cap = cap_pairs;
+    r.out_u64 = out_u64;
+    r.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
+    const unsigned g = (unsigned)(nchunks < 4096 ? nchunks : 4096);
+    hipLaunchKernelGGL(fasta_resolve_kernel, dim3(g), dim3(kWave), 0, c->stream, r);
+    HIPCHK(hipGetLastError());
+  }
+  c->inflight = kFasta;
+  c->nchunks = nchunks;
+  c->cap = cap_pairs;
+  c->out_u64 = out_u64;
+  return DP_OK;
+}
+
+int dp_fasta_result(dp_ctx* c, uint64_t* n_pairs, int64_t* pending, uint64_t* chunk_end) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (c->inflight != kFasta) return fail(DP_ERR_INVALID, "no FASTA scan in flight on this ctx");
+  c->inflight = -1;
+  rc = collect_ctrl(c, 0);
+  if (rc) return rc;
+  const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
+  const uint64_t total = c->nchunks ? c->h_tab[c->ctrl_off + 1] : 0;
+  if (n_pairs) *n_pairs = total;
+  if (pending) memcpy(pending, c->h_tab + c->pend_off, c->nchunks * 8);
+  if (chunk_end) {
+    // empty chunks were never visited: carry the previous chunk's end
+    uint64_t prev = 0;
+    for (uint64_t i = 0; i < c->nchunks; ++i) {
+      uint64_t e = c->h_tab[c->pend_off + c->nchunks + i];
+      if (e == ~0ull) e = prev;
+      chunk_end[i] = e;
+      prev = e;
+    }
+  }
+  if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out (grid not co-resident?)");
+  if (err & kErrOverflow) return fail(DP_ERR_OVERFLOW, "Python integer out of bounds for uint32");
+  if (total > c->cap) return fail(DP_ERR_CAPACITY, "output capacity " + std::to_string(c->cap) + " < " +
+                                                       std::to_string(total) + " pairs");
+  return DP_OK;
+}
+
+int dp_fasta_index(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t obj_size,
+                   const uint64_t* chunks, uint64_t nchunks, void* d_out, int out_u64, uint64_t cap_pairs,
+                   uint64_t* n_pairs, int64_t* pending, uint64_t* chunk_end) {
+  int rc = dp_fasta_index_async(c, d_buf, buf_len, buf_base, obj_size, chunks, nchunks, d_out, out_u64, cap_pairs);
+  if (rc) return rc;
+  return dp_fasta_result(c, n_pairs, pending, chunk_end);
+}
+
+int dp_delim_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin,
+                         uint64_t end, uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out,
+                         int out_u64, uint64_t cap) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is already in flight on this ctx");
+  if (every_k == 0) return fail(DP_ERR_INVALID, "every_k must be >= 1");
+  if (delim > 255) return fail(DP_ERR_INVALID, "delim must be a byte");
+  if (end > begin && !d_buf) return fail(DP_ERR_INVALID, "null buffer");
+  if (cap && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
+  const uint64_t ch[2] = {begin, end};
+  uint64_t units = 0;
+  rc = stage_chunks(c, d_buf, buf_len, buf_base, ch, 1, &units);
+  if (rc) return rc;
+  rc = launch_scan(c, kDelim, d_buf, buf_base, 1, units, d_out, out_u64, cap, delim, every_k, emit_add);
+  if (rc) return rc;
+  c->inflight = kDelim;
+  c->nchunks = 1;
+  c->cap = cap;
+  c->out_u64 = out_u64;
+  c->every_k = every_k;
+  return DP_OK;
+}
+
+int dp_delim_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (c->inflight != kDelim) return fail(DP_ERR_INVALID, "no delimiter scan in flight on this ctx");
+  const uint64_t k = c->every_k;
+  c->inflight = -1;
+  rc = collect_ctrl(c, 0);
+  if (rc) return rc;
+  const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
+  const uint64_t nd = c->h_tab[c->ctrl_off + 1];
+  const uint64_t nout = k ? nd / k : 0;
+  if (n_delims) *n_delims = nd;
+  if (n_out) *n_out = nout;
+  if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out (grid not co-resident?)");
+  if (err & kErrOverflow) return fail(DP_ERR_OVERFLOW, "Python integer out of bounds for uint32");
+  if (nout > c->cap) return fail(DP_ERR_CAPACITY, "output capacity " + std::to_string(c->cap) + " < " +
+                                                      std::to_string(nout) + " offsets");
+  return DP_OK;
+}
+
+int dp_delim_index(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin, uint64_t end,
+                   uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out, int out_u64, uint64_t cap,
+                   uint64_t* n_out, uint64_t* n_delims) {
+  int rc = dp_delim_index_async(c, d_buf, buf_len, buf_base, begin, end, delim, every_k, emit_add, d_out, out_u64, cap);
+  if (rc) return rc;
+  return dp_delim_result(c, n_out, n_delims);
+}
+
+int dp_find_delim(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t from, uint32_t delim,
+                  int64_t* pos) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  if (!pos) return fail(DP_ERR_INVALID, "null pos");
+  if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is already in flight on this ctx");
+  if (delim > 255) return fail(DP_ERR_INVALID, "delim must be a byte");
+  if (from < buf_base) return fail(DP_ERR_INVALID, "from < buffer base");
+  *pos = -1;
+  if (from >= buf_base + buf_len) return DP_OK;
+  rc = ensure_tab(c, 8);
+  if (rc) return rc;
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  long long* d_res = reinterpret_cast<long long*>(c->d_tab);
+  c->last_tab.clear();   // the table area is reused as scratch here
+  hipLaunchKernelGGL(find_kernel, dim3(1), dim3(kWave), 0, c->stream, d_buf - shift, from - buf_base + shift,
+                     shift + buf_len, delim * 0x01010101u, d_res);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(c->h_tab, c->d_tab, 8, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const long long r = (long long)c->h_tab[0];
+  *pos = r < 0 ? -1 : (int64_t)(r - (long long)shift + (long long)buf_base);
+  return DP_OK;
+}
+
+int dp_timing_enable(dp_ctx* c, int enable) {
+  if (!c) return fail(DP_ERR_INVALID, "null");
+  c->timing = enable != 0;
+  return DP_OK;
+}
+
+int dp_timing_read(dp_ctx* c, double* total_ms, uint64_t* launches) {
+  int rc = check_ctx(c);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  rc = harvest_events(c);
+  if (rc) return rc;
+  if (total_ms) *total_ms = c->ms_acc;
+  if (launches) *launches = c->launches;
+  c->ms_acc = 0.0;
+  c->launches = 0;
+  return DP_OK;
+}
+
+int dp_scan_geometry(dp_ctx* c, int* grid, int* unit_bytes) {
+  if (!c) return fail(DP_ERR_INVALID, "null");
+  if (grid) *grid = c->grid;
+  if (unit_bytes) *unit_bytes = kUnitBytes;
+  return DP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,249 @@
+"""Device-side scan contexts: one ``dp_ctx`` (device + HIP stream + workspace) per host thread per GPU.
+
+This is the only Python module that talks to libdpscan.so.  Buffers handed to the kernels are device
+pointers (ints): either the context's own grow-only staging buffers (``*_host`` helpers upload Python
+bytes / numpy arrays), or caller-owned device memory (e.g. a torch tensor's ``data_ptr()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import DPCapacityError, check
+
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+_I64P = ctypes.POINTER(ctypes.c_int64)
+
+
+def _host_ptr(data) -> Tuple[int, int, object]:
+    """(address, nbytes, keepalive) of a bytes-like / numpy object without copying."""
+    if isinstance(data, np.ndarray):
+        a = np.ascontiguousarray(data).view(np.uint8).reshape(-1)
+    else:
+        a = np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+    return a.ctypes.data, a.nbytes, a
+
+
+class DeviceBuffer:
+    """Device memory owned through the C ABI (freed with the context)."""
+
+    def __init__(self, ctx: "ScanContext", nbytes: int):
+        self.ctx = ctx
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(_lib.load().dp_malloc(ctx.handle, max(16, self.nbytes), ctypes.byref(p)))
+        self.ptr = int(p.value)
+
+    def free(self):
+        if self.ptr and self.ctx.handle:
+            check(_lib.load().dp_free(self.ctx.handle, ctypes.c_void_p(self.ptr)))
+        self.ptr = 0
+
+
+class ScanContext:
+    """A ``dp_ctx``: device, stream and scan workspace.  Not shared between threads."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(self.lib.dp_ctx_create(int(device), ctypes.byref(h)))
+        self.handle = h
+        self.device = int(device)
+        self._bufs = {}
+
+    # ---------------------------------------------------------------- memory
+    def workspace(self, name: str, nbytes: int) -> DeviceBuffer:
+        """Grow-only named device buffer."""
+        b = self._bufs.get(name)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+            b = DeviceBuffer(self, max(int(nbytes), 1 << 16))
+            self._bufs[name] = b
+        return b
+
+    def h2d(self, dst: int, data, nbytes: Optional[int] = None) -> None:
+        ptr, n, keep = _host_ptr(data)
+        n = n if nbytes is None else nbytes
+        check(self.lib.dp_h2d(self.handle, ctypes.c_void_p(dst), ctypes.c_void_p(ptr), n))
+        check(self.lib.dp_sync(self.handle))   # pageable source: keep it alive until the copy is done
+        del keep
+
+    def d2h(self, out: np.ndarray, src: int) -> np.ndarray:
+        if out.nbytes:
+            check(self.lib.dp_d2h(self.handle, ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(src), out.nbytes))
+            check(self.lib.dp_sync(self.handle))
+        return out
+
+    def upload(self, data, name: str = "input") -> Tuple[int, int]:
+        """Copy host bytes into the named staging buffer; returns (device pointer, nbytes)."""
+        _, n, _ = _host_ptr(data)
+        buf = self.workspace(name, n + 16)
+        self.h2d(buf.ptr, data)
+        return buf.ptr, n
+
+    def sync(self) -> None:
+        check(self.lib.dp_sync(self.handle))
+
+    @property
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        check(self.lib.dp_ctx_get_stream(self.handle, ctypes.byref(s)))
+        return int(s.value or 0)
+
+    def set_stream(self, stream: Optional[int]) -> None:
+        check(self.lib.dp_ctx_set_stream(self.handle, ctypes.c_void_p(stream or 0)))
+
+    # ---------------------------------------------------------------- FASTA
+    def fasta_index(self, d_buf: int, buf_len: int, buf_base: int, obj_size: int,
+                    chunks: Sequence[Tuple[int, int]], u64: bool = False, cap: Optional[int] = None):
+        """FASTA (start, end) pairs of a chunk plan over device bytes (dp_fasta_index).
+
+        Returns (pairs (n, 2) uint32|uint64, pending (nchunks,) int64, chunk_end (nchunks,) uint64).
+        """
+        ch = np.ascontiguousarray(np.asarray(chunks, dtype=np.uint64).reshape(-1))
+        nch = len(ch) // 2
+        dtype = np.uint64 if u64 else np.uint32
+        if cap is None:
+            cap = buf_len // 512 + 1024
+        pending = np.full(nch, -1, np.int64)
+        cend = np.zeros(nch, np.uint64)
+        n = ctypes.c_uint64(0)
+        while True:
+            out = self.workspace("out", 2 * cap * np.dtype(dtype).itemsize + 16)
+            rc = self.lib.dp_fasta_index(self.handle, ctypes.c_void_p(d_buf), buf_len, buf_base, obj_size,
+                                         ch.ctypes.data_as(_U64P), nch, ctypes.c_void_p(out.ptr), int(u64), cap,
+                                         ctypes.byref(n), pending.ctypes.data_as(_I64P), cend.ctypes.data_as(_U64P))
+            if rc == _lib.DP_ERR_CAPACITY:
+                cap = int(n.value)
+                continue
+            check(rc)
+            break
+        pairs = self.d2h(np.empty((int(n.value), 2), dtype), out.ptr)
+        return pairs, pending, cend
+
+    def fasta_index_async(self, d_buf, buf_len, buf_base, obj_size, chunks_u64: np.ndarray, d_out: int,
+                          u64: bool, cap: int) -> None:
+        check(self.lib.dp_fasta_index_async(self.handle, ctypes.c_void_p(d_buf), buf_len, buf_base, obj_size,
+                                            chunks_u64.ctypes.data_as(_U64P), len(chunks_u64) // 2,
+                                            ctypes.c_void_p(d_out), int(u64), cap))
+
+    def fasta_result(self, nchunks: int):
+        n = ctypes.c_uint64(0)
+        pending = np.full(nchunks, -1, np.int64)
+        cend = np.zeros(nchunks, np.uint64)
+        check(self.lib.dp_fasta_result(self.handle, ctypes.byref(n), pending.ctypes.data_as(_I64P),
+                                       cend.ctypes.data_as(_U64P)))
+        return int(n.value), pending, cend
+
+    # ---------------------------------------------------------------- delimiters
+    def delim_index(self, d_buf: int, buf_len: int, buf_base: int, begin: int, end: int, delim: int = 10,
+                    every_k: int = 1, emit_add: int = 0, u64: bool = True, cap: Optional[int] = None):
+        """Sorted offsets of every ``every_k``-th ``delim`` in object bytes [begin, end) (dp_delim_index).
+
+        Returns (offsets uint64|uint32, number of delimiters seen)."""
+        dtype = np.uint64 if u64 else np.uint32
+        if cap is None:
+            cap = (end - begin) // (16 * every_k) + 1024
+        n = ctypes.c_uint64(0)
+        nd = ctypes.c_uint64(0)
+        while True:
+            out = self.workspace("out", cap * np.dtype(dtype).itemsize + 16)
+            rc = self.lib.dp_delim_index(self.handle, ctypes.c_void_p(d_buf), buf_len, buf_base, begin, end,
+                                         int(delim), int(every_k), int(emit_add), ctypes.c_void_p(out.ptr),
+                                         int(u64), cap, ctypes.byref(n), ctypes.byref(nd))
+            if rc == _lib.DP_ERR_CAPACITY:
+                cap = int(n.value)
+                continue
+            check(rc)
+            break
+        return self.d2h(np.empty(int(n.value), dtype), out.ptr), int(nd.value)
+
+    def delim_index_async(self, d_buf, buf_len, buf_base, begin, end, delim, every_k, emit_add, d_out, u64, cap):
+        check(self.lib.dp_delim_index_async(self.handle, ctypes.c_void_p(d_buf), buf_len, buf_base, begin, end,
+                                            int(delim), int(every_k), int(emit_add), ctypes.c_void_p(d_out),
+                                            int(u64), cap))
+
+    def delim_result(self):
+        n = ctypes.c_uint64(0)
+        nd = ctypes.c_uint64(0)
+        check(self.lib.dp_delim_result(self.handle, ctypes.byref(n), ctypes.byref(nd)))
+        return int(n.value), int(nd.value)
+
+    def find_delim(self, d_buf: int, buf_len: int, buf_base: int, start: int, delim: int = 10) -> int:
+        """First object offset >= start holding ``delim`` in the buffer, or -1."""
+        pos = ctypes.c_int64(-1)
+        check(self.lib.dp_find_delim(self.handle, ctypes.c_void_p(d_buf), buf_len, buf_base, start, int(delim),
+                                     ctypes.byref(pos)))
+        return int(pos.value)
+
+    # ---------------------------------------------------------------- host-buffer conveniences
+    def fasta_index_host(self, data, buf_base: int, obj_size: int, chunks, u64: bool = False):
+        ptr, n = self.upload(data)
+        return self.fasta_index(ptr, n, buf_base, obj_size, chunks, u64=u64)
+
+    def delim_index_host(self, data, buf_base: int, begin: int, end: int, **kw):
+        ptr, n = self.upload(data)
+        return self.delim_index(ptr, n, buf_base, begin, end, **kw)
+
+    def find_delim_host(self, data, buf_base: int, start: int, delim: int = 10) -> int:
+        ptr, n = self.upload(data, name="halo")
+        return self.find_delim(ptr, n, buf_base, start, delim)
+
+    # ---------------------------------------------------------------- timing / geometry
+    def timing(self, enable: bool) -> None:
+        check(self.lib.dp_timing_enable(self.handle, int(bool(enable))))
+
+    def timing_read(self) -> Tuple[float, int]:
+        ms = ctypes.c_double(0.0)
+        n = ctypes.c_uint64(0)
+        check(self.lib.dp_timing_read(self.handle, ctypes.byref(ms), ctypes.byref(n)))
+        return float(ms.value), int(n.value)
+
+    def geometry(self) -> Tuple[int, int]:
+        g = ctypes.c_int(0)
+        u = ctypes.c_int(0)
+        check(self.lib.dp_scan_geometry(self.handle, ctypes.byref(g), ctypes.byref(u)))
+        return int(g.value), int(u.value)
+
+    def close(self) -> None:
+        if self.handle:
+            for b in self._bufs.values():
+                b.free()
+            self._bufs.clear()
+            check(self.lib.dp_ctx_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def device_count() -> int:
+    return _lib.device_count()
+
+
+def get_context(device: int = 0) -> ScanContext:
+    """The calling thread's context for ``device`` (created on first use)."""
+    ctxs = getattr(_tls, "ctxs", None)
+    if ctxs is None:
+        ctxs = _tls.ctxs = {}
+    c = ctxs.get(device)
+    if c is None:
+        c = ctxs[device] = ScanContext(device)
+    return c
+
+
+def pick_device(i: int, devices: Optional[Iterable[int]] = None) -> int:
+    """Round-robin device for job ``i`` over ``devices`` (default: every visible GPU)."""
+    devs = list(devices) if devices is not None else list(range(max(1, device_count())))
+    return devs[i % len(devs)]

@@ -1,0 +1,113 @@
+/*
+ * dpscan.h — C ABI of libdpscan.so, the MI355X (gfx950) record-boundary scan behind dataplug_amd.
+ *
+ * Every entry point is a plain C function over raw pointers and sizes (no torch / HIP types in the
+ * signatures; streams are opaque `void*` = hipStream_t).  Status is returned as an int (DP_OK = 0);
+ * the message of the last failure on the calling thread is available from dp_last_error().  No C++
+ * exception crosses this boundary.  A dp_ctx is bound to one device and owns one stream plus the
+ * scan workspace; use one ctx per host thread (calls on distinct ctx are thread-safe, and ctypes
+ * releases the GIL around them).
+ *
+ * Reference interfaces each entry point replaces (CLOUDLAB-URV/dataplug @ 2025-07-11):
+ *   dp_fasta_index  <- dataplug/formats/genomics/fasta.py:24-63 (preprocess_fasta: the per-chunk
+ *                      re.finditer(rb">.+(\n)?") scan at :36, the (start,end) pairs at :39-43, the
+ *                      split-header end fix-up at :45-56 and the uint32 packing at :61-62), run for a
+ *                      whole chunk plan at once (preprocessing/preprocess.py:38 + handler.py:36-38).
+ *   dp_delim_index  <- the newline boundaries resolved byte-by-byte in CSVSlice.get / VCFSlice.get
+ *                      (formats/generic/csv.py:52-105, formats/genomics/vcf.py:88-149) and the line
+ *                      counting gztool does for GZipText/FASTQGZip (formats/compressed/gzipped.py:46-153,
+ *                      formats/genomics/fastq.py:19-48), as one sorted offset index (every_k = 4 with
+ *                      emit_add = 1 gives FASTQ read end offsets).
+ *   dp_find_delim   <- the seek()+readline() that finds the end of a header line cut by a chunk end
+ *                      (fasta.py:45-56) — used to resolve ends beyond the bytes a call was given.
+ */
+#ifndef DPSCAN_H
+#define DPSCAN_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DP_OK 0
+#define DP_ERR_INVALID 1   /* bad argument */
+#define DP_ERR_HIP 2       /* a HIP runtime call failed (message in dp_last_error) */
+#define DP_ERR_CAPACITY 3  /* output capacity too small; the required count is still returned */
+#define DP_ERR_OVERFLOW 4  /* a uint32 offset would be >= 2^32 (the reference raises OverflowError) */
+#define DP_ERR_TIMEOUT 5   /* an inter-workgroup wait hit its bound (kernel terminated, results invalid) */
+
+typedef struct dp_ctx dp_ctx;
+
+int dp_abi_version(void);                                  /* returns the ABI version number */
+const char* dp_last_error(void);                           /* thread-local message of the last failure */
+int dp_device_count(int* n);
+int dp_ctx_create(int device, dp_ctx** out);               /* binds `device`, creates a non-blocking stream */
+int dp_ctx_destroy(dp_ctx* ctx);
+int dp_ctx_get_stream(dp_ctx* ctx, void** stream);
+int dp_ctx_set_stream(dp_ctx* ctx, void* stream);          /* NULL restores the ctx's own stream */
+int dp_ctx_device(dp_ctx* ctx, int* device);
+
+int dp_malloc(dp_ctx* ctx, uint64_t bytes, void** dptr);   /* device memory on the ctx's device */
+int dp_free(dp_ctx* ctx, void* dptr);
+int dp_host_alloc(uint64_t bytes, void** hptr);            /* pinned host memory */
+int dp_host_free(void* hptr);
+int dp_h2d(dp_ctx* ctx, void* dst, const void* src, uint64_t n);   /* async on the ctx stream */
+int dp_d2h(dp_ctx* ctx, void* dst, const void* src, uint64_t n);   /* async on the ctx stream */
+int dp_sync(dp_ctx* ctx);                                           /* waits for the ctx stream */
+
+/*
+ * FASTA header index (fasta.py:24-74 semantics, bit-exact).
+ *   d_buf[0 .. buf_len) holds object bytes [buf_base, buf_base + buf_len); obj_size is the object size.
+ *   chunks[2*i], chunks[2*i+1] = [c0, c1) of chunk i in OBJECT offsets (the reference chunk plan, which
+ *   may overlap); every chunk must lie inside the buffer.  Per chunk, a '>' at p is a header start iff
+ *   p+1 < c1, d[p+1] != '\n' and no earlier '>' lies on the same line inside the chunk; its end is
+ *   1 + the first '\n' at or after p in the whole object, or obj_size if there is none.
+ *   d_out receives interleaved (start, end) pairs in chunk order, as uint32 (out_u64 = 0, the reference
+ *   format) or uint64; at most cap_pairs pairs are written, *n_pairs is the full count.
+ *   pending (host array of nchunks, may be NULL): -1, or the pair index whose end lies beyond the
+ *   buffer end (buf_base + buf_len < obj_size); resolve those with dp_find_delim on later bytes.
+ *   chunk_end (host array of nchunks, may be NULL): pairs emitted up to and including chunk i, so chunk
+ *   i owns pairs [chunk_end[i-1], chunk_end[i]) — the per-chunk split merge_fasta_metadata concatenates.
+ *   Returns DP_ERR_OVERFLOW when out_u64 = 0 and an offset is >= 2^32.
+ */
+int dp_fasta_index(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t obj_size,
+                   const uint64_t* chunks, uint64_t nchunks, void* d_out, int out_u64, uint64_t cap_pairs,
+                   uint64_t* n_pairs, int64_t* pending, uint64_t* chunk_end);
+/* Same, enqueued without waiting; complete with dp_fasta_result (at most one call in flight per ctx). */
+int dp_fasta_index_async(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base,
+                         uint64_t obj_size, const uint64_t* chunks, uint64_t nchunks, void* d_out, int out_u64,
+                         uint64_t cap_pairs);
+int dp_fasta_result(dp_ctx* ctx, uint64_t* n_pairs, int64_t* pending, uint64_t* chunk_end);
+
+/*
+ * Delimiter offset index over object bytes [begin, end) (object offsets, inside the buffer).
+ *   Counting every byte == delim as g = 0, 1, 2, ... in order, the entries with g % every_k == every_k-1
+ *   are written as d_out[g / every_k] = offset + emit_add (uint32 if out_u64 = 0 else uint64).
+ *   every_k = 1, emit_add = 0: the '\n' offsets of a CSV/VCF body.  every_k = 4, emit_add = 1: FASTQ
+ *   read end offsets.  *n_out = entries (full count even beyond cap), *n_delims = delimiters seen.
+ */
+int dp_delim_index(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin,
+                   uint64_t end, uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out, int out_u64,
+                   uint64_t cap, uint64_t* n_out, uint64_t* n_delims);
+int dp_delim_index_async(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin,
+                         uint64_t end, uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out,
+                         int out_u64, uint64_t cap);
+int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
+
+/* First object offset >= from holding `delim` in the buffer, or -1 (seek+readline of fasta.py:45-56). */
+int dp_find_delim(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t from,
+                  uint32_t delim, int64_t* pos);
+
+/* Kernel timing: HIP events around every scan-kernel launch on the ctx stream (off by default). */
+int dp_timing_enable(dp_ctx* ctx, int enable);
+int dp_timing_read(dp_ctx* ctx, double* total_ms, uint64_t* launches);   /* syncs; then resets */
+
+/* Launch geometry (for tests/tuning): workgroups of the persistent scan grid, and unit size in bytes. */
+int dp_scan_geometry(dp_ctx* ctx, int* grid, int* unit_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DPSCAN_H */

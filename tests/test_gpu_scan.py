@@ -1,0 +1,160 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the reference's golden vectors and the oracle.
+
+Bit-exact for every case (integer/byte work).  Sizes here finish in seconds; the BASELINE-size cases
+(4 GiB FASTA, GiB-scale CSV) are in test_gpu_full_size.py.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from dataplug_amd import synth
+from oracle import cpu_ref, dpref
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_pairs(ctx, obj: np.ndarray, chunks, u64=False, offset=0):
+    """Upload ``obj`` (optionally at a misaligned device address) and index the chunk plan."""
+    buf = ctx.workspace("t_in", len(obj) + 64)
+    ctx.h2d(buf.ptr + offset, obj)
+    pairs, pending, cend = ctx.fasta_index(buf.ptr + offset, len(obj), 0, len(obj), chunks, u64=u64)
+    assert (pending == -1).all()
+    return pairs, cend
+
+
+def test_golden_fuzz_and_sample(ctx, fasta_cases):
+    z = fasta_cases
+    bad = []
+    for i in range(len(z["chunk_size"])):
+        obj = z["data"][z["data_off"][i]:z["data_off"][i + 1]]
+        exp = z["expected"][z["expected_off"][i]:z["expected_off"][i + 1]]
+        plan = cpu_ref.chunk_plan(len(obj), int(z["chunk_size"][i]))
+        pairs, cend = _gpu_pairs(ctx, obj, plan, offset=i % 16)
+        if not np.array_equal(pairs.reshape(-1), exp) or len(pairs) != z["num_sequences"][i]:
+            bad.append(i)
+    assert not bad, f"{len(bad)} mismatching golden cases, first {bad[:5]}"
+
+
+def test_golden_synthetic(ctx, fasta_cases):
+    z = fasta_cases
+    off = z["syn_index_off"]
+    for j in range(len(z["syn_seed"])):
+        a = synth.fasta(int(z["syn_size"][j]), int(z["syn_seed"][j]))
+        assert synth.sha256(a) == z["syn_sha256"][j]
+        pairs, _ = _gpu_pairs(ctx, a, cpu_ref.chunk_plan(len(a), int(z["syn_chunk_size"][j])))
+        np.testing.assert_array_equal(pairs.reshape(-1), z["syn_index"][off[j]:off[j + 1]])
+
+
+def _adversarial(kind: str, size: int, seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    if kind == "random":
+        return rng.integers(0, 256, size, dtype=np.uint8)
+    if kind == "long_lines":      # lines far longer than a 32 KiB unit, sparse '>'
+        a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size)]
+        a[rng.integers(0, size, 40)] = 10
+        a[rng.integers(0, size, 400)] = 62
+        return a
+    if kind == "no_newline":
+        a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size)]
+        a[rng.integers(0, size, 300)] = 62
+        return a
+    if kind == "dense":           # '>' and '\n' everywhere (up to 6 headers per 16 bytes)
+        return np.frombuffer(b">\nA", np.uint8)[rng.integers(0, 3, size)]
+    if kind == "all_gt":
+        return np.full(size, 62, np.uint8)
+    if kind == "all_nl":
+        return np.full(size, 10, np.uint8)
+    raise KeyError(kind)
+
+
+@pytest.mark.parametrize("kind", ["random", "long_lines", "no_newline", "dense", "all_gt", "all_nl"])
+@pytest.mark.parametrize("div", [1, 3, 64, 1000])
+def test_adversarial_vs_oracle(ctx, kind, div):
+    a = _adversarial(kind, 3_000_017, 7)
+    plan = cpu_ref.chunk_plan(len(a), math.ceil(len(a) / div))
+    exp = dpref.fasta_pairs(a, plan)
+    pairs, cend = _gpu_pairs(ctx, a, plan, u64=True, offset=5)
+    np.testing.assert_array_equal(pairs, exp)
+    # per-chunk split == per-chunk reference partials
+    k = 0
+    for i, (c0, c1) in enumerate(plan):
+        n = len(dpref.fasta_pairs(a, [(c0, c1)]))
+        k += n
+        assert int(cend[i]) == k
+
+
+@pytest.mark.parametrize("size,seed", [(64 << 20, 1), ((48 << 20) + 12345, 2)])
+@pytest.mark.parametrize("div", [1, 4, 7, 64])
+def test_synthetic_fasta_vs_oracle(ctx, size, seed, div):
+    a = synth.fasta(size, seed)
+    plan = cpu_ref.chunk_plan(len(a), math.ceil(len(a) / div))
+    exp = dpref.fasta_pairs(a, plan)
+    pairs, _ = _gpu_pairs(ctx, a, plan)
+    np.testing.assert_array_equal(pairs.astype(np.uint64), exp)
+
+
+def test_quirk_chunk_size_eq_num_chunks_minus_one(ctx):
+    a = synth.fasta(12 * 1024 + 3, 9)
+    size = len(a)
+    cs = next(c for c in range(1, size) if size // c == c + 1)
+    plan = cpu_ref.chunk_plan(size, cs)
+    assert all(c1 == size for _, c1 in plan)          # every chunk reads to EOF: duplicates
+    exp = np.frombuffer(cpu_ref.fasta_index(bytes(a), cs)[0], np.uint32)
+    pairs, _ = _gpu_pairs(ctx, a, plan)
+    np.testing.assert_array_equal(pairs.reshape(-1), exp)
+
+
+def test_uint32_overflow_raises_like_reference(ctx):
+    # a window of an object that straddles 2**32: the reference's np.array(..., uint32) raises
+    a = synth.fasta(1 << 20, 3)
+    base = (1 << 32) - (1 << 19)
+    buf = ctx.workspace("t_in", len(a) + 64)
+    ctx.h2d(buf.ptr, a)
+    with pytest.raises(OverflowError):
+        ctx.fasta_index(buf.ptr, len(a), base, base + len(a), [(base, base + len(a))], u64=False)
+    pairs, _, _ = ctx.fasta_index(buf.ptr, len(a), base, base + len(a), [(base, base + len(a))], u64=True)
+    exp = dpref.fasta_pairs(a, [(0, len(a))]) + np.uint64(base)
+    np.testing.assert_array_equal(pairs, exp)
+
+
+def test_pending_end_beyond_buffer(ctx):
+    # the chunk ends inside a header line and the buffer stops there too: the end is reported pending
+    a = np.frombuffer(b"ACGT\n>seq1 a long header line\nACGT\n", np.uint8)
+    cut = 10
+    buf = ctx.workspace("t_in", 64)
+    ctx.h2d(buf.ptr, a[:cut])
+    pairs, pending, _ = ctx.fasta_index(buf.ptr, cut, 0, len(a), [(0, cut)])
+    assert pairs.shape == (1, 2) and pairs[0, 0] == 5 and pending[0] == 0
+    halo = a[cut:]
+    pos = ctx.find_delim_host(halo, cut, cut)
+    assert pos == 29
+    # same object, whole buffer: resolved on device
+    pairs, _ = _gpu_pairs(ctx, a, [(0, cut)])
+    assert pairs.tolist() == [[5, 30]]
+
+
+@pytest.mark.parametrize("k,add", [(1, 0), (4, 1), (3, 0)])
+@pytest.mark.parametrize("begin,end", [(0, None), (17, -12345)])
+def test_delim_vs_oracle(ctx, k, add, begin, end):
+    a = synth.csv((32 << 20) + 77, 4)
+    end = len(a) if end is None else len(a) + end
+    buf = ctx.workspace("t_in", len(a) + 64)
+    ctx.h2d(buf.ptr + 3, a)
+    got, nd = ctx.delim_index(buf.ptr + 3, len(a), 0, begin, end, 10, k, add, u64=True)
+    exp, end_nd = dpref.delim(a, begin, end, 10, k, add)
+    assert nd == end_nd
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_delim_fastq_reads(ctx):
+    a = synth.fastq(200_003, 5)
+    got, nd = ctx.delim_index_host(a, 0, 0, len(a), delim=10, every_k=4, emit_add=1)
+    assert nd == 4 * 200_003 and len(got) == 200_003
+    np.testing.assert_array_equal(got, cpu_ref.delim_index(a, 0, len(a), 10, 4, 1))
+
+
+def test_find_delim(ctx):
+    a = np.frombuffer(b"x" * 5000 + b"\n" + b"y" * 10, np.uint8)
+    assert ctx.find_delim_host(a, 100, 100) == 5100
+    assert ctx.find_delim_host(a, 100, 5101) == -1
