@@ -194,6 +194,10 @@ class ScanContext:
         ptr, n = self.upload(data, name="halo")
         return self.find_delim(ptr, n, buf_base, start, delim)
 
+    def stream_read(self, d_buf: int, nbytes: int, blocks_per_cu: int = 8) -> None:
+        """Calibration read of ``nbytes`` device bytes (async; time it with timing())."""
+        check(self.lib.dp_stream_read(self.handle, ctypes.c_void_p(d_buf), nbytes, blocks_per_cu))
+
     # ---------------------------------------------------------------- timing / geometry
     def timing(self, enable: bool) -> None:
         check(self.lib.dp_timing_enable(self.handle, int(bool(enable))))

@@ -100,6 +100,9 @@ int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
 int dp_find_delim(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t from,
                   uint32_t delim, int64_t* pos);
 
+/* Calibration: read `bytes` (16-byte aligned) with a plain streaming kernel (async, timed like the scans). */
+int dp_stream_read(dp_ctx* ctx, const void* d_buf, uint64_t bytes, int blocks_per_cu);
+
 /* Kernel timing: HIP events around every scan-kernel launch on the ctx stream (off by default). */
 int dp_timing_enable(dp_ctx* ctx, int enable);
 int dp_timing_read(dp_ctx* ctx, double* total_ms, uint64_t* launches);   /* syncs; then resets */

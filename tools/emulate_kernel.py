@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import numpy as np
 
-WAVE, WAVES, ROWS = 64, 4, 8
+WAVE, WAVES, ROWS = 64, 8, 8
 ROW = WAVE * 16
 WAVE_BYTES = ROW * ROWS
 UNIT = WAVE_BYTES * WAVES
@@ -114,25 +114,34 @@ def run(buf: np.ndarray, chunks, mode="fasta", delim=10, every_k=1, emit_add=0, 
             wbase = ubase + w * WAVE_BYTES
             if mode == "fasta":
                 S = nlseen = fV = 0
+                fn_off = -1
                 cnt = 0
+                mk = []
                 for r in range(ROWS):
                     row0 = wbase + r * ROW
+                    zero = (np.zeros(WAVE, np.int64), np.zeros(WAVE, np.int64))
                     if row0 >= hi:
-                        break
+                        mk.append(zero)
+                        continue
                     pos0 = row0 + LANES * 16
                     need = S or not nlseen or ballot(maybe_has(b, pos0, 62) & (pos0 < hi))
                     if not need:
+                        mk.append(zero)
                         continue
                     rend = row0 + ROW
                     nxt = int(b[rend] == 10) if rend < hi else 0
                     V, nl, emits, ends, sb, H, S_out = fasta_row(b, pos0, lo, hi, S, nxt)
                     if not nlseen and H:
-                        fV = int(sb[(H & -H).bit_length() - 1])
+                        j0 = (H & -H).bit_length() - 1
+                        fV = int(sb[j0])
+                        fn_off = r * ROW + j0 * 16 + (int(nl[j0]) & -int(nl[j0])).bit_length() - 1
                         nlseen = 1
+                    mk.append((emits.copy(), ends.copy()))
                     cnt += int(popc(emits).sum())
                     S = S_out
                 if not nlseen:
                     fV = S
+                masks.append((mk, fV, fn_off))
                 f = (cnt, cnt - fV, S, S if nlseen else 1)
                 if chunk_first and w == 0:
                     f = (f[0], f[0], f[2], f[2])
@@ -191,14 +200,19 @@ def run(buf: np.ndarray, chunks, mode="fasta", delim=10, every_k=1, emit_add=0, 
                 row0 = wbase + r * ROW
                 pos0 = row0 + LANES * 16
                 if mode == "fasta":
-                    if row0 >= hi:
-                        break
-                    need = S or ballot(maybe_has(b, pos0, 62) & (pos0 < hi))
-                    if not need:
-                        continue
-                    rend = row0 + ROW
-                    nxt = int(b[rend] == 10) if rend < hi else 0
-                    V, nl, emits, ends, sb, H, S_out = fasta_row(b, pos0, lo, hi, S, nxt)
+                    mk, fV, fn_off = masks[w]
+                    if r == 0:
+                        drop = bool(S) and bool(fV)
+                        add_end = bool(S) and fn_off >= 0
+                    emits, ends = mk[r][0].copy(), mk[r][1].copy()
+                    if add_end and fn_off // ROW == r:
+                        ends[(fn_off // 16) % 64] |= 1 << (fn_off % 16)
+                    if drop:
+                        bal = ballot(emits != 0)
+                        if bal:
+                            l0 = (bal & -bal).bit_length() - 1
+                            emits[l0] &= emits[l0] - 1
+                            drop = False
                     pc = popc(emits)
                     ex = np.concatenate(([0], np.cumsum(pc)[:-1]))
                     for l in range(WAVE):
@@ -210,7 +224,6 @@ def run(buf: np.ndarray, chunks, mode="fasta", delim=10, every_k=1, emit_add=0, 
                             if int(ends[l]) >> bit & 1:
                                 out[(count + ex[l] + below - 1, 1)] = int(pos0[l]) + bit + 1
                     count += int(pc.sum())
-                    S = S_out
                 else:
                     m = masks[w][r]
                     pc = popc(m)
