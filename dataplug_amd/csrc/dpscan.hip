@@ -6,26 +6,25 @@
 //   * scan_kernel<DELIM>: sorted offsets of a delimiter byte (CSV/VCF newline index, FASTQ read ends).
 //   * fasta_resolve_kernel / find_kernel: the "header cut by the chunk end" fix-up (fasta.py:45-56).
 //
-// Single-pass structure (memory-bound byte scan, no MFMA):
-//   * persistent grid, workgroup = 4 waves; a workgroup owns a 32 KiB "unit" per iteration (each wave a
-//     contiguous 8 KiB, 8 rows of 1 KiB = 64 lanes x 16 B global_load_dwordx4, all issued up front and
-//     kept in VGPRs).
-//   * per 16-byte lane: SWAR exact byte-match masks ('>' and '\n'), a carry trick that marks the first
-//     valid '>' of every line segment, and 64-lane ballot scans for the carried line state and the
-//     emit counts (bit-sliced ballots + mbcnt) — no LDS traffic in the row loop.
-//   * phase A computes the unit's summary as a FUNCTION of the incoming line state (count / out-state
-//     if the unit starts inside a line that already emitted a header, or not); units chain their
-//     summaries with a decoupled look-back over 8-byte {status, value} descriptors (agent-scope relaxed
-//     atomics = sc1, one store per descriptor, see cdna_hip_programming.md G16 R2); phase B replays the
-//     registers with the true prefix and writes the offsets.  Input bytes are read from HBM exactly once.
-//   * all waits on other workgroups are bounded (DP_ERR_TIMEOUT) — units are statically strided over a
-//     grid sized to be fully resident, so a unit only ever waits on lower units already running.
+// Single pass, memory-bound (no MFMA):
+//   * persistent grid, one 1024-thread workgroup per CU = 15 data waves + 1 coordinator wave; the
+//     workgroup owns the 120 KiB units u = blockIdx.x + k*G (each data wave 8 rows of 1 KiB = 64 lanes
+//     x 16 B bounds-checked buffer loads, double-buffered in VGPRs, hand-waited).
+//   * per 16-byte lane: SWAR exact byte matches packed into one interleaved 32-bit mask ('\n' at even,
+//     '>' at odd bits), a carry trick that marks the first valid '>' of every line segment, and the
+//     lane-level line state from one 64-bit carry trick on the wave's ballots (SGPRs).
+//   * phase A summarises a wave's 8 KiB as a FUNCTION of the incoming line state and parks its masks in
+//     LDS; the coordinator chains unit summaries across workgroups with a decoupled look-back over
+//     8-byte {status, value} descriptors (agent-scope relaxed atomics = sc1; cdna_hip_programming.md G16
+//     R2) and hands prefixes back through LDS flags; phase B turns masks into offsets.  Input bytes are
+//     read from HBM exactly once; data waves never wait on each other (no workgroup barrier per unit).
+//   * every wait is bounded (DP_ERR_TIMEOUT); units are statically strided over a grid of one
+//     workgroup per CU, so a unit only ever waits on lower units owned by running workgroups.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
 
-#include <mutex>
 #include <string>
 #include <vector>
 
@@ -34,16 +33,20 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kWaves = 16;                         // waves per workgroup: 15 data + 1 coordinator
-constexpr int kDataWaves = 15;
-constexpr int kCoord = 15;
-constexpr int kThreads = kWave * kWaves;
+constexpr int kDataWaves = 15;                     // + 1 coordinator wave
+constexpr int kCoord = kDataWaves;
+constexpr int kWaves = kDataWaves + 1;
+constexpr int kThreads = kWave * kWaves;           // 1024
 constexpr int kRowBytes = kWave * 16;              // one dwordx4 per lane
 constexpr int kRows = 8;                           // rows per wave per unit
 constexpr int kWaveBytes = kRowBytes * kRows;      // 8 KiB
 constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 120 KiB look-back unit
+constexpr int kRing = 4;                           // LDS ring depth (units in flight per workgroup)
+constexpr int kLag = 2;                            // resolve(j) once AGG(j + kLag) is out
+constexpr int kBLag = kLag + 1;                    // data waves run phase B(j) after phase A(j + kBLag)
 constexpr uint32_t kGT = 0x3E3E3E3Eu;              // '>'
 constexpr uint32_t kNL = 0x0A0A0A0Au;              // '\n'
+constexpr uint32_t kOdd = 0xAAAAAAAAu, kEven = 0x55555555u;
 
 constexpr uint32_t kErrTimeout = 1u;
 constexpr uint32_t kErrOverflow = 2u;
@@ -51,7 +54,7 @@ constexpr uint32_t kErrOverflow = 2u;
 constexpr uint64_t kStatAgg = 1ull << 62;
 constexpr uint64_t kStatPrefix = 2ull << 62;
 constexpr uint64_t kStatMask = 3ull << 62;
-constexpr uint32_t kSpinLimit = 1u << 22;          // x s_sleep(2) per poll: well above any legal wait
+constexpr uint32_t kSpinLimit = 1u << 22;          // polls (with s_sleep) before giving up
 
 enum Mode { kFasta = 0, kDelim = 1 };
 
@@ -59,9 +62,6 @@ struct ScanArgs {
   const uint8_t* base;         // 16-byte aligned base; coordinates below are relative to it
   uint64_t shift;              // buffer start - base (0..15)
   uint64_t obj_base;           // object offset of buffer byte 0
-  const uint64_t* chunk_lo;    // [nchunks] aligned coords
-  const uint64_t* chunk_hi;    // [nchunks]
-  const uint64_t* chunk_u0;    // [nchunks + 1] first unit of each chunk
   uint64_t nchunks;
   uint64_t nunits;
   unsigned long long* desc;    // [nunits] look-back descriptors (zeroed per launch)
@@ -72,7 +72,7 @@ struct ScanArgs {
   uint32_t every_k;
   uint32_t emit_add;
   uint32_t* err;
-  unsigned long long* total;   // [2] inclusive count of the last unit; (DELIM) number of delimiters
+  unsigned long long* total;   // inclusive count at the last unit
   long long* pending;          // FASTA: [nchunks] pair index whose end is unresolved at chunk end, or -1
   unsigned long long* chunk_end;  // [nchunks] inclusive count at the end of each (non-empty) chunk
 };
@@ -93,18 +93,32 @@ __device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t pat) {
   return pack4(eq4(v.x, pat)) | (pack4(eq4(v.y, pat)) << 4) | (pack4(eq4(v.z, pat)) << 8) |
          (pack4(eq4(v.w, pat)) << 12);
 }
+// 4 bytes -> 8 interleaved flags: bit 2j = (byte j == '\n'), bit 2j+1 = (byte j == '>').  The pairs of
+// bytes 0..2 are gathered by one mul_u32_u24 (partial products land on disjoint bits: no carries).
+__device__ __forceinline__ uint32_t pair8(uint32_t w) {
+  const uint32_t c = (eq4(w, kGT) | (eq4(w, kNL) >> 1)) >> 6;   // byte j: bit 8j = nl, 8j+1 = gt
+  const uint32_t t = (((c & 0x30303u) * 0x41041u) >> 18) & 0x3Fu;
+  return t | ((c >> 18) & 0xC0u);
+}
+__device__ __forceinline__ uint32_t pairs32(const uint4& v) {
+  return pair8(v.x) | (pair8(v.y) << 8) | (pair8(v.z) << 16) | (pair8(v.w) << 24);
+}
 __device__ __forceinline__ bool maybe_has(const uint4& v, uint32_t pat) {
   // no false negatives (classic haszero); false positives only make the exact path run
   auto hz = [](uint32_t x) { return (x - 0x01010101u) & ~x; };
   return ((hz(v.x ^ pat) | hz(v.y ^ pat) | hz(v.z ^ pat) | hz(v.w ^ pat)) & 0x80808080u) != 0;
 }
-__device__ __forceinline__ uint32_t clip16(uint64_t pos0, uint64_t lo, uint64_t hi) {
-  uint32_t m = 0xFFFFu;
-  if (pos0 < lo) m = (lo - pos0 >= 16) ? 0u : (m << (uint32_t)(lo - pos0)) & 0xFFFFu;
-  if (pos0 + 16 > hi) m = (hi <= pos0) ? 0u : m & ((1u << (uint32_t)(hi - pos0)) - 1u);
-  return m;
+// bytes [a, b) of a 16-byte lane (a, b clamped to 0..16) as 16 single / 32 paired bits
+__device__ __forceinline__ uint32_t range16(int64_t a, int64_t b) {
+  a = a < 0 ? 0 : (a > 16 ? 16 : a);
+  b = b < 0 ? 0 : (b > 16 ? 16 : b);
+  return b <= a ? 0u : ((0xFFFFu >> (16 - (b - a))) << a);
 }
-__device__ __forceinline__ uint64_t lanemask_lt(int lane) { return (1ull << lane) - 1ull; }
+__device__ __forceinline__ uint32_t range32(int64_t a, int64_t b) {
+  a = a < 0 ? 0 : (a > 16 ? 16 : a);
+  b = b < 0 ? 0 : (b > 16 ? 16 : b);
+  return b <= a ? 0u : (uint32_t)((0xFFFFFFFFull >> (32 - 2 * (b - a))) << (2 * a));
+}
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -123,6 +137,9 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& total) {
 }
 template <int BITS>
 __device__ __forceinline__ uint32_t wave_total(uint32_t c) {
+  const uint64_t any2 = __ballot(c > 1u);
+  const uint64_t any1 = __ballot(c != 0u);
+  if (!any2) return (uint32_t)__popcll(any1);        // common: at most one per lane
   uint32_t tot = 0;
 #pragma unroll
   for (int b = 0; b < BITS; ++b) tot += (uint32_t)__popcll(__ballot((c >> b) & 1u)) << b;
@@ -133,12 +150,31 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
   const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
   return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t ld_desc(unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void st_desc(unsigned long long* p, uint64_t v) {
   __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// LDS hand-offs inside the workgroup.  LDS executes one wave's operations in order, so a relaxed flag
+// written after the payload (with a compiler barrier in between) is seen after it; no global fence
+// (which would make the data waves drain their in-flight prefetch).
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_add(uint32_t* p, uint32_t v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
 // Summary of a byte range as a function of the incoming line state S (does the current line already
 // hold an emitted header?): count and outgoing state for S = false (F) and S = true (T).
@@ -162,46 +198,6 @@ __device__ __forceinline__ uint64_t pack_prefix(uint64_t count, uint32_t s) {
   return kStatPrefix | ((uint64_t)s << 48) | (count & 0xFFFFFFFFFFFFull);
 }
 
-// One 16-byte lane of a FASTA row.  Inputs: lane's bytes, clip mask, next-byte-is-'\n' for bit 15,
-// whether the chunk's last byte (p = c1-1, never a header: needs p+1 < c1) is in this lane, and the
-// wave-uniform incoming state S.  See DESIGN.md §3.2 for the derivation of the carry trick.
-struct FRow {
-  uint32_t V, nl, emits, ends;
-  uint32_t s_before_nl;   // line state just before this lane's first '\n'
-  uint64_t H;             // ballot: lanes holding a '\n'
-  uint32_t S_out;         // wave-uniform state after the row
-};
-__device__ __forceinline__ FRow fasta_row(const uint4& v, uint32_t valid, uint32_t nxt_nl, int last_bit,
-                                          uint32_t S, int lane) {
-  FRow f;
-  const uint32_t gt = mask16(v, kGT) & valid;
-  const uint32_t nl = mask16(v, kNL) & valid;
-  const uint32_t nb = (__shfl_down((int)nl, 1) & 1);
-  const uint32_t nxt = (lane == kWave - 1) ? nxt_nl : nb;
-  uint32_t V = gt & ~((nl >> 1) | (nxt << 15));      // '>' followed by a non-'\n' byte
-  if (last_bit >= 0) V &= ~(1u << last_bit);          // p + 1 < c1
-  const uint32_t X = V | nl;
-  const uint32_t R = ((~X) & 0xFFFFu) + ((nl << 1) | 1u);   // first X bit at/after each line start
-  const uint32_t low = nl & (0u - nl);
-  const uint32_t fs = low ? low - 1u : 0xFFFFu;       // bits before the lane's first '\n'
-  const uint32_t s_last = ((R >> 16) & 1u) ^ 1u;      // a valid '>' after the lane's last '\n'
-  const uint64_t H = __ballot(nl != 0u);
-  const uint64_t SB = __ballot(s_last);
-  const uint64_t lt = lanemask_lt(lane);
-  const uint64_t prior = H & lt;
-  uint32_t S_lane;
-  if (prior) S_lane = ((SB & lt) >> (63 - __clzll(prior))) != 0ull;
-  else S_lane = S || ((SB & lt) != 0ull);
-  f.V = V;
-  f.nl = nl;
-  f.emits = V & R & (S_lane ? ~fs : 0xFFFFu);
-  f.ends = nl & (~R | (S_lane ? low : 0u));
-  f.s_before_nl = S_lane || ((V & fs) != 0u);
-  f.H = H;
-  f.S_out = H ? ((SB >> (63 - __clzll(H))) != 0ull) : (S || SB != 0ull);
-  return f;
-}
-
 template <typename T>
 __device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
   reinterpret_cast<T*>(out)[i] = (T)v;
@@ -210,7 +206,7 @@ __device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
 // ------------------------------------------------------------------------------------------ look-back
 // Unit summaries in the decoupled look-back carry an "inclusive prefix" flag: a PREFIX descriptor is a
 // constant function (it already counts everything before it), so composing anything in front of it
-// yields it unchanged.  then() is associative, which lets a wave reduce a whole window in a tree.
+// yields it unchanged.  lb_then() is associative, which lets a wave reduce a whole window in a tree.
 struct LB {
   uint64_t cF, cT;
   uint32_t fl;     // bit0 sF, bit1 sT, bit2 inclusive prefix
@@ -228,8 +224,7 @@ __device__ __forceinline__ LB lb_then(const LB& a, const LB& b) {   // a (farthe
 }
 __device__ __forceinline__ LB lb_from_desc(uint64_t d) {
   const uint64_t st = d & kStatMask;
-  if (st == kStatAgg)
-    return LB{d & 0xFFFFFFull, (d >> 24) & 0xFFFFFFull, (uint32_t)(d >> 48) & 3u};
+  if (st == kStatAgg) return LB{d & 0xFFFFFFull, (d >> 24) & 0xFFFFFFull, (uint32_t)(d >> 48) & 3u};
   if (st == kStatPrefix) {
     const uint64_t c = d & 0xFFFFFFFFFFFFull;
     const uint32_t s = (uint32_t)(d >> 48) & 1u;
@@ -246,12 +241,11 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t x, int s) {
 constexpr uint64_t kIdentDesc = kStatMask;   // status 3: "no unit here" (identity, always valid)
 
 // One wave: prefix count P and line state S entering unit u.  The window is every unit between this
-// workgroup's previous unit (u - G, whose inclusive prefix the workgroup still holds in registers) and
-// u: all of them are published by workgroups that are running, so one parallel load of the window
-// (4 descriptors per lane for G <= 256) and a 6-step ordered tree reduction resolve it — no serial
-// chain of prefixes.  Spins are bounded (kErrTimeout).
-__device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t G, uint64_t baseP,
-                                         uint32_t baseS, int lane, uint64_t& P, uint32_t& S_in) {
+// workgroup's previous unit (u - G, whose inclusive prefix the coordinator holds in registers) and u,
+// all published by running workgroups: one parallel load (4 descriptors per lane for G <= 256) and a
+// 6-step ordered tree reduction resolve it — no serial chain of prefixes.  Spins are bounded.
+__device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t G, uint64_t baseP, uint32_t baseS,
+                                      int lane, uint64_t& P, uint32_t& S_in) {
   const uint64_t W = u < G - 1 ? u : G - 1;          // D[k] = desc[u-1-k] for k < W, D[W] = base prefix
   const uint64_t basedesc = pack_prefix(baseP, baseS);
   LB acc = lb_ident();
@@ -308,64 +302,52 @@ __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t
   S_in = acc.fl & 1u;
 }
 
-// ------------------------------------------------------------------------------------------ scan kernel
-// Workgroup = 15 data waves + 1 coordinator wave (1024 threads), one workgroup per CU, persistent over
-// units u = blockIdx.x + k*G (120 KiB each).  Software pipeline, ONE workgroup barrier per unit:
-//
-//   data waves   : phase A(k) -> post summary(k) -> prefetch unit k+2 -> BARRIER_k -> phase B(k-1)
-//   coordinator  :                                                      BARRIER_k -> look-back(k),
-//                                                                                    geometry of k+4
-//
-// so the coordinator's look-back of unit k (cross-XCD descriptor latency) overlaps the data waves'
-// phase B(k-1) + phase A(k+1).  Data waves only LOAD input (bounds-checked buffer loads, hand-waited)
-// and STORE offsets; all other global traffic is on the coordinator.  LDS carries geometry (4-slot
-// ring), per-wave summaries and prefixes (2 slots each).
-struct GeoL {                // one unit (wave-uniform)
-  uint64_t lo, hi;           // chunk [lo, hi) in aligned coordinates
-  uint64_t ubase;            // first byte of the unit (data wave w starts at ubase + w*kWaveBytes)
-  uint64_t c;                // chunk index
-  uint32_t first, last, valid, pad;
+// ------------------------------------------------------------------------------------------ geometry
+// Unit -> chunk lookup over the chunk table (read-only, read through the constant address space so it
+// compiles to scalar loads and never enters the vector-memory counter the data waves' hand-waited loads
+// rely on).  A cursor follows
+// the increasing units of one wave, falling back to a binary search when it would skip chunks.
+typedef __attribute__((address_space(4))) const uint64_t cu64;   // constant address space: s_load
+struct Tab {
+  cu64* lo;
+  cu64* hi;
+  cu64* u0;                          // [nchunks + 1]
 };
-
-struct Shared {
-  GeoL geo[4];
-  uint64_t cF[2][kDataWaves], cT[2][kDataWaves], P[2][kDataWaves];
-  uint32_t sF[2][kDataWaves], sT[2][kDataWaves], S[2][kDataWaves];
-  uint32_t m[2][kDataWaves][kRows][kWave];   // per lane-row masks of the unit awaiting phase B (60 KiB)
-};
-
-// Coordinator-side unit -> chunk lookup with a cursor (units of one workgroup increase), falling back to
-// a binary search when the cursor would have to skip chunks.
 struct Cursor {
-  uint64_t c, u0, u1;        // chunk c covers units [u0, u1) (valid once the first lookup happened)
+  uint64_t c, u0, u1, lo, hi;        // chunk c = [lo, hi) covers units [u0, u1)
   uint32_t valid;
 };
-__device__ __forceinline__ GeoL coord_geo(const ScanArgs& A, uint64_t u, Cursor& cur) {
-  GeoL g;
-  g.pad = 0;
-  if (u >= A.nunits) {
+struct Geo {                          // one unit (wave-uniform)
+  uint64_t lo, hi, ubase, c;
+  uint32_t first, last, valid;
+};
+__device__ __forceinline__ Geo geo_of(const Tab& T, uint64_t nchunks, uint64_t nunits, uint64_t u, Cursor& cur) {
+  Geo g;
+  if (u >= nunits) {
     g.lo = g.hi = g.ubase = g.c = 0;
     g.first = g.last = g.valid = 0;
     return g;
   }
   if (!cur.valid || u < cur.u0 || u >= cur.u1) {
-    uint64_t c = 0, cn = A.nchunks;
-    if (cur.valid && u >= cur.u1 && cur.c + 1 < A.nchunks && A.chunk_u0[cur.c + 2] > u) {
+    uint64_t c = 0, cn = nchunks;
+    if (cur.valid && u >= cur.u1 && cur.c + 1 < nchunks && T.u0[cur.c + 2] > u) {
       c = cur.c + 1;                                   // common case: the next chunk
     } else {
       while (cn - c > 1) {
         const uint64_t m = (c + cn) >> 1;
-        if (A.chunk_u0[m] <= u) c = m; else cn = m;
+        if (T.u0[m] <= u) c = m; else cn = m;
       }
     }
     cur.c = c;
-    cur.u0 = A.chunk_u0[c];
-    cur.u1 = A.chunk_u0[c + 1];
+    cur.u0 = T.u0[c];
+    cur.u1 = T.u0[c + 1];
+    cur.lo = T.lo[c];
+    cur.hi = T.hi[c];
     cur.valid = 1;
   }
   g.c = cur.c;
-  g.lo = A.chunk_lo[cur.c];
-  g.hi = A.chunk_hi[cur.c];
+  g.lo = cur.lo;
+  g.hi = cur.hi;
   g.first = (u == cur.u0);
   g.last = (u + 1 == cur.u1);
   g.valid = 1;
@@ -373,24 +355,7 @@ __device__ __forceinline__ GeoL coord_geo(const ScanArgs& A, uint64_t u, Cursor&
   return g;
 }
 
-__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((int)(uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ GeoL geo_from_lds(const GeoL& s) {   // make it provably wave-uniform
-  GeoL g;
-  g.lo = rfl64(s.lo);
-  g.hi = rfl64(s.hi);
-  g.ubase = rfl64(s.ubase);
-  g.c = rfl64(s.c);
-  g.first = __builtin_amdgcn_readfirstlane((int)s.first);
-  g.last = __builtin_amdgcn_readfirstlane((int)s.last);
-  g.valid = __builtin_amdgcn_readfirstlane((int)s.valid);
-  g.pad = 0;
-  return g;
-}
-
+// ------------------------------------------------------------------------------------------ input loads
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -404,9 +369,10 @@ struct Buf {
 // loads in flight per buffer.  Issued as inline asm: the compiler inserts no wait for them, and the
 // data waves wait with ONE explicit `s_waitcnt vmcnt(kLoadsPerBuf)` at the top of phase A (the only
 // younger vector-memory ops are the other buffer's loads plus stores, which only make it conservative).
+// tools/isa_guard.py checks the compiled code never touches a destination before that wait.
 constexpr int kLoadsPerBuf = kRows + 1;
 
-__device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const GeoL& g, int wave, int lane) {
+__device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const Geo& g, int wave, int lane) {
   const uint64_t wbase = g.valid ? g.ubase + (uint64_t)wave * kWaveBytes : 0ull;
   const uint64_t hi16 = (g.hi + 15) & ~15ull;
   uint32_t nrec = 0;
@@ -433,33 +399,105 @@ __device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const GeoL& 
 // Wait for this buffer's loads, then "redefine" every destination register: the empty asm makes each
 // value live until here (an unused destination must not be reallocated while its load is in flight)
 // and nothing that reads the data can be scheduled above the wait.
-__device__ __forceinline__ void wait_buf(Buf& b) {
-  asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsPerBuf) : "memory");
+__device__ __forceinline__ void touch_buf(Buf& b) {
   asm volatile("" : "+v"(b.x[0]), "+v"(b.x[1]), "+v"(b.x[2]), "+v"(b.x[3]), "+v"(b.x[4]), "+v"(b.x[5]),
                "+v"(b.x[6]), "+v"(b.x[7]), "+v"(b.la) :: "memory");
+}
+__device__ __forceinline__ void wait_buf(Buf& b) {
+  asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsPerBuf) : "memory");
+  touch_buf(b);
+  __builtin_amdgcn_sched_barrier(0);
+}
+// After the last step both buffers still have (unused) loads in flight: wait for them and keep their
+// destinations live until then, or the compiler reuses those VGPRs and the landing loads clobber them.
+__device__ __forceinline__ void drain_bufs(Buf& a, Buf& b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  touch_buf(a);
+  touch_buf(b);
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// What phase B of a unit needs after its registers have been reused for the next prefetch (wave-uniform;
-// the per lane-row masks themselves wait in LDS, sh.m[k & 1][wave]: FASTA emits | ends << 16, DELIM
-// delimiter bits).
+// ------------------------------------------------------------------------------------------ LDS state
+// Phase-B state of a unit (wave-uniform; the per lane-row masks wait in LDS too: FASTA interleaved
+// emits (odd bits) | ends (even bits), DELIM delimiter bits).
 struct Pend {
   uint64_t wbase;
   uint32_t rows;             // bit r: row r has a nonzero mask in some lane
   uint32_t fV;               // FASTA: first segment of the wave range held a valid '>'
-  int fn_off;                // FASTA: first '\n' of the wave range (offset in the range) or -1
+  int fn_off;                // FASTA: first '\n' of the wave range (byte offset in the range) or -1
+  uint32_t pad;
 };
 
-// Phase A of one unit on one data wave: masks + the wave's summary (as a function of the line state).
+struct Shared {
+  uint64_t cF[kRing][kDataWaves], cT[kRing][kDataWaves];   // per-wave summaries
+  uint32_t sF[kRing][kDataWaves], sT[kRing][kDataWaves];
+  uint64_t P[kRing][kDataWaves];                           // per-wave prefixes from the coordinator
+  uint32_t S[kRing][kDataWaves];
+  uint32_t done[kRing];                                    // data waves finished phase A of the slot's unit
+  uint32_t ready[kRing];                                   // = unit index + 1 once P/S of the slot are set
+  Pend pend[kRing][kDataWaves];
+  uint32_t m[kRing][kDataWaves][kRows][kWave];             // 120 KiB
+};
+
+// ------------------------------------------------------------------------------------------ FASTA row
+// One row (64 lanes x 16 bytes) under the wave-uniform incoming line state S.  Interleaved masks:
+// bit 2i = byte i is '\n', bit 2i+1 = byte i is a valid '>' (followed by a non-'\n' byte inside the chunk).
+struct FRow {
+  uint32_t m;                // emits (odd bits) | ends (even bits)
+  uint32_t nemit;            // emits in this lane
+  uint32_t s_before_nl;      // line state just before this lane's first '\n'
+  uint32_t first_nl;         // bit index (even) of this lane's first '\n', or 32
+  uint64_t H;                // ballot: lanes holding a '\n'
+  uint32_t S_out;            // wave-uniform state after the row
+};
+__device__ __forceinline__ FRow fasta_row(uint32_t M, uint32_t nxt63, int last_bit, uint32_t S, int lane) {
+  FRow f;
+  const uint32_t NL = M & kEven, GT = M & kOdd;
+  // next lane's byte 0 is '\n'? (wave_shl:1 DPP; lane 63 takes the lookahead byte)
+  const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(NL & 1u), 0x130, 0xF, 0xF, false);
+  const uint32_t nxt = (lane == kWave - 1) ? nxt63 : nb;
+  uint32_t V = GT & ~((NL >> 1) | (nxt << 31));      // '>' followed by a non-'\n' byte
+  if (last_bit >= 0) V &= ~(1u << last_bit);          // p + 1 < c1
+  const uint32_t X = V | NL;
+  // first X bit at/after every line start (lane start, byte after each '\n'): carries run through ~X
+  const uint64_t R64 = (uint64_t)(~X) + ((((uint64_t)NL) << 2) | 1ull);
+  const uint32_t R = (uint32_t)R64;
+  const uint32_t s_last = (uint32_t)(R64 >> 32) ^ 1u;    // a valid '>' after the lane's last '\n'
+  const uint64_t H = __ballot(NL != 0u);
+  const uint64_t SB = __ballot(s_last);
+  // line state at each lane's start: exit(p) = H(p) ? SB(p) : exit(p-1) | SB(p), start(0) = S — a
+  // carry chain over the 64 lanes: generate = SB, propagate = ~H (wave-uniform, scalar unit)
+  const uint64_t a = SB | ~H;
+  const uint64_t s1 = a + SB;
+  const uint64_t c1 = s1 < a;
+  const uint64_t s2 = s1 + (uint64_t)S;
+  const uint64_t c2 = s2 < s1;
+  const uint64_t Sstart = s2 ^ a ^ SB;
+  f.S_out = (uint32_t)(c1 | c2);
+  const uint32_t S_lane = (uint32_t)((Sstart >> lane) & 1ull);
+  const uint32_t low = NL & (0u - NL);
+  const uint32_t fs = low ? low - 1u : 0xFFFFFFFFu;   // bits before the lane's first '\n'
+  const uint32_t emits = V & R & (S_lane ? ~fs : 0xFFFFFFFFu);
+  const uint32_t ends = NL & (~R | (S_lane ? low : 0u));
+  f.m = emits | ends;
+  f.nemit = (uint32_t)__popc(emits);
+  f.s_before_nl = S_lane | ((V & fs) != 0u);
+  f.first_nl = low ? (uint32_t)__builtin_ctz(low) : 32u;
+  f.H = H;
+  return f;
+}
+
+// ------------------------------------------------------------------------------------------ phase A / B
+// Phase A of one unit on one data wave: masks (to LDS) + the wave's summary as a function of the
+// incoming line state (hypothesis: the wave's range starts with S = false).
 template <int MODE>
-__device__ __forceinline__ Func phase_a(const ScanArgs& A, const GeoL& g, Buf& b, Pend& p, uint32_t (&ms)[kRows][kWave],
+__device__ __forceinline__ Func phase_a(const ScanArgs& A, const Geo& g, Buf& b, Pend& p, uint32_t (&ms)[kRows][kWave],
                                         int lane, int wave) {
   uint64_t cnt = 0;
   uint32_t S = 0, nlseen = 0, fV = 0;
   int fn_off = -1;
   const uint64_t lo = g.lo, hi = g.hi;
   const uint64_t wbase = g.ubase + (uint64_t)wave * kWaveBytes;
-  p.wbase = wbase;
   uint32_t rows = 0;
   wait_buf(b);                                       // this buffer landed; the other one stays in flight
   uint4 v[kRows];
@@ -469,30 +507,38 @@ __device__ __forceinline__ Func phase_a(const ScanArgs& A, const GeoL& g, Buf& b
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const uint64_t row0 = wbase + (uint64_t)r * kRowBytes;
-    const uint64_t pos0 = row0 + (uint64_t)lane * 16;
     if (!g.valid || row0 >= hi) continue;
+    // edge row: touches the chunk start, or holds the chunk's last byte (never a header: p+1 < c1)
+    const bool edge = row0 < lo || row0 + kRowBytes >= hi;
+    const int64_t rel_lo = (int64_t)lo - (int64_t)row0 - 16 * lane;   // chunk bounds relative to the lane
+    const int64_t rel_hi = (int64_t)hi - (int64_t)row0 - 16 * lane;
     uint32_t mr;
     if constexpr (MODE == kFasta) {
-      const bool need = S || !nlseen || (__ballot(maybe_has(v[r], kGT)) != 0ull);
-      if (!need) continue;
+      if (!S && nlseen && __ballot(maybe_has(v[r], kGT)) == 0ull) continue;
       uint32_t nxt = 0;
       if (row0 + kRowBytes < hi) {
         const uint32_t w = (r + 1 < kRows) ? v[(r + 1) & (kRows - 1)].x : la;
         nxt = ((uint32_t)__builtin_amdgcn_readlane((int)w, 0) & 0xFFu) == 10u;
       }
-      const int64_t lb = (int64_t)hi - 1 - (int64_t)pos0;
-      const FRow f = fasta_row(v[r], clip16(pos0, lo, hi), nxt, (lb >= 0 && lb < 16) ? (int)lb : -1, S, lane);
+      uint32_t M = pairs32(v[r]);
+      int last_bit = -1;
+      if (edge) {
+        M &= range32(rel_lo, rel_hi);
+        last_bit = (rel_hi >= 1 && rel_hi <= 16) ? (int)(2 * (rel_hi - 1) + 1) : -1;
+      }
+      const FRow f = fasta_row(M, nxt, last_bit, S, lane);
       if (!nlseen && f.H) {
         const int j0 = (int)__builtin_ctzll(f.H);
         fV = __builtin_amdgcn_readlane((int)f.s_before_nl, j0);
-        fn_off = r * kRowBytes + j0 * 16 + __builtin_amdgcn_readlane((int)(f.nl ? __builtin_ctz(f.nl) : 0), j0);
+        fn_off = r * kRowBytes + j0 * 16 + (int)(__builtin_amdgcn_readlane((int)f.first_nl, j0) >> 1);
         nlseen = 1;
       }
-      mr = f.emits | (f.ends << 16);
-      cnt += wave_total<3>((uint32_t)__popc(f.emits));
+      mr = f.m;
+      cnt += wave_total<3>(f.nemit);
       S = f.S_out;
     } else {
-      mr = mask16(v[r], A.delim) & clip16(pos0, lo, hi);
+      mr = mask16(v[r], A.delim);
+      if (edge) mr &= range16(rel_lo, rel_hi);
       cnt += wave_total<5>((uint32_t)__popc(mr));
     }
     if (__ballot(mr != 0u)) {
@@ -500,7 +546,6 @@ __device__ __forceinline__ Func phase_a(const ScanArgs& A, const GeoL& g, Buf& b
       ms[r][lane] = mr;
     }
   }
-  p.rows = rows;
   Func ws;
   if constexpr (MODE == kFasta) {
     if (!nlseen) fV = S;
@@ -509,8 +554,11 @@ __device__ __forceinline__ Func phase_a(const ScanArgs& A, const GeoL& g, Buf& b
   } else {
     ws = Func{cnt, cnt, 0u, 0u};
   }
+  p.wbase = wbase;
+  p.rows = rows;
   p.fV = fV;
   p.fn_off = fn_off;
+  p.pad = 0;
   return ws;
 }
 
@@ -529,8 +577,8 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
 #pragma unroll
     for (int r = 0; r < kRows; ++r) {
       const uint32_t mr = (p.rows >> r) & 1u ? ms[r][lane] : 0u;
-      uint32_t e = mr & 0xFFFFu, n = mr >> 16;
-      if (add_end && (fn_off >> 10) == r && lane == ((fn_off >> 4) & 63)) n |= 1u << (fn_off & 15);
+      uint32_t e = mr & kOdd, n = mr & kEven;
+      if (add_end && (fn_off >> 10) == r && lane == ((fn_off >> 4) & 63)) n |= 1u << (2 * (fn_off & 15));
       if (drop) {
         const uint64_t bal = __ballot(e != 0u);
         if (bal) {
@@ -546,7 +594,7 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
       for (uint32_t x = e; x; x &= x - 1u) {
         const int bb = __builtin_ctz(x);
         const uint64_t i = i0 + (uint32_t)__popc(e & ((1u << bb) - 1u));
-        const uint64_t val = ob + (uint64_t)bb;
+        const uint64_t val = ob + (uint64_t)(bb >> 1);
         if (i < A.cap) {
           if (A.out_u64) put<uint64_t>(A.out, 2 * i, val);
           else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, 2 * i, val); }
@@ -555,7 +603,7 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
       for (uint32_t x = n; x; x &= x - 1u) {
         const int bb = __builtin_ctz(x);
         const uint64_t i = i0 + (uint32_t)__popc(e & ((1u << bb) - 1u)) - 1u;
-        const uint64_t val = ob + (uint64_t)bb + 1u;
+        const uint64_t val = ob + (uint64_t)(bb >> 1) + 1u;
         if (i < A.cap) {
           if (A.out_u64) put<uint64_t>(A.out, 2 * i + 1, val);
           else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, 2 * i + 1, val); }
@@ -571,7 +619,6 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
       const uint32_t mm = ms[r][lane];
       uint32_t tot;
       const uint32_t ex = wave_excl<5>((uint32_t)__popc(mm), tot);
-      if (tot == 0) continue;
       const uint64_t i0 = count + ex;
       const uint64_t ob = obase + p.wbase + (uint64_t)r * kRowBytes + (uint64_t)lane * 16 + A.emit_add;
       for (uint32_t x = mm; x; x &= x - 1u) {
@@ -593,104 +640,150 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
 
-// One pipeline step of a data wave: phase A(k) on buffer b, prefetch k+2 into b, barrier, phase B(k-1).
+// Bounded LDS poll for a value written by another wave of the workgroup.
+__device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint32_t* err) {
+  for (uint32_t spins = 0; lds_ld(p) != v; ++spins) {
+    if (spins > kSpinLimit) {
+      if (__lane_id() == 0) atomicOr(err, kErrTimeout);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  cbar();
+  return true;
+}
+
+// Data wave, phase B of unit j once the coordinator has published its prefixes.
 template <int MODE>
-__device__ __forceinline__ void data_step(const ScanArgs& A, uint64_t k, GeoL& g, Buf& b, Pend& pk,
-                                          const Pend& pprev, int lane, int wave, Shared& sh) {
-  const Func ws = phase_a<MODE>(A, g, b, pk, sh.m[k & 1][wave], lane, wave);
-  load_buf(b, A, geo_from_lds(sh.geo[(k + 2) & 3]), wave, lane);
-  const GeoL gn = geo_from_lds(sh.geo[(k + 1) & 3]);
+__device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int lane, int wave, Shared& sh) {
+  const int s = (int)(j % kRing);
+  lds_wait_eq(&sh.ready[s], (uint32_t)j + 1u, A.err);
+  Pend p = sh.pend[s][wave];
+  p.wbase = rfl64(p.wbase);
+  p.rows = rfl(p.rows);
+  p.fV = rfl(p.fV);
+  p.fn_off = (int)rfl((uint32_t)p.fn_off);
+  const uint64_t P = rfl64(sh.P[s][wave]);
+  const uint32_t S = rfl(sh.S[s][wave]);
+  phase_b<MODE>(A, p, sh.m[s][wave], P, S, lane);
+}
+
+// One data-wave step with unit k: phase A(k) on buffer b -> post -> prefetch the unit after next into
+// b -> phase B(k - kBLag).
+template <int MODE>
+__device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint64_t k, uint64_t u0, uint64_t G,
+                                          Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh) {
+  const int s = (int)(k % kRing);
+  Pend p;
+  const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave);
   if (lane == 0) {
-    const int s = (int)(k & 1);
     sh.cF[s][wave] = ws.cF; sh.cT[s][wave] = ws.cT; sh.sF[s][wave] = ws.sF; sh.sT[s][wave] = ws.sT;
+    sh.pend[s][wave] = p;
+    cbar();
+    lds_add(&sh.done[s], 1u);
   }
-  __syncthreads();                                   // BARRIER_k
-  if (k > 0) {
-    const int s = (int)((k - 1) & 1);
-    phase_b<MODE>(A, pprev, sh.m[s][wave], sh.P[s][wave], sh.S[s][wave], lane);
-  }
-  g = gn;
+  const Geo g2 = geo_of(T, A.nchunks, A.nunits, u0 + (k + 2) * (uint64_t)G, cur);
+  load_buf(b, A, g2, wave, lane);
+  if (k >= (uint64_t)kBLag) data_finish<MODE>(A, k - kBLag, lane, wave, sh);
+  g = gnext;
+  gnext = g2;
 }
 
-// Coordinator: after BARRIER_k, resolve unit k (look-back) and compute the geometry of unit k+4.
-template <int MODE>
-__device__ __forceinline__ void coord_step(const ScanArgs& A, uint64_t k, uint64_t u, uint64_t G, int lane,
-                                           Shared& sh, uint64_t& prevP, uint32_t& prevS, Cursor& cur) {
-  __syncthreads();                                   // BARRIER_k
-  const int s = (int)(k & 1);
-  const GeoL g = geo_from_lds(sh.geo[k & 3]);
-  Func unit = Func{sh.cF[s][0], sh.cT[s][0], sh.sF[s][0], sh.sT[s][0]};
+__device__ __forceinline__ Func unit_func(const Shared& sh, int s) {
+  Func f = Func{sh.cF[s][0], sh.cT[s][0], sh.sF[s][0], sh.sT[s][0]};
 #pragma unroll
-  for (int i = 1; i < kDataWaves; ++i)
-    unit = f_then(unit, Func{sh.cF[s][i], sh.cT[s][i], sh.sF[s][i], sh.sT[s][i]});
-  if (u > 0 && lane == 0) st_desc(&A.desc[u], pack_agg(unit));
-  uint64_t P;
-  uint32_t S_in;
-  lookback(A, u, G, u >= G ? prevP : 0ull, u >= G ? prevS : 0u, lane, P, S_in);
-  const uint64_t P_incl = P + (S_in ? unit.cT : unit.cF);
-  const uint32_t S_out = S_in ? unit.sT : unit.sF;
-  prevP = P_incl;
-  prevS = S_out;
-  if (lane == 0) {
-    st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
-    uint64_t p = P;
-    uint32_t st = g.first ? 0u : S_in;
-    for (int i = 0; i < kDataWaves; ++i) {
-      sh.P[s][i] = p;
-      sh.S[s][i] = st;
-      p += st ? sh.cT[s][i] : sh.cF[s][i];
-      st = st ? sh.sT[s][i] : sh.sF[s][i];
+  for (int i = 1; i < kDataWaves; ++i) f = f_then(f, Func{sh.cF[s][i], sh.cT[s][i], sh.sF[s][i], sh.sT[s][i]});
+  return f;
+}
+
+// Coordinator: publish the aggregate of every unit as soon as its 15 data waves are done with it, and
+// resolve unit j (look-back -> inclusive prefix, per-wave prefixes, per-chunk results) once the
+// aggregate of unit j + kLag is out.
+template <int MODE>
+__device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint64_t u0, uint64_t G, uint64_t K,
+                                            int lane, Shared& sh) {
+  Cursor cur{0, 0, 0, 0, 0, 0};
+  uint64_t prevP = 0;
+  uint32_t prevS = 0;
+  uint64_t published = 0;
+  for (uint64_t j = 0; j < K; ++j) {
+    // publish aggregates up to j + kLag (inclusive) or the end
+    const uint64_t want = (j + kLag + 1 < K) ? j + kLag + 1 : K;
+    while (published < want) {
+      const int s = (int)(published % kRing);
+      lds_wait_eq(&sh.done[s], (uint32_t)kDataWaves, A.err);
+      const uint64_t u = u0 + published * G;
+      if (u > 0 && lane == 0) st_desc(&A.desc[u], pack_agg(unit_func(sh, s)));
+      ++published;
     }
-    if (u + 1 == A.nunits) A.total[0] = P_incl;
-    if (g.last) {
-      A.chunk_end[g.c] = P_incl;
-      if constexpr (MODE == kFasta) A.pending[g.c] = S_out ? (long long)P_incl - 1 : -1ll;
+    const int s = (int)(j % kRing);
+    const uint64_t u = u0 + j * G;
+    const Func unit = unit_func(sh, s);
+    const Geo g = geo_of(T, A.nchunks, A.nunits, u, cur);
+    uint64_t P;
+    uint32_t S_in;
+    lookback(A, u, G, u >= G ? prevP : 0ull, u >= G ? prevS : 0u, lane, P, S_in);
+    const uint64_t P_incl = P + (S_in ? unit.cT : unit.cF);
+    const uint32_t S_out = S_in ? unit.sT : unit.sF;
+    prevP = P_incl;
+    prevS = S_out;
+    if (lane == 0) {
+      st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
+      uint64_t p = P;
+      uint32_t st = g.first ? 0u : S_in;
+      for (int i = 0; i < kDataWaves; ++i) {
+        sh.P[s][i] = p;
+        sh.S[s][i] = st;
+        p += st ? sh.cT[s][i] : sh.cF[s][i];
+        st = st ? sh.sT[s][i] : sh.sF[s][i];
+      }
+      if (u + 1 == A.nunits) A.total[0] = P_incl;
+      if (g.last) {
+        A.chunk_end[g.c] = P_incl;
+        if constexpr (MODE == kFasta) A.pending[g.c] = S_out ? (long long)P_incl - 1 : -1ll;
+      }
+      sh.done[s] = 0;                                // slot free for unit j + kRing
+      cbar();
+      lds_st(&sh.ready[s], (uint32_t)j + 1u);
     }
   }
-  const GeoL g4 = coord_geo(A, u + 4 * G, cur);
-  if (lane == 0) sh.geo[k & 3] = g4;
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A) {
+__global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64_t* __restrict__ tab_lo,
+                                                        const uint64_t* __restrict__ tab_hi,
+                                                        const uint64_t* __restrict__ tab_u0) {
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __shared__ Shared sh;
+  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_u0};
   const uint64_t G = gridDim.x;
   const uint64_t u0 = blockIdx.x;
   const uint64_t K = u0 < A.nunits ? (A.nunits - u0 + G - 1) / G : 0;   // units of this workgroup
+  if (threadIdx.x < kRing) {
+    sh.done[threadIdx.x] = 0;
+    sh.ready[threadIdx.x] = 0;
+  }
+  __syncthreads();
   if (wave == kCoord) {
-    Cursor cur{0, 0, 0, 0};
-    GeoL g[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) g[i] = coord_geo(A, u0 + i * G, cur);
-    if (lane == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sh.geo[i] = g[i];
-    }
-    __syncthreads();                                 // BARRIER_init
-    uint64_t prevP = 0;
-    uint32_t prevS = 0;
-    for (uint64_t k = 0; k < K; ++k) coord_step<MODE>(A, k, u0 + k * G, G, lane, sh, prevP, prevS, cur);
-    __syncthreads();                                 // BARRIER_K
+    coordinator<MODE>(A, T, u0, G, K, lane, sh);
   } else {
-    __syncthreads();                                 // BARRIER_init
-    GeoL g = geo_from_lds(sh.geo[0]);
+    Cursor cur{0, 0, 0, 0, 0, 0};
+    Geo g = geo_of(T, A.nchunks, A.nunits, u0, cur);
+    Geo gnext = geo_of(T, A.nchunks, A.nunits, u0 + G, cur);
     Buf bA, bB;
-    Pend pA{0, 0, 0, -1}, pB{0, 0, 0, -1};
     load_buf(bA, A, g, wave, lane);
-    load_buf(bB, A, geo_from_lds(sh.geo[1]), wave, lane);
+    load_buf(bB, A, gnext, wave, lane);
     uint64_t k = 0;
     while (k < K) {
-      data_step<MODE>(A, k, g, bA, pA, pB, lane, wave, sh);
+      data_step<MODE>(A, T, k, u0, G, g, gnext, bA, cur, lane, wave, sh);
       if (++k == K) break;
-      data_step<MODE>(A, k, g, bB, pB, pA, lane, wave, sh);
+      data_step<MODE>(A, T, k, u0, G, g, gnext, bB, cur, lane, wave, sh);
       ++k;
     }
-    __syncthreads();                                 // BARRIER_K
-    const int s = (int)((K - 1) & 1);
-    if (K & 1) phase_b<MODE>(A, pA, sh.m[s][wave], sh.P[s][wave], sh.S[s][wave], lane);
-    else if (K) phase_b<MODE>(A, pB, sh.m[s][wave], sh.P[s][wave], sh.S[s][wave], lane);
+    drain_bufs(bA, bB);
+    const uint64_t j0 = K > (uint64_t)kBLag ? K - kBLag : 0;
+    for (uint64_t j = j0; j < K; ++j) data_finish<MODE>(A, j, lane, wave, sh);   // drain
   }
 }
 
@@ -699,7 +792,7 @@ __device__ uint64_t wave_find(const uint8_t* base, uint64_t from, uint64_t end, 
   for (uint64_t a = from & ~15ull; a < end; a += kRowBytes) {
     const uint64_t pa = a + (uint64_t)lane * 16;
     uint32_t m = 0;
-    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), pat) & clip16(pa, from, end);
+    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), pat) & range16((int64_t)from - (int64_t)pa, (int64_t)end - (int64_t)pa);
     const uint64_t bal = __ballot(m != 0u);
     if (bal) {
       const int l = (int)__builtin_ctzll(bal);
@@ -919,9 +1012,6 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.base = d_buf - shift;
   a.shift = shift;
   a.obj_base = buf_base;
-  a.chunk_lo = c->d_tab;
-  a.chunk_hi = c->d_tab + n;
-  a.chunk_u0 = c->d_tab + 2 * n;
   a.nchunks = n;
   a.nunits = units;
   a.desc = c->d_desc;
@@ -944,10 +1034,13 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   hipEvent_t e0;
   rc = ev_begin(c, &e0);
   if (rc) return rc;
+  const uint64_t* tlo = c->d_tab;
+  const uint64_t* thi = c->d_tab + n;
+  const uint64_t* tu0 = c->d_tab + 2 * n;
   if (mode == kFasta)
-    hipLaunchKernelGGL(scan_kernel<kFasta>, dim3(grid), dim3(kThreads), 0, c->stream, a);
+    hipLaunchKernelGGL(scan_kernel<kFasta>, dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   else
-    hipLaunchKernelGGL(scan_kernel<kDelim>, dim3(grid), dim3(kThreads), 0, c->stream, a);
+    hipLaunchKernelGGL(scan_kernel<kDelim>, dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   HIPCHK(hipGetLastError());
   return ev_end(c);
 }

@@ -16,7 +16,7 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "dataplug_amd", "csrc", "dpscan.hip")
-KERNELS = ["_ZN12_GLOBAL__N_111scan_kernelILi0EEEvNS_8ScanArgsE", "_ZN12_GLOBAL__N_111scan_kernelILi1EEEvNS_8ScanArgsE"]
+KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_111scan_kernelILi[01]EE\w*):", re.M)
 
 
 def compile_asm() -> str:
@@ -38,7 +38,9 @@ def regs(tok: str):
 def check(asm_path: str):
     text = open(asm_path).read()
     problems = []
-    for k in KERNELS:
+    kernels = KERNEL_RE.findall(text)
+    assert len(kernels) == 2, kernels
+    for k in kernels:
         body = text[text.index(k + ":"):]
         body = body[:body.index(".Lfunc_end")]
         pending = set()          # registers with an un-waited input load
@@ -48,8 +50,9 @@ def check(asm_path: str):
             if not s:
                 continue
             if s.endswith(":"):
-                if prev_uncond:          # not reachable by fall-through: a different path
-                    pending.clear()
+                # conservative: a block can be entered from anywhere, so pending loads stay pending
+                # until a vmcnt wait (textual order; may over-report, never under-reports a path the
+                # layout puts after the loads)
                 continue
             prev_uncond = s.split()[0] in ("s_branch", "s_endpgm", "s_setpc_b64")
             if s.startswith("s_waitcnt") and "vmcnt" in s:
