@@ -1,0 +1,157 @@
+"""Newline index artefact shared by the CSV and VCF plugins, and the slice boundaries derived from it.
+
+The reference finds CSV/VCF slice boundaries at ``get()`` time by scanning a padded byte range in Python
+(csv.py:52-105, vcf.py:88-149).  Here ``preprocess`` builds the sorted ``uint64`` offsets of every ``'\\n'``
+on the GPU once, stores them at ``s3://<bucket>.meta/<key>.lines``, and a partition strategy resolves each
+slice's exact byte range from that index, reproducing the reference's ``get()`` output (SURVEY.md §8(a)
+formulas, restated below with the clamps the reference's buffer arithmetic implies).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Optional, Tuple
+
+import numpy as np
+
+from ..version import __version__
+
+LINES_SUFFIX = ".lines"
+_PRELOAD_BYTES = 256 << 20
+_BLOCK = 8192                      # entries per cached block for large indexes
+
+
+def store_line_index(cloud_object, offsets: np.ndarray) -> str:
+    key = cloud_object.meta_path.key + LINES_SUFFIX
+    cloud_object.storage.put_object(Body=np.ascontiguousarray(offsets, dtype="<u8").tobytes(),
+                                    Bucket=cloud_object.meta_path.bucket, Key=key,
+                                    Metadata={"dataplug": __version__})
+    return key
+
+
+class LineIndex:
+    """Sorted newline offsets; ``nxt(x)`` = 1 + first '\\n' at or after x (None if none)."""
+
+    def __init__(self, offsets: Optional[np.ndarray] = None, storage=None, bucket: str = "", key: str = "",
+                 count: Optional[int] = None):
+        self._arr = None if offsets is None else np.asarray(offsets, dtype=np.uint64)
+        self._storage, self._bucket, self._key = storage, bucket, key
+        self._blocks: "OrderedDict[int, np.ndarray]" = OrderedDict()
+        if self._arr is None:
+            if count is None:
+                count = int(storage.head_object(Bucket=bucket, Key=key)["ContentLength"]) // 8
+            self.count = int(count)
+            if self.count * 8 <= _PRELOAD_BYTES:
+                self._arr = self._fetch(0, self.count)
+        else:
+            self.count = len(self._arr)
+
+    @classmethod
+    def of(cls, cloud_object) -> "LineIndex":
+        attrs = cloud_object.attributes
+        key = getattr(attrs, "line_index_key", None) if attrs is not None else None
+        if not key:
+            raise KeyError(f"{cloud_object!r} has no newline index: preprocess it with dataplug_amd (line_index=True)")
+        return cls(storage=cloud_object.storage, bucket=cloud_object.meta_path.bucket, key=key,
+                   count=getattr(attrs, "num_lines", None))
+
+    def _fetch(self, i0: int, i1: int) -> np.ndarray:
+        if i1 <= i0:
+            return np.zeros(0, np.uint64)
+        res = self._storage.get_object(Bucket=self._bucket, Key=self._key, Range=f"bytes={8 * i0}-{8 * i1 - 1}")
+        return np.frombuffer(res["Body"].read(), dtype="<u8").astype(np.uint64, copy=False)
+
+    def _block(self, b: int) -> np.ndarray:
+        blk = self._blocks.get(b)
+        if blk is None:
+            blk = self._fetch(b * _BLOCK, min(self.count, (b + 1) * _BLOCK))
+            self._blocks[b] = blk
+            if len(self._blocks) > 64:
+                self._blocks.popitem(last=False)
+        return blk
+
+    def _search(self, x: int) -> int:
+        """Index of the first entry >= x (``count`` if none)."""
+        if self._arr is not None:
+            return int(np.searchsorted(self._arr, np.uint64(x)))
+        nb = -(-self.count // _BLOCK)
+        lo, hi = 0, nb                      # first block whose last entry >= x
+        while lo < hi:
+            mid = (lo + hi) // 2
+            last = self._block(mid)[-1]
+            if int(last) >= x:
+                hi = mid
+            else:
+                lo = mid + 1
+        if lo == nb:
+            return self.count
+        return lo * _BLOCK + int(np.searchsorted(self._block(lo), np.uint64(x)))
+
+    def value(self, i: int) -> int:
+        if self._arr is not None:
+            return int(self._arr[i])
+        return int(self._block(i // _BLOCK)[i % _BLOCK])
+
+    def nxt(self, x: int) -> Optional[int]:
+        i = self._search(x)
+        return self.value(i) + 1 if i < self.count else None
+
+    def contains(self, x: int) -> bool:
+        i = self._search(x)
+        return i < self.count and self.value(i) == x
+
+
+class SliceError(Exception):
+    """The reference's ``get()`` fails for this slice (kept as an error, not papered over)."""
+
+
+def csv_body(lines: LineIndex, size: int, r0: int, r1: int, chunk_id: int, num_chunks: int,
+             padding: int) -> Tuple[int, int]:
+    """Object bytes [start, end) that ``CSVSlice.get`` (csv.py:52-105) returns (after the header prefix).
+
+    The reference reads ``bytes=r0-r1`` (inclusive) → buffer end ``be = min(r1 + 1, size)``.
+    * start: chunk 0 → r0; else r0 itself when byte r0 is '\\n' (that line is then in two slices), otherwise
+      1 + the first '\\n' after r0, capped at ``be`` (readline stops at the buffer end).
+    * end: last chunk → ``be``; otherwise 1 + the first '\\n' at or after ``be - padding - 1``.  The
+      reference seeks to a negative position when ``be - r0 <= padding`` (ValueError), and its buffer-
+      expansion loop never finds a '\\n' it did not already hold, so a missing '\\n' in
+      [be - padding - 1, be) is an error as well."""
+    be = min(r1 + 1, size)
+    if chunk_id == 0:
+        start = r0
+    elif lines.contains(r0):
+        start = r0
+    else:
+        n = lines.nxt(r0 + 1)
+        start = be if n is None else min(n, be)
+    if chunk_id == num_chunks - 1:
+        return start, be
+    if be - r0 <= padding:
+        raise SliceError(f"slice {chunk_id} holds {be - r0} bytes <= padding {padding}: the reference's "
+                         f"CSVSlice.get seeks to a negative position (ValueError)")
+    n = lines.nxt(be - padding - 1)
+    if n is None or n > be:
+        raise SliceError(f"slice {chunk_id}: no newline in the last {padding + 1} bytes of its range; the "
+                         f"reference's buffer expansion (csv.py:81-94) cannot find one either")
+    return start, n
+
+
+def vcf_body(lines: LineIndex, size: int, r0: int, r1: int, chunk_id: int, num_chunks: int) -> Tuple[int, int]:
+    """Object bytes [start, end) of a ``VCFSlice.get`` body (vcf.py:88-149).
+
+    Buffer end ``be = min(r1 + 1, size)``.  start: chunk 0 → r0 (= body_offset); else 1 + the first '\\n' at
+    or after r0, capped at ``be``.  end: last chunk → ``be``; else 1 + the first '\\n' at or after ``be - 1``
+    (the reference's expansion reads further ranges until it sees one; none before EOF → its GET past the
+    end fails)."""
+    be = min(r1 + 1, size)
+    if chunk_id == 0:
+        start = r0
+    else:
+        n = lines.nxt(r0)
+        start = be if n is None else min(n, be)
+    if chunk_id == num_chunks - 1:
+        return start, be
+    n = lines.nxt(be - 1)
+    if n is None:
+        raise SliceError(f"slice {chunk_id}: no newline after byte {be - 1}; the reference's range expansion "
+                         f"requests bytes past the end of the object")
+    return start, n

@@ -44,6 +44,26 @@ class DeviceBuffer:
         self.ptr = 0
 
 
+class PinnedBuffer:
+    """Page-locked host memory (dp_host_alloc) with a uint8 numpy view; H2D from it is a true async DMA."""
+
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(_lib.load().dp_host_alloc(max(16, self.nbytes), ctypes.byref(p)))
+        self.ptr = int(p.value)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(16, self.nbytes)).from_address(self.ptr))
+
+    def view(self, n: Optional[int] = None) -> memoryview:
+        return memoryview(self.array)[: self.nbytes if n is None else n]
+
+    def free(self):
+        if self.ptr:
+            self.array = None
+            check(_lib.load().dp_host_free(ctypes.c_void_p(self.ptr)))
+        self.ptr = 0
+
+
 class ScanContext:
     """A ``dp_ctx``: device, stream and scan workspace.  Not shared between threads."""
 
@@ -54,6 +74,7 @@ class ScanContext:
         self.handle = h
         self.device = int(device)
         self._bufs = {}
+        self._pinned = {}
 
     # ---------------------------------------------------------------- memory
     def workspace(self, name: str, nbytes: int) -> DeviceBuffer:
@@ -65,6 +86,20 @@ class ScanContext:
             b = DeviceBuffer(self, max(int(nbytes), 1 << 16))
             self._bufs[name] = b
         return b
+
+    def pinned(self, name: str, nbytes: int) -> PinnedBuffer:
+        """Grow-only named pinned host buffer."""
+        b = self._pinned.get(name)
+        if b is None or b.nbytes < nbytes:
+            if b is not None:
+                b.free()
+            b = PinnedBuffer(max(int(nbytes), 1 << 16))
+            self._pinned[name] = b
+        return b
+
+    def h2d_async(self, dst: int, src_ptr: int, nbytes: int) -> None:
+        """Async copy from pinned host memory on the context stream (caller keeps the source alive)."""
+        check(self.lib.dp_h2d(self.handle, ctypes.c_void_p(dst), ctypes.c_void_p(src_ptr), int(nbytes)))
 
     def h2d(self, dst: int, data, nbytes: Optional[int] = None) -> None:
         ptr, n, keep = _host_ptr(data)
@@ -216,9 +251,10 @@ class ScanContext:
 
     def close(self) -> None:
         if self.handle:
-            for b in self._bufs.values():
+            for b in list(self._bufs.values()) + list(self._pinned.values()):
                 b.free()
             self._bufs.clear()
+            self._pinned.clear()
             check(self.lib.dp_ctx_destroy(self.handle))
             self.handle = None
 

@@ -1,0 +1,195 @@
+"""Object-level index builds: storage → pinned host → HBM → HIP scan → host index.
+
+These are what the format plugins call.  Everything computational runs in libdpscan (HIP); the host side
+only moves bytes and stitches per-GPU results in chunk order.  Multi-GPU: an object's map chunks are
+independent (preprocess.py:39-51 of the reference), so the chunk list is cut into contiguous groups, one
+per GPU, each scanned by one launch on its own device; no collective.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from ._lib import DPScanUnavailable
+from ..dist import split_groups
+from .device import ScanContext, device_count, get_context
+
+_GET_PART = 32 << 20          # ranged-GET part size for parallel fetches
+_GET_THREADS = 16
+_HALO0 = 64 << 10             # first look-ahead window when a header line crosses the fetched bytes
+
+
+def devices(max_devices: Optional[int] = None) -> List[int]:
+    env = os.environ.get("DATAPLUG_AMD_DEVICES")
+    if env:
+        devs = [int(x) for x in env.split(",") if x.strip()]
+    else:
+        n = device_count()
+        if n <= 0:
+            raise DPScanUnavailable("no HIP device visible: the index build runs on MI355X GPUs only")
+        devs = list(range(n))
+    return devs[:max_devices] if max_devices else devs
+
+
+# ------------------------------------------------------------------------------------------ storage → host
+def read_range_into(storage, bucket: str, key: str, lo: int, hi: int, out: memoryview,
+                    part: int = _GET_PART, threads: int = _GET_THREADS) -> None:
+    """Object bytes [lo, hi) into ``out`` (len >= hi - lo) with parallel ranged GETs (inclusive Range)."""
+    n = hi - lo
+    if n <= 0:
+        return
+    out = out.cast("B") if out.format != "B" else out
+
+    def one(a: int) -> None:
+        b = min(n, a + part)
+        res = storage.get_object(Bucket=bucket, Key=key, Range=f"bytes={lo + a}-{lo + b - 1}")
+        body = res["Body"]
+        got = a
+        with body:
+            while got < b:
+                r = body.readinto(out[got:b])
+                if not r:
+                    raise IOError(f"short read of {bucket}/{key} at {lo + got}")
+                got += r
+
+    starts = list(range(0, n, part))
+    if len(starts) == 1:
+        one(0)
+        return
+    with cf.ThreadPoolExecutor(min(threads, len(starts))) as ex:
+        list(ex.map(one, starts))
+
+
+def resolve_line_end(ctx: ScanContext, storage, bucket: str, key: str, size: int, pos: int) -> int:
+    """1 + the first '\\n' at or after object offset ``pos``, or ``size`` (what the reference's
+    seek(start) + readline() + tell() gives for a header cut by its chunk end, fasta.py:45-56).
+    The search itself runs on the GPU (dp_find_delim) over growing look-ahead windows."""
+    win = _HALO0
+    while pos < size:
+        hi = min(size, pos + win)
+        buf = ctx.pinned("halo", hi - pos)
+        read_range_into(storage, bucket, key, pos, hi, buf.view(hi - pos))
+        d = ctx.workspace("halo", hi - pos + 64)
+        ctx.h2d_async(d.ptr, buf.ptr, hi - pos)
+        p = ctx.find_delim(d.ptr, hi - pos, pos, pos, 10)
+        if p >= 0:
+            return p + 1
+        pos = hi
+        win *= 4
+    return size
+
+
+# ------------------------------------------------------------------------------------------ FASTA
+def _fasta_group(dev: int, co, plan: Sequence[Tuple[int, int]], u64: bool) -> np.ndarray:
+    ctx = get_context(dev)
+    size = co.size
+    lo = min(c0 for c0, _ in plan)
+    hi = max(c1 for _, c1 in plan)
+    n = hi - lo
+    host = ctx.pinned("object", n)
+    read_range_into(co.storage, co.path.bucket, co.path.key, lo, hi, host.view(n))
+    d = ctx.workspace("input", n + 64)
+    ctx.h2d_async(d.ptr, host.ptr, n)
+    pairs, pending, _ = ctx.fasta_index(d.ptr, n, lo, size, plan, u64=u64)
+    for p in pending[pending >= 0]:
+        start = int(pairs[p, 0])
+        end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, size, hi)
+        if not u64 and end > 0xFFFFFFFF:
+            raise OverflowError(f"FASTA offset {end} does not fit the uint32 index (header at {start})")
+        pairs[p, 1] = end
+    return pairs
+
+
+def fasta_index_object(co, plan: Sequence[Tuple[int, int]], u64: bool = False,
+                       max_devices: Optional[int] = None) -> np.ndarray:
+    """(n, 2) (start, end) pairs of every chunk of ``plan`` concatenated in chunk order — the index
+    ``merge_fasta_metadata`` (fasta.py:66-74) assembles from the per-chunk map outputs."""
+    if not plan:
+        return np.zeros((0, 2), np.uint64 if u64 else np.uint32)
+    devs = devices(max_devices)
+    groups = split_groups(len(plan), len(devs))
+    if len(groups) == 1:
+        return _fasta_group(devs[0], co, plan, u64)
+    with cf.ThreadPoolExecutor(len(groups)) as ex:
+        futs = [ex.submit(_fasta_group, devs[k], co, plan[i0:i1], u64) for k, (i0, i1) in enumerate(groups)]
+        parts = [f.result() for f in futs]
+    return np.concatenate(parts)
+
+
+def fasta_index_chunk(co, data, chunk_offset: int, job: int = 0, u64: bool = False) -> np.ndarray:
+    """Pairs of one map chunk whose bytes ``data`` the caller already holds (the per-chunk plugin call),
+    scanned on GPU ``job % n_gpus``."""
+    devs = devices()
+    ctx = get_context(devs[job % len(devs)])
+    n = len(data)
+    pairs, pending, _ = ctx.fasta_index_host(data, chunk_offset, co.size, [(chunk_offset, chunk_offset + n)], u64=u64)
+    for p in pending[pending >= 0]:
+        end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, co.size, chunk_offset + n)
+        if not u64 and end > 0xFFFFFFFF:
+            raise OverflowError(f"FASTA offset {end} does not fit the uint32 index")
+        pairs[p, 1] = end
+    return pairs
+
+
+# ------------------------------------------------------------------------------------------ newline / record index
+def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int):
+    ctx = get_context(dev)
+    n = hi - lo
+    host = ctx.pinned("object", n)
+    read_range_into(co.storage, co.path.bucket, co.path.key, lo, hi, host.view(n))
+    d = ctx.workspace("input", n + 64)
+    ctx.h2d_async(d.ptr, host.ptr, n)
+    return ctx.delim_index(d.ptr, n, lo, lo, hi, delim=delim, every_k=every_k, emit_add=emit_add, u64=True)
+
+
+def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int = 10,
+                      max_devices: Optional[int] = None, part_bytes: int = 16 << 30) -> np.ndarray:
+    """Sorted uint64 offsets of every ``delim`` byte of object bytes [begin, end).
+
+    The range is cut into independent parts (at most ``part_bytes`` each, at least one per GPU) scanned
+    round-robin on the GPUs and concatenated in order."""
+    end = co.size if end is None else end
+    if end <= begin:
+        return np.zeros(0, np.uint64)
+    devs = devices(max_devices)
+    nparts = max(len(devs), -(-(end - begin) // part_bytes))
+    step = -(-(end - begin) // nparts)
+    bounds = [(begin + i * step, min(end, begin + (i + 1) * step)) for i in range(nparts)]
+    bounds = [b for b in bounds if b[1] > b[0]]
+
+    def run(k: int):
+        lo, hi = bounds[k]
+        return _delim_group(devs[k % len(devs)], co, lo, hi, delim, 1, 0)[0]
+
+    if len(bounds) == 1:
+        return run(0)
+    # one worker per GPU; parts of the same GPU run in order on that GPU's thread
+    by_dev = {}
+    for k in range(len(bounds)):
+        by_dev.setdefault(k % len(devs), []).append(k)
+    out = [None] * len(bounds)
+
+    def worker(ks):
+        for k in ks:
+            out[k] = run(k)
+
+    with cf.ThreadPoolExecutor(len(by_dev)) as ex:
+        list(ex.map(worker, by_dev.values()))
+    return np.concatenate(out)
+
+
+def record_index_bytes(data, delim: int = 10, every_k: int = 1, emit_add: int = 0, device: int = 0,
+                       u64: bool = True):
+    """(offsets, number of delimiters) over host bytes already in memory (e.g. an inflated FASTQ stream)."""
+    ctx = get_context(device)
+    n = len(data)
+    if n == 0:
+        return np.zeros(0, np.uint64 if u64 else np.uint32), 0
+    host = ctx.pinned("object", n)
+    host.array[:n] = np.frombuffer(memoryview(data).cast("B"), np.uint8)
+    d = ctx.workspace("input", n + 64)
+    ctx.h2d_async(d.ptr, host.ptr, n)
+    return ctx.delim_index(d.ptr, n, 0, 0, n, delim=delim, every_k=every_k, emit_add=emit_add, u64=u64)

@@ -178,3 +178,11 @@ def tiled_fasta_host(size: int, seed: int = 0, block: int = 64 * 2**20 - 4099) -
         out[off:off + n] = base[:n]
     _fix_fasta_tail(out)
     return out
+
+
+def tiled_host(base: np.ndarray, size: int) -> np.ndarray:
+    """``size`` bytes made of repeated copies of ``base`` (the last copy truncated)."""
+    out = np.empty(size, np.uint8)
+    for off, n in tile_plan(len(base), size):
+        out[off:off + n] = base[:n]
+    return out

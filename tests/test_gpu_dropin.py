@@ -1,0 +1,200 @@
+"""co.preprocess() drop-in through the HIP path (libdpscan) against the reference's outputs.
+
+FASTA: the sample and the golden fuzz cases (reference-generated), synthetic objects at several chunk
+sizes (oracle), the per-chunk joblib route, multi-group splits (DATAPLUG_AMD_DEVICES=0,0,... runs the
+multi-GPU grouping on one GPU), and a header line crossing a group boundary (pending-end resolution).
+CSV/VCF: the GPU newline index equals the bytes' '\\n' positions and the partitions equal the reference's
+get() outputs.  FASTQ.gz: total_lines and per-read ends on the inflated stream, read batches' lines."""
+import gzip
+import json
+import os
+
+import numpy as np
+import pytest
+
+from dataplug_amd import synth
+from dataplug_amd.cloudobject import CloudObject
+from dataplug_amd.storage import LoopbackS3Server, MemoryStore
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def server():
+    with LoopbackS3Server() as srv:
+        yield srv
+
+
+def _co(fmt, data: bytes, key: str, cfg):
+    co = CloudObject.from_s3(fmt, f"s3://data/{key}", fetch=False, s3_config=cfg)
+    try:
+        co.storage.head_bucket(Bucket="data")
+    except Exception:
+        co.storage.create_bucket(Bucket="data")
+    co.storage.put_object(Body=data, Bucket="data", Key=key)
+    return CloudObject.from_s3(fmt, f"s3://data/{key}", s3_config=cfg)
+
+
+def _index(co):
+    return np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read(),
+                         np.uint32)
+
+
+def _mem(name):
+    MemoryStore._named.pop(name, None)
+    return {"endpoint_url": f"memory://{name}"}
+
+
+# ------------------------------------------------------------------------------------------------ FASTA
+@pytest.mark.parametrize("parallel_config", [{}, {"backend": "threading", "n_jobs": 4}])
+def test_fasta_sample_over_loopback(server, fasta_cases, parallel_config):
+    from dataplug_amd.formats.genomics.fasta import FASTA, partition_chunks_strategy
+    z = fasta_cases
+    i = list(z["kind"]).index("sample")
+    data = bytes(z["data"][z["data_off"][i]:z["data_off"][i + 1]])
+    co = _co(FASTA, data, f"sample{len(parallel_config)}.fasta", server.storage_config)
+    co.preprocess(parallel_config=parallel_config, chunk_size=-(-len(data) // 4))
+    assert co.attributes.num_sequences == 9
+    assert _index(co).reshape(-1, 2).tolist() == [[0, 60], [236, 296], [473, 533], [709, 769], [946, 1006],
+                                                  [1183, 1249], [1426, 1486], [1663, 1721], [1898, 1958]]
+    g = [r for r in json.load(open(os.path.join(GOLDEN, "fasta_slices.json"))) if r["object"] == "sample"]
+    for rec in g:
+        sl = co.partition(partition_chunks_strategy, num_chunks=rec["num_chunks"])
+        assert [[s.offset, None if s.header is None else list(s.header), s.range_0, s.range_1] for s in sl] == \
+            rec["slices"]
+
+
+def test_fasta_golden_cases_batch_and_per_chunk(fasta_cases):
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    z = fasta_cases
+    cfg = _mem("gpu_golden")
+    for i in range(0, len(z["chunk_size"]), 7):
+        data = bytes(z["data"][z["data_off"][i]:z["data_off"][i + 1]])
+        exp = z["expected"][z["expected_off"][i]:z["expected_off"][i + 1]]
+        cs = int(z["chunk_size"][i])
+        for pc in ({}, {"backend": "sequential"}):
+            co = _co(FASTA, data, f"g{i}_{len(pc)}", cfg)
+            co.preprocess(parallel_config=pc, chunk_size=cs)
+            assert np.array_equal(_index(co), exp), (i, str(z["kind"][i]), cs, pc)
+            assert co.attributes.num_sequences == int(z["num_sequences"][i])
+
+
+@pytest.mark.parametrize("devices", ["0", "0,0", "0,0,0,0,0,0,0,0"])
+@pytest.mark.parametrize("div", [1, 4, 9, 64])
+def test_fasta_synthetic_groups(monkeypatch, devices, div):
+    from oracle import cpu_ref, dpref
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", devices)
+    data = synth.fasta(16 << 20, 7 + div)
+    cs = -(-len(data) // div)
+    co = _co(FASTA, data.tobytes(), f"syn{div}", _mem(f"gpu_syn_{div}_{len(devices)}"))
+    co.preprocess(chunk_size=cs)
+    exp = dpref.fasta_pairs(data, cpu_ref.chunk_plan(len(data), cs))
+    assert np.array_equal(_index(co), exp.reshape(-1).astype(np.uint32))
+
+
+def test_fasta_header_crossing_group_boundary(monkeypatch):
+    """A header line opened near the end of group 0's last chunk whose '\\n' lies far inside group 1's
+    region: group 0's buffer has no newline after it -> pending -> dp_find_delim on later bytes."""
+    from oracle import cpu_ref, dpref
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0")
+    n, cs = 1 << 20, 1 << 18                     # 4 chunks -> groups [0,2) [2,4); boundary at 2*cs
+    a = np.full(n, ord("A"), np.uint8)
+    a[::61] = 10
+    a[2 * cs - 300: 2 * cs + 200_000] = ord("x")  # one very long header line across the boundary
+    a[2 * cs - 300] = ord(">")
+    a[2 * cs - 301] = 10
+    a[-1] = 10
+    co = _co(FASTA, a.tobytes(), "cross", _mem("gpu_cross"))
+    co.preprocess(chunk_size=cs)
+    exp = dpref.fasta_pairs(a, cpu_ref.chunk_plan(n, cs))
+    got = _index(co).reshape(-1, 2)
+    assert np.array_equal(got, exp.astype(np.uint32))
+    assert any(e > 2 * cs + 100_000 for _, e in got.tolist())
+
+
+def test_fasta_quirk_every_chunk_to_eof():
+    """chunk_size == num_chunks - 1: every map job reads to EOF, headers repeat (handler.py:36-38)."""
+    from oracle import cpu_ref, dpref
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    cs = 200
+    data = synth.fasta(cs * (cs + 1) + 5, 3)
+    assert len(data) // cs == cs + 1
+    co = _co(FASTA, data.tobytes(), "quirk", _mem("gpu_quirk"))
+    co.preprocess(chunk_size=cs)
+    exp = dpref.fasta_pairs(data, cpu_ref.chunk_plan(len(data), cs))
+    assert len(exp) > 200 * 3
+    assert np.array_equal(_index(co), exp.reshape(-1).astype(np.uint32))
+
+
+# ------------------------------------------------------------------------------------------------ CSV / VCF
+@pytest.mark.parametrize("devices", ["0", "0,0,0"])
+def test_csv_line_index_and_partitions(monkeypatch, devices):
+    from dataplug_amd.formats.generic import csv as fcsv
+    from dataplug_amd.formats._lines import SliceError
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", devices)
+    g = json.load(open(os.path.join(GOLDEN, "csv_slices.json")))["objects"]
+    for rec in g:
+        data = bytes(synth.csv(1 << 16, 5)) if rec["object"] == "synth_csv" else rec["num_chunks"]["1"][0][2].encode()
+        co = _co(fcsv.CSV, data, rec["object"] + devices, _mem(f"gpu_csv_{rec['object']}_{len(devices)}"))
+        co.preprocess()
+        assert co.attributes.columns == rec["columns"]
+        lines = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.attributes.line_index_key)
+                              ["Body"].read(), "<u8")
+        assert np.array_equal(lines, np.flatnonzero(np.frombuffer(data, np.uint8) == 10))
+        for n, expected in rec["num_chunks"].items():
+            for s, e in zip(co.partition(fcsv.partition_num_chunks, num_chunks=int(n)), expected):
+                if isinstance(e[2], dict):
+                    with pytest.raises(SliceError):
+                        s.get()
+                else:
+                    assert s.get() == e[2]
+
+
+def test_csv_large_multi_part(monkeypatch):
+    from dataplug_amd.formats.generic import csv as fcsv
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0,0,0")
+    data = synth.csv(96 << 20, 9)
+    co = _co(fcsv.CSV, data.tobytes(), "big.csv", _mem("gpu_csv_big"))
+    co.preprocess()
+    lines = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.attributes.line_index_key)
+                          ["Body"].read(), "<u8")
+    assert np.array_equal(lines, np.flatnonzero(data == 10))
+    from oracle import cpu_ref
+    obj = data.tobytes()
+    for s in co.partition(fcsv.partition_num_chunks, num_chunks=25):
+        assert s.get() == cpu_ref.csv_slice_get(obj, co.attributes.columns, s.range_0, s.range_1, s.chunk_id, 25)
+
+
+def test_vcf_line_index_and_partitions(monkeypatch):
+    from dataplug_amd.formats.genomics import vcf as fvcf
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0")
+    g = json.load(open(os.path.join(GOLDEN, "vcf_slices.json")))["objects"]
+    rec = [r for r in g if r["object"] == "synth_vcf"][0]
+    data = bytes(synth.vcf(1 << 16, 6))
+    co = _co(fvcf.VCF, data, "s.vcf", _mem("gpu_vcf"))
+    co.preprocess()
+    assert co.attributes.body_offset == rec["body_offset"] and co.attributes.columns == rec["columns"]
+    meta = co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read().decode()
+    assert meta == rec["meta"]
+    for n, expected in rec["num_chunks"].items():
+        assert [s.get() for s in co.partition(fvcf.partition_num_chunks, num_chunks=int(n))] == \
+            [e[2] for e in expected]
+
+
+# ------------------------------------------------------------------------------------------------ FASTQ.gz
+def test_fastq_gz_reads():
+    from dataplug_amd.formats.genomics.fastq import FASTQGZip, load_read_index, partition_reads_batches
+    raw = synth.fastq(20_000, seed=4).tobytes()
+    co = _co(FASTQGZip, gzip.compress(raw, 6), "r.fastq.gz", _mem("gpu_fastq"))
+    co.preprocess()
+    lines = raw.split(b"\n")[:-1]
+    assert co.attributes.total_lines == len(lines) == 80_000
+    ends = load_read_index(co)
+    nl = np.flatnonzero(np.frombuffer(raw, np.uint8) == 10)
+    assert np.array_equal(ends, nl[3::4] + 1)
+    batches = co.partition(partition_reads_batches, num_batches=7)
+    got = [ln for b in batches for ln in b.get()]
+    assert got == [x.decode() for x in lines]

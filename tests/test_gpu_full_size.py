@@ -1,0 +1,78 @@
+"""BASELINE-size cases through the C ABI (device-resident), checked exactly.
+
+* 4 GiB synthetic FASTA, chunk_size = size/4 (BASELINE configs[1]) and size/64: every pair vs the C oracle.
+* 4.5 GiB FASTA: the uint32 index raises OverflowError like the reference; the uint64 index is exact.
+* 8 GiB CSV (configs[2] shape, scaled to keep the host check cheap): the input repeats a base block, so
+  the expected newline index is the base block's offsets shifted by every copy — checked in full, plus
+  every-4th (FASTQ read ends) on the same bytes.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from dataplug_amd import synth
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+GiB = 1 << 30
+
+
+def _plan(size, cs):
+    n = size // cs
+    return [(i * cs, size if cs == n - 1 else (i + 1) * cs) for i in range(n)]
+
+
+@pytest.fixture(scope="module")
+def fasta4(ctx):
+    host = synth.tiled_fasta_host(4 * GiB, seed=1)
+    d = ctx.workspace("full_in", len(host) + 64)
+    ctx.h2d(d.ptr, host)
+    return host, d
+
+
+@pytest.mark.parametrize("div", [4, 64])
+def test_fasta_4gib_exact(ctx, fasta4, div):
+    from oracle import dpref
+    host, d = fasta4
+    size = len(host)
+    plan = _plan(size, math.ceil(size / div))
+    pairs, pending, cend = ctx.fasta_index(d.ptr, size, 0, size, plan, u64=False, cap=size // 512)
+    assert (pending < 0).all()
+    exp = dpref.fasta_pairs(host, plan)
+    assert len(pairs) == len(exp) > 2_000_000
+    assert np.array_equal(pairs.astype(np.uint64), exp)
+    assert cend[-1] == len(exp)
+
+
+def test_fasta_over_4gib_overflow_and_u64(ctx):
+    from oracle import dpref
+    size = 4 * GiB + GiB // 2
+    host = synth.tiled_fasta_host(size, seed=2)
+    d = ctx.workspace("full_in", size + 64)
+    ctx.h2d(d.ptr, host)
+    plan = _plan(size, math.ceil(size / 4))
+    with pytest.raises(OverflowError):
+        ctx.fasta_index(d.ptr, size, 0, size, plan, u64=False, cap=size // 512)
+    pairs, pending, _ = ctx.fasta_index(d.ptr, size, 0, size, plan, u64=True, cap=size // 512)
+    exp = dpref.fasta_pairs(host, plan)
+    assert np.array_equal(pairs, exp)
+    assert int(pairs[-1, 1]) > 2**32
+
+
+def test_csv_8gib_newline_index(ctx):
+    base = synth.csv(64 * (1 << 20) - 333, 9)       # ends with '\n'
+    size = 8 * GiB
+    host = synth.tiled_host(base, size)
+    d = ctx.workspace("full_in", size + 64)
+    ctx.h2d(d.ptr, host)
+    del host
+    bnl = np.flatnonzero(base == 10).astype(np.uint64)
+    parts = []
+    for off, n in synth.tile_plan(len(base), size):
+        parts.append(bnl[bnl < n] + np.uint64(off))
+    exp = np.concatenate(parts)
+    got, nd = ctx.delim_index(d.ptr, size, 0, 0, size, delim=10, u64=True)
+    assert nd == len(exp) and np.array_equal(got, exp)
+    del got
+    got4, nd4 = ctx.delim_index(d.ptr, size, 0, 0, size, delim=10, every_k=4, emit_add=1, u64=True)
+    assert nd4 == len(exp) and np.array_equal(got4, exp[3::4] + np.uint64(1))

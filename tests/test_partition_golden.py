@@ -1,0 +1,156 @@
+"""Partition strategies + slice get() against the REFERENCE's own outputs (tests/golden/*.json).
+
+The index a strategy reads is built here from the object bytes (numpy: the newline positions / the golden
+FASTA index are inputs, not the thing under test); what is tested is the host logic that turns an index
+into slices — CSV/VCF bodies from the newline index (formats/_lines.py), FASTA slices, FASTQ batches.
+Objects: the reference's sample files are rebuilt from the golden single-slice get() and checked against
+the recorded sha256; synthetic objects are regenerated from their seeds (dataplug_amd.synth).
+"""
+import base64
+import json
+import os
+
+import numpy as np
+import pytest
+
+from dataplug_amd import synth
+from dataplug_amd.cloudobject import CloudObject
+from dataplug_amd.formats._lines import SliceError, store_line_index
+from dataplug_amd.preprocessing.handler import upload_metadata
+from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
+from dataplug_amd.storage import MemoryStore
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, begin=0):
+    store = f"golden_{name}_{fmt.co_class.__name__}"
+    MemoryStore._named.pop(store, None)
+    co = CloudObject.from_s3(fmt, f"s3://dataplug/{name}", fetch=False, s3_config={"endpoint_url": f"memory://{store}"})
+    co.storage.create_bucket(Bucket="dataplug")
+    co.storage.create_bucket(Bucket="dataplug.meta")
+    co.storage.put_object(Body=data, Bucket="dataplug", Key=name)
+    if nl:
+        arr = np.frombuffer(data, np.uint8)
+        off = np.flatnonzero(arr[begin:] == 10).astype(np.uint64) + np.uint64(begin)
+        attrs = dict(attrs, line_index_key=store_line_index(co, off), num_lines=len(off))
+    upload_metadata(co, PreprocessingMetadata(metadata=meta, attributes=attrs))
+    co.fetch()
+    return co
+
+
+def _csv_objects():
+    for rec in _load("csv_slices.json")["objects"]:
+        if rec["object"] == "synth_csv":
+            data = bytes(synth.csv(1 << 16, 5))
+        else:
+            data = rec["num_chunks"]["1"][0][2].encode()        # one slice from byte 0 = the whole object
+        assert synth.sha256(np.frombuffer(data, np.uint8)) == rec["sha256"]
+        yield rec, data
+
+
+def _vcf_objects():
+    for rec in _load("vcf_slices.json")["objects"]:
+        if rec["object"] == "synth_vcf":
+            data = bytes(synth.vcf(1 << 16, 6))
+        else:
+            one = rec["num_chunks"]["1"][0][2]                  # header meta + "\n" + body
+            body = one[len(rec["meta"]) + 1:].encode()
+            head = rec["meta"].encode() + b"\n"
+            data = head + body
+        if synth.sha256(np.frombuffer(data, np.uint8)) != rec["sha256"]:
+            pytest.skip(f"{rec['object']}: header not recoverable byte-exactly from the golden meta")
+        yield rec, data
+
+
+def test_csv_partitions_match_reference():
+    from dataplug_amd.formats.generic import csv as fcsv
+    checked = 0
+    for rec, data in _csv_objects():
+        co = _co(fcsv.CSV, rec["object"], data, {"columns": rec["columns"], "dtypes": rec["dtypes"]})
+        cases = [(fcsv.partition_num_chunks, {"num_chunks": int(n)}, v) for n, v in rec["num_chunks"].items()]
+        cases += [(fcsv.partition_chunk_size, {"chunk_size": int(c)}, v) for c, v in rec["chunk_size"].items()]
+        for strat, kw, expected in cases:
+            slices = co.partition(strat, **kw)
+            assert [[s.range_0, s.range_1] for s in slices] == [e[:2] for e in expected], (rec["object"], kw)
+            for s, e in zip(slices, expected):
+                if isinstance(e[2], dict):
+                    with pytest.raises(SliceError):
+                        s.get()
+                else:
+                    assert s.get() == e[2], (rec["object"], kw, s.chunk_id)
+                checked += 1
+    assert checked > 100
+
+
+def test_vcf_partitions_match_reference():
+    from dataplug_amd.formats.genomics import vcf as fvcf
+    for rec, data in _vcf_objects():
+        co = _co(fvcf.VCF, rec["object"], data,
+                 {"columns": rec["columns"], "vcf_attributes": rec["vcf_attributes"],
+                  "body_offset": rec["body_offset"]}, meta=rec["meta"].encode(), begin=rec["body_offset"])
+        for n, expected in rec["num_chunks"].items():
+            slices = co.partition(fvcf.partition_num_chunks, num_chunks=int(n))
+            assert [[s.range_0, s.range_1] for s in slices] == [e[:2] for e in expected]
+            for s, e in zip(slices, expected):
+                if isinstance(e[2], dict):
+                    with pytest.raises(SliceError):
+                        s.get()
+                else:
+                    assert s.get() == e[2], (rec["object"], n, s.chunk_id)
+
+
+def test_vcf_header_parse_matches_reference():
+    from dataplug_amd.formats.genomics.vcf import parse_vcf_header
+    import io
+    for rec, data in _vcf_objects():
+        header, meta, columns, bo = parse_vcf_header(io.BytesIO(data))
+        assert bo == rec["body_offset"]
+        assert columns == rec["columns"]
+        assert meta == rec["vcf_attributes"]
+        assert "\n".join(header) == rec["meta"]
+
+
+def _fasta_object(name):
+    if name == "sample":
+        z = np.load(os.path.join(GOLDEN, "fasta_cases.npz"))
+        kinds = list(z["kind"])
+        i = kinds.index("sample")
+        return bytes(z["data"][z["data_off"][i]:z["data_off"][i + 1]])
+    if name == "synth1":
+        return bytes(synth.fasta(1 << 18, 11))
+    return None
+
+
+def test_fasta_partitions_match_reference():
+    from dataplug_amd.formats.genomics import fasta as ffa
+    from oracle import cpu_ref          # checker: builds the index input the strategy reads
+    n_checked = 0
+    for rec in _load("fasta_slices.json"):
+        data = _fasta_object(rec["object"])
+        if data is None:
+            continue
+        idx, nseq = cpu_ref.fasta_index(data, rec["chunk_size"])
+        co = _co(ffa.FASTA, rec["object"], data, {"num_sequences": nseq}, meta=idx, nl=False)
+        slices = co.partition(ffa.partition_chunks_strategy, num_chunks=rec["num_chunks"])
+        got = [[s.offset, None if s.header is None else list(s.header), s.range_0, s.range_1] for s in slices]
+        assert got == rec["slices"], (rec["object"], rec["num_chunks"])
+        if "get" in rec:
+            assert [base64.b64encode(s.get()).decode() for s in slices] == rec["get"]
+        n_checked += 1
+    assert n_checked >= 5
+
+
+def test_fastq_read_batches_match_reference():
+    from dataplug_amd.formats.genomics.fastq import read_pairs
+    g = _load("fastq_batches.json")
+    for c in g["cases"]:
+        assert [list(p) for p in read_pairs(c["total_lines"], c["num_batches"])] == c["line_pairs"]
+    with pytest.raises(Exception) as e:
+        read_pairs(10, 2)
+    assert str(e.value) == g["non_multiple_of_4_error"]

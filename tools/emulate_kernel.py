@@ -2,7 +2,9 @@
 
 Every wave-level step of the HIP kernel is mirrored on 64-element arrays (one element per lane) with the
 same bit formulas, ballots, unit/wave/row geometry, function-form summaries and the 64-lane look-back
-window, so logic bugs show up here without a GPU.  Used by tests/test_kernel_model.py.
+window, so logic bugs show up here without a GPU.  Used by tests/test_kernel_model.py.  The model keeps 8 waves per
+unit (the kernel now runs 15 data waves + 1 coordinator, and a pipelined schedule); the per-row bit logic,
+the function-form summaries and their composition are unchanged by that, and are what this checks.
 """
 from __future__ import annotations
 
