@@ -185,7 +185,7 @@ def main():
         achieved = alg_bytes / kern_avg_max
         value = total_bytes / dt_max / GiB
         out = {
-            "metric": "fasta_index_scan_GiB_per_s_device_resident",
+            "metric": "GiB/s scanned (device-resident) + offsets/s, FASTA index at 1/2/4/8 MI355X",
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,

@@ -8,20 +8,24 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "dpscan.hip")
 OUT = os.path.join(HERE, "lib", "libdpscan.so")
+OUT_PROF = os.path.join(HERE, "lib", "libdpscan_prof.so")   # diagnostics: in-kernel section timers
 ARCH = os.environ.get("DPSCAN_ARCH", "gfx950")
 
 
-def build(verbose: bool = False) -> str:
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+def build(verbose: bool = False, prof: bool = False) -> str:
+    out = OUT_PROF if prof else OUT
+    os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-result", "-o", OUT + ".tmp", SRC]
+           "-Wno-unused-result", "-o", out + ".tmp", SRC]
+    if prof:
+        cmd.insert(1, "-DDP_PROF")
     if verbose:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(verbose="-v" in sys.argv))
+    print(build(verbose="-v" in sys.argv, prof="--prof" in sys.argv))

@@ -58,6 +58,27 @@ constexpr uint32_t kSpinLimit = 1u << 22;          // polls (with s_sleep) befor
 
 enum Mode { kFasta = 0, kDelim = 1 };
 
+// In-kernel section timers (diagnostics build only: -DDP_PROF).  Per workgroup and wave, kProfSlots
+// accumulated s_memtime deltas; read back with dp_debug_profile().
+#ifdef DP_PROF
+constexpr int kProfSlots = 8;
+constexpr int kProfWaves = 16;
+constexpr int kProfMaxGrid = 1024;
+__device__ unsigned long long g_prof[kProfMaxGrid * kProfWaves * kProfSlots];
+#define PROF_DECL uint64_t prof_acc[kProfSlots] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t prof_t = __builtin_amdgcn_s_memtime()
+#define PROF_MARK(slot) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[slot] += t_ - prof_t; prof_t = t_; } while (0)
+#define PROF_FLUSH(wave) do { if (__lane_id() == 0 && blockIdx.x < kProfMaxGrid) { for (int i_ = 0; i_ < kProfSlots; ++i_) \
+    g_prof[((uint64_t)blockIdx.x * kProfWaves + (wave)) * kProfSlots + i_] = prof_acc[i_]; } } while (0)
+#define PROF_ARG , uint64_t (&prof_acc)[kProfSlots], uint64_t& prof_t
+#define PROF_PASS , prof_acc, prof_t
+#else
+#define PROF_DECL do {} while (0)
+#define PROF_MARK(slot) do {} while (0)
+#define PROF_FLUSH(wave) do {} while (0)
+#define PROF_ARG
+#define PROF_PASS
+#endif
+
 struct ScanArgs {
   const uint8_t* base;         // 16-byte aligned base; coordinates below are relative to it
   uint64_t shift;              // buffer start - base (0..15)
@@ -492,7 +513,7 @@ __device__ __forceinline__ FRow fasta_row(uint32_t M, uint32_t nxt63, int last_b
 // incoming line state (hypothesis: the wave's range starts with S = false).
 template <int MODE>
 __device__ __forceinline__ Func phase_a(const ScanArgs& A, const Geo& g, Buf& b, Pend& p, uint32_t (&ms)[kRows][kWave],
-                                        int lane, int wave) {
+                                        int lane, int wave PROF_ARG) {
   uint64_t cnt = 0;
   uint32_t S = 0, nlseen = 0, fV = 0;
   int fn_off = -1;
@@ -500,6 +521,7 @@ __device__ __forceinline__ Func phase_a(const ScanArgs& A, const Geo& g, Buf& b,
   const uint64_t wbase = g.ubase + (uint64_t)wave * kWaveBytes;
   uint32_t rows = 0;
   wait_buf(b);                                       // this buffer landed; the other one stays in flight
+  PROF_MARK(0);
   uint4 v[kRows];
 #pragma unroll
   for (int r = 0; r < kRows; ++r) v[r] = make_uint4(b.x[r][0], b.x[r][1], b.x[r][2], b.x[r][3]);
@@ -559,6 +581,7 @@ __device__ __forceinline__ Func phase_a(const ScanArgs& A, const Geo& g, Buf& b,
   p.fV = fV;
   p.fn_off = fn_off;
   p.pad = 0;
+  PROF_MARK(1);
   return ws;
 }
 
@@ -655,9 +678,11 @@ __device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint3
 
 // Data wave, phase B of unit j once the coordinator has published its prefixes.
 template <int MODE>
-__device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int lane, int wave, Shared& sh) {
+__device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int lane, int wave, Shared& sh PROF_ARG) {
   const int s = (int)(j % kRing);
+  PROF_MARK(2);
   lds_wait_eq(&sh.ready[s], (uint32_t)j + 1u, A.err);
+  PROF_MARK(3);
   Pend p = sh.pend[s][wave];
   p.wbase = rfl64(p.wbase);
   p.rows = rfl(p.rows);
@@ -666,16 +691,18 @@ __device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int l
   const uint64_t P = rfl64(sh.P[s][wave]);
   const uint32_t S = rfl(sh.S[s][wave]);
   phase_b<MODE>(A, p, sh.m[s][wave], P, S, lane);
+  PROF_MARK(4);
 }
 
 // One data-wave step with unit k: phase A(k) on buffer b -> post -> prefetch the unit after next into
 // b -> phase B(k - kBLag).
 template <int MODE>
 __device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint64_t k, uint64_t u0, uint64_t G,
-                                          Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh) {
+                                          Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh
+                                          PROF_ARG) {
   const int s = (int)(k % kRing);
   Pend p;
-  const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave);
+  const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave PROF_PASS);
   if (lane == 0) {
     sh.cF[s][wave] = ws.cF; sh.cT[s][wave] = ws.cT; sh.sF[s][wave] = ws.sF; sh.sT[s][wave] = ws.sT;
     sh.pend[s][wave] = p;
@@ -684,7 +711,8 @@ __device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint6
   }
   const Geo g2 = geo_of(T, A.nchunks, A.nunits, u0 + (k + 2) * (uint64_t)G, cur);
   load_buf(b, A, g2, wave, lane);
-  if (k >= (uint64_t)kBLag) data_finish<MODE>(A, k - kBLag, lane, wave, sh);
+  if (k >= (uint64_t)kBLag) data_finish<MODE>(A, k - kBLag, lane, wave, sh PROF_PASS);
+  else PROF_MARK(2);
   g = gnext;
   gnext = g2;
 }
@@ -702,6 +730,7 @@ __device__ __forceinline__ Func unit_func(const Shared& sh, int s) {
 template <int MODE>
 __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint64_t u0, uint64_t G, uint64_t K,
                                             int lane, Shared& sh) {
+  PROF_DECL;
   Cursor cur{0, 0, 0, 0, 0, 0};
   uint64_t prevP = 0;
   uint32_t prevS = 0;
@@ -711,10 +740,13 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     const uint64_t want = (j + kLag + 1 < K) ? j + kLag + 1 : K;
     while (published < want) {
       const int s = (int)(published % kRing);
+      PROF_MARK(3);
       lds_wait_eq(&sh.done[s], (uint32_t)kDataWaves, A.err);
+      PROF_MARK(0);
       const uint64_t u = u0 + published * G;
       if (u > 0 && lane == 0) st_desc(&A.desc[u], pack_agg(unit_func(sh, s)));
       ++published;
+      PROF_MARK(1);
     }
     const int s = (int)(j % kRing);
     const uint64_t u = u0 + j * G;
@@ -722,7 +754,9 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     const Geo g = geo_of(T, A.nchunks, A.nunits, u, cur);
     uint64_t P;
     uint32_t S_in;
+    PROF_MARK(3);
     lookback(A, u, G, u >= G ? prevP : 0ull, u >= G ? prevS : 0u, lane, P, S_in);
+    PROF_MARK(2);
     const uint64_t P_incl = P + (S_in ? unit.cT : unit.cF);
     const uint32_t S_out = S_in ? unit.sT : unit.sF;
     prevP = P_incl;
@@ -747,6 +781,8 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
       lds_st(&sh.ready[s], (uint32_t)j + 1u);
     }
   }
+  PROF_MARK(3);
+  PROF_FLUSH(kCoord);
 }
 
 template <int MODE>
@@ -768,6 +804,7 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   if (wave == kCoord) {
     coordinator<MODE>(A, T, u0, G, K, lane, sh);
   } else {
+    PROF_DECL;
     Cursor cur{0, 0, 0, 0, 0, 0};
     Geo g = geo_of(T, A.nchunks, A.nunits, u0, cur);
     Geo gnext = geo_of(T, A.nchunks, A.nunits, u0 + G, cur);
@@ -775,15 +812,19 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
     load_buf(bA, A, g, wave, lane);
     load_buf(bB, A, gnext, wave, lane);
     uint64_t k = 0;
+    PROF_MARK(5);
     while (k < K) {
-      data_step<MODE>(A, T, k, u0, G, g, gnext, bA, cur, lane, wave, sh);
+      data_step<MODE>(A, T, k, u0, G, g, gnext, bA, cur, lane, wave, sh PROF_PASS);
       if (++k == K) break;
-      data_step<MODE>(A, T, k, u0, G, g, gnext, bB, cur, lane, wave, sh);
+      data_step<MODE>(A, T, k, u0, G, g, gnext, bB, cur, lane, wave, sh PROF_PASS);
       ++k;
     }
     drain_bufs(bA, bB);
+    PROF_MARK(6);
     const uint64_t j0 = K > (uint64_t)kBLag ? K - kBLag : 0;
-    for (uint64_t j = j0; j < K; ++j) data_finish<MODE>(A, j, lane, wave, sh);   // drain
+    for (uint64_t j = j0; j < K; ++j) data_finish<MODE>(A, j, lane, wave, sh PROF_PASS);   // drain
+    PROF_MARK(6);
+    PROF_FLUSH(wave);
   }
 }
 
@@ -1374,6 +1415,23 @@ int dp_timing_read(dp_ctx* c, double* total_ms, uint64_t* launches) {
   c->ms_acc = 0.0;
   c->launches = 0;
   return DP_OK;
+}
+
+int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slots, int* waves) {
+#ifdef DP_PROF
+  if (!c || !host_words) return fail(DP_ERR_INVALID, "dp_debug_profile: null argument");
+  const uint64_t n = n_words < (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots ? n_words
+                                                                                 : (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpyFromSymbol(host_words, HIP_SYMBOL(g_prof), n * 8, 0, hipMemcpyDeviceToHost));
+  if (slots) *slots = kProfSlots;
+  if (waves) *waves = kProfWaves;
+  return DP_OK;
+#else
+  (void)c; (void)host_words; (void)n_words; (void)slots; (void)waves;
+  return fail(DP_ERR_INVALID, "dp_debug_profile: library built without -DDP_PROF");
+#endif
 }
 
 int dp_scan_geometry(dp_ctx* c, int* grid, int* unit_bytes) {

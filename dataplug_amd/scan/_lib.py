@@ -53,6 +53,7 @@ SIGNATURES = [
     ("dp_stream_read", _c.c_int, [_p, _p, _u64, _c.c_int]),
     ("dp_timing_enable", _c.c_int, [_p, _c.c_int]),
     ("dp_timing_read", _c.c_int, [_p, _c.POINTER(_c.c_double), _u64p]),
+    ("dp_debug_profile", _c.c_int, [_p, _u64p, _u64, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
     ("dp_scan_geometry", _c.c_int, [_p, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
 ]
 

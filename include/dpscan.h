@@ -107,6 +107,11 @@ int dp_stream_read(dp_ctx* ctx, const void* d_buf, uint64_t bytes, int blocks_pe
 int dp_timing_enable(dp_ctx* ctx, int enable);
 int dp_timing_read(dp_ctx* ctx, double* total_ms, uint64_t* launches);   /* syncs; then resets */
 
+/* Diagnostics: per (workgroup, wave) in-kernel section timers of the last scan launch (s_memtime ticks,
+ * `slots` words per wave, `waves` waves per workgroup).  Only a library built with -DDP_PROF
+ * (lib/libdpscan_prof.so) records them; the production build returns DP_ERR_INVALID. */
+int dp_debug_profile(dp_ctx* ctx, uint64_t* host_words, uint64_t n_words, int* slots, int* waves);
+
 /* Launch geometry (for tests/tuning): workgroups of the persistent scan grid, and unit size in bytes. */
 int dp_scan_geometry(dp_ctx* ctx, int* grid, int* unit_bytes);
 

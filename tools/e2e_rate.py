@@ -1,0 +1,85 @@
+"""End-to-end (PCIe-inclusive) rate of the FASTA index build, for DESIGN.md §6 (never bench.py's value).
+
+    python tools/e2e_rate.py [--size BYTES] [--reps N]
+
+co.preprocess(chunk_size=size/4) on a synthetic FASTA held by (a) an in-process store (memory://) and
+(b) the loopback HTTP S3 server: ranged GETs into pinned host memory -> H2D -> scan -> D2H of the index
+-> PUT of index + attrs.  Also times the stages separately on the same object.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dataplug_amd import synth  # noqa: E402
+from dataplug_amd.cloudobject import CloudObject  # noqa: E402
+from dataplug_amd.formats.genomics.fasta import FASTA  # noqa: E402
+from dataplug_amd.scan import get_context  # noqa: E402
+from dataplug_amd.scan import objects as so  # noqa: E402
+from dataplug_amd.storage import LoopbackS3Server, MemoryStore  # noqa: E402
+
+GiB = float(1 << 30)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=4 << 30)
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    size = args.size
+    host = synth.tiled_fasta_host(size, seed=1)
+    store = MemoryStore.named("e2e")
+    store.create_bucket("genomics")
+    store.create_bucket("genomics.meta")
+    store.put("genomics", "x.fasta", memoryview(host))
+    del host
+    cs = math.ceil(size / 4)
+    res = {"object_bytes": size, "chunk_size": cs}
+    srv = LoopbackS3Server(store).start()
+    for name, cfg in (("memory", {"endpoint_url": "memory://e2e"}), ("loopback_http", srv.storage_config)):
+        co = CloudObject.from_s3(FASTA, "s3://genomics/x.fasta", s3_config=cfg)
+        co.preprocess(chunk_size=cs, force=True)          # warm: context, pinned + device buffers
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            co.preprocess(chunk_size=cs, force=True)
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        res[f"{name}_preprocess_s"] = round(t, 3)
+        res[f"{name}_GiB_per_s"] = round(size / t / GiB, 2)
+        print(name, res, flush=True)
+    # stage breakdown (memory store)
+    co = CloudObject.from_s3(FASTA, "s3://genomics/x.fasta", s3_config={"endpoint_url": "memory://e2e"})
+    ctx = get_context(0)
+    pin = ctx.pinned("object", size)
+    t0 = time.perf_counter()
+    so.read_range_into(co.storage, "genomics", "x.fasta", 0, size, pin.view(size))
+    t_get = time.perf_counter() - t0
+    d = ctx.workspace("input", size + 64)
+    ctx.sync()
+    t0 = time.perf_counter()
+    ctx.h2d_async(d.ptr, pin.ptr, size)
+    ctx.sync()
+    t_h2d = time.perf_counter() - t0
+    plan = [(i * cs, min(size, (i + 1) * cs)) for i in range(size // cs)]
+    ctx.fasta_index(d.ptr, size, 0, size, plan)
+    t0 = time.perf_counter()
+    pairs, _, _ = ctx.fasta_index(d.ptr, size, 0, size, plan)
+    t_scan = time.perf_counter() - t0
+    res.update({"stage_get_into_pinned_GiB_per_s": round(size / t_get / GiB, 2),
+                "stage_h2d_GiB_per_s": round(size / t_h2d / GiB, 2),
+                "stage_scan_plus_d2h_s": round(t_scan, 4), "index_bytes": int(pairs.nbytes)})
+    srv.stop()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
