@@ -43,7 +43,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--traffic-bytes", type=float, default=None,
-                   help="HBM bytes per scan launch from a rocprofv3 --pmc pass (profiles/), if measured")
+                   help="HBM bytes per scan launch from a rocprofv3 --pmc pass (overrides --traffic-from)")
+    p.add_argument("--traffic-from", default=os.path.join(REPO, "profiles", "latest_pmc_summary.json"),
+                   help="pmc_summary.json (tools/pmc_summary.py) of this same command: FETCH_SIZE x2 (gfx950) "
+                        "+ WRITE_SIZE per scan_kernel<FASTA> launch")
     return p.parse_args()
 
 
@@ -180,6 +183,14 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(host, chunk_size)
 
+    traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
+    if traffic is None and args.traffic_from and os.path.exists(args.traffic_from):
+        with open(args.traffic_from) as f:
+            pmc = json.load(f)
+        if pmc.get("object_bytes", size) == size and "hbm_traffic_bytes" in pmc:
+            traffic = pmc["hbm_traffic_bytes"]
+            traffic_src = os.path.relpath(os.path.realpath(args.traffic_from), REPO)
+
     if rank == 0:
         alg_bytes = size + 8.0 * n_pairs            # N input bytes read once + 8 B per (start, end) pair
         achieved = alg_bytes / kern_avg_max
@@ -204,7 +215,8 @@ def main():
             "offsets_per_s": round(total_offsets / dt_max, 1),
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": args.traffic_bytes,
+                         "traffic": None if traffic is None else int(traffic),
+                         "traffic_source": traffic_src,
                          "kernel": "scan_kernel<FASTA>", "kernel_avg_us": round(kern_avg_max * 1e6, 2),
                          "alg_bytes_per_launch": int(alg_bytes)},
             "cpu_baseline": cpu,

@@ -9,6 +9,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "dpscan.hip")
 OUT = os.path.join(HERE, "lib", "libdpscan.so")
 OUT_PROF = os.path.join(HERE, "lib", "libdpscan_prof.so")   # diagnostics: in-kernel section timers
+GZ_SRC = os.path.join(HERE, "csrc", "dpgz.c")
+GZ_OUT = os.path.join(HERE, "lib", "libdpgz.so")            # host-side gzip access-point index (zlib)
 ARCH = os.environ.get("DPSCAN_ARCH", "gfx950")
 
 
@@ -27,5 +29,14 @@ def build(verbose: bool = False, prof: bool = False) -> str:
     return out
 
 
+def build_gz() -> str:
+    os.makedirs(os.path.dirname(GZ_OUT), exist_ok=True)
+    cc = os.environ.get("CC", "gcc")
+    subprocess.run([cc, "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-o", GZ_OUT + ".tmp", GZ_SRC, "-lz"], check=True)
+    os.replace(GZ_OUT + ".tmp", GZ_OUT)
+    return GZ_OUT
+
+
 if __name__ == "__main__":
+    print(build_gz())
     print(build(verbose="-v" in sys.argv, prof="--prof" in sys.argv))

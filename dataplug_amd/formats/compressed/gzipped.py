@@ -1,23 +1,29 @@
-"""Gzipped text (dataplug/formats/compressed/gzipped.py) with a GPU line/read index of the inflated stream.
+"""Gzipped text (dataplug/formats/compressed/gzipped.py) with a GPU line/read index and native access points.
 
 The reference shells out to gztool 1.4.3 (gzipped.py:26-153; not vendored, not installed here) for
-``total_lines`` and a window table.  Here the object is inflated on the host (zlib, multi-member) and the
-inflated bytes are scanned on the GPU: ``total_lines`` = number of '\\n' (+1 for a final unterminated
-line — gztool's own convention is unpinned), plus the ``uint64`` end offset of every
-``record_lines``-th line (FASTQ: every read) stored at ``<key>.records``.  The window table keeps the
-reference's parquet columns; this round it holds the stream-start entry only, so slices inflate from the
-start of the object (random-access checkpoints are the next step).
+``total_lines``, a window table and a binary index that lets a slice resume inflating mid-object.  Here:
+
+* libdpgz.so (zlib, ``dataplug_amd/csrc/dpgz.c``) inflates the object once and records access points at
+  deflate block boundaries every ``span`` inflated bytes plus every gzip member start;
+* the inflated bytes are scanned on the GPU (``dp_delim_index``): every '\n' offset, from which
+  ``total_lines`` (+1 for a final unterminated line — gztool's own convention is unpinned),
+  each point's line number and the per-record (FASTQ read) end offsets follow;
+* the meta object is the window table as parquet with the reference's columns (window, compressed_byte,
+  uncompressed_byte, line_number, window_size, window_offset) plus ``bits``, ``member_start`` and
+  ``line_start``; the 32 KiB windows are stored at ``attributes.index_key`` (``<key>.idx``) and the
+  record ends (uint64) at ``<key>.records``;
+* ``GZipTextSlice`` resumes at the last point at or before its first line (``dataplug_amd.gz``).
 """
 from __future__ import annotations
 
 import io
 import logging
-import zlib
 from math import ceil
 from typing import TYPE_CHECKING, Iterator, List
 
 import numpy as np
 
+from ... import gz as gzidx
 from ...entities import CloudDataFormat, CloudObjectSlice, PartitioningStrategy
 from ...preprocessing.metadata import PreprocessingMetadata
 from ...scan import objects as scan_objects
@@ -29,25 +35,9 @@ if TYPE_CHECKING:
 logger = logging.getLogger(__name__)
 
 CHUNK_SIZE = 1 << 20
-WINDOW_COLUMNS = ["window", "compressed_byte", "uncompressed_byte", "line_number", "window_size", "window_offset"]
-
-
-def inflate_stream(chunks: Iterator[bytes]) -> Iterator[bytes]:
-    """Inflate a (possibly multi-member) gzip byte stream."""
-    d = zlib.decompressobj(wbits=31)
-    for c in chunks:
-        while c:
-            out = d.decompress(c)
-            if out:
-                yield out
-            if d.eof:
-                c = d.unused_data
-                d = zlib.decompressobj(wbits=31)
-            else:
-                c = b""
-    tail = d.flush()
-    if tail:
-        yield tail
+SPAN = 4 << 20
+WINDOW_COLUMNS = ["window", "compressed_byte", "uncompressed_byte", "line_number", "window_size", "window_offset",
+                  "bits", "member_start", "line_start"]
 
 
 def _body_chunks(body, size: int = CHUNK_SIZE) -> Iterator[bytes]:
@@ -58,30 +48,52 @@ def _body_chunks(body, size: int = CHUNK_SIZE) -> Iterator[bytes]:
         yield c
 
 
-def inflate_object(cloud_object) -> bytes:
-    res = cloud_object.storage.get_object(Bucket=cloud_object.path.bucket, Key=cloud_object.path.key)
-    with res["Body"] as body:
-        return b"".join(inflate_stream(_body_chunks(body)))
+def window_table(inflated: np.ndarray, points: np.ndarray, newlines: np.ndarray):
+    """(window table rows, windows blob) for the access points of one object."""
+    rows, blobs, off = [], [], 0
+    for i, p in enumerate(points):
+        ob = int(p["out_byte"])
+        w = b"" if p["member_start"] else gzidx.window_of(inflated, ob)
+        line = int(np.searchsorted(newlines, np.uint64(ob))) + 1       # line holding byte ob (1-based)
+        at_start = ob == 0 or int(inflated[ob - 1]) == 10
+        rows.append([i, int(p["in_byte"]), ob, line, len(w), off, int(p["bits"]), int(p["member_start"]), int(at_start)])
+        blobs.append(w)
+        off += len(w)
+    return rows, b"".join(blobs)
 
 
-def preprocess_gzip(cloud_object: "CloudObject", record_lines: int = 4) -> PreprocessingMetadata:
+def preprocess_gzip(cloud_object: "CloudObject", record_lines: int = 4, span: int = SPAN) -> PreprocessingMetadata:
     import pandas as pd
 
-    text = inflate_object(cloud_object)
-    ends, n_newlines = scan_objects.record_index_bytes(text, delim=10, every_k=record_lines, emit_add=1)
-    total_lines = n_newlines + (1 if text and text[-1:] != b"\n" else 0)
-    records_key = cloud_object.meta_path.key + ".records"
-    cloud_object.storage.put_object(Body=np.ascontiguousarray(ends, dtype="<u8").tobytes(),
-                                    Bucket=cloud_object.meta_path.bucket, Key=records_key,
-                                    Metadata={"dataplug": __version__})
-    df = pd.DataFrame([[0, 0, 0, 1, 0, 0]], columns=WINDOW_COLUMNS).set_index(["window"])
+    res = cloud_object.storage.get_object(Bucket=cloud_object.path.bucket, Key=cloud_object.path.key)
+    with res["Body"] as body:
+        data = body.read()
+    inflated, points = gzidx.build_index(data, span=span)
+    del data
+    newlines, n_nl = scan_objects.record_index_bytes(inflated, delim=10, every_k=1, emit_add=0)
+    total_lines = n_nl + (1 if len(inflated) and inflated[-1] != 10 else 0)
+    ends = newlines[record_lines - 1::record_lines] + np.uint64(1)
+    rows, windows = window_table(inflated, points, newlines)
+    meta = cloud_object.meta_path
+    idx_key, rec_key = meta.key + ".idx", meta.key + ".records"
+    st = cloud_object.storage
+    st.put_object(Body=windows, Bucket=meta.bucket, Key=idx_key, Metadata={"dataplug": __version__})
+    st.put_object(Body=np.ascontiguousarray(ends, dtype="<u8").tobytes(), Bucket=meta.bucket, Key=rec_key,
+                  Metadata={"dataplug": __version__})
+    df = pd.DataFrame(rows, columns=WINDOW_COLUMNS).set_index(["window"])
     out = io.BytesIO()
     df.to_parquet(out, engine="pyarrow")
     out.seek(0)
     return PreprocessingMetadata(metadata=out, attributes={
-        "total_lines": int(total_lines), "index_key": cloud_object.meta_path.key,
-        "records_key": records_key, "record_lines": int(record_lines), "num_records": int(len(ends)),
-        "uncompressed_size": len(text)})
+        "total_lines": int(total_lines), "index_key": idx_key, "records_key": rec_key,
+        "record_lines": int(record_lines), "num_records": int(len(ends)), "uncompressed_size": int(len(inflated)),
+        "gzip_members": int(points["member_start"].sum())})
+
+
+def load_window_table(cloud_object):
+    import pandas as pd
+    meta = cloud_object.storage.get_object(Bucket=cloud_object.meta_path.bucket, Key=cloud_object.meta_path.key)
+    return pd.read_parquet(io.BytesIO(meta["Body"].read()))
 
 
 def _get_ranges_from_line_pairs(cloud_object: "CloudObject", pairs):
@@ -125,23 +137,54 @@ class GZipTextSlice(CloudObjectSlice):
         want = self.line_1 - self.line_0
         if want <= 0:
             return
-        res = co.storage.get_object(Bucket=co.path.bucket, Key=co.path.key)
-        line_no = 1
+        df = load_window_table(co)
+        ln = df["line_number"].to_numpy()
+        ok = (ln < self.line_0) | ((ln == self.line_0) & (df["line_start"].to_numpy() == 1))
+        i = int(np.flatnonzero(ok)[-1]) if ok.any() else 0
+        row = df.iloc[i]
+        points = np.zeros(len(df), gzidx.POINT_DTYPE)
+        points["in_byte"] = df["compressed_byte"].to_numpy()
+        points["out_byte"] = df["uncompressed_byte"].to_numpy()
+        points["bits"] = df["bits"].to_numpy()
+        points["member_start"] = df["member_start"].to_numpy()
+        window = b""
+        if int(row["window_size"]):
+            w0 = int(row["window_offset"])
+            window = co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.attributes.index_key,
+                                           Range=f"bytes={w0}-{w0 + int(row['window_size']) - 1}")["Body"].read()
+
+        def fetch(offset: int):
+            if offset >= co.size:
+                return
+            body = co.storage.get_object(Bucket=co.path.bucket, Key=co.path.key, Range=f"bytes={offset}-")["Body"]
+            with body:
+                yield from _body_chunks(body)
+
+        skip = self.line_0 - int(row["line_number"])       # newlines to pass before line_0 starts
         carry = b""
         emitted = 0
-        with res["Body"] as body:
-            for piece in inflate_stream(_body_chunks(body)):
-                buf = carry + piece
-                parts = buf.split(b"\n")
-                carry = parts.pop()
-                for p in parts:
-                    if line_no >= self.line_0:
-                        yield p.decode("utf-8")
-                        emitted += 1
-                        if emitted >= want:
-                            return
-                    line_no += 1
-        if carry and line_no >= self.line_0 and emitted < want:
+        for piece in gzidx.inflate_from(points, i, window, fetch):
+            buf = carry + piece
+            if skip:
+                pos = 0
+                while skip:
+                    nl = buf.find(b"\n", pos)
+                    if nl < 0:
+                        break
+                    pos = nl + 1
+                    skip -= 1
+                if skip:
+                    carry = b""
+                    continue
+                buf = buf[pos:]
+            parts = buf.split(b"\n")
+            carry = parts.pop()
+            for p in parts:
+                yield p.decode("utf-8")
+                emitted += 1
+                if emitted >= want:
+                    return
+        if carry and not skip and emitted < want:
             yield carry.decode("utf-8")
 
     def get(self) -> List[str]:

@@ -188,8 +188,10 @@ def test_vcf_line_index_and_partitions(monkeypatch):
 def test_fastq_gz_reads():
     from dataplug_amd.formats.genomics.fastq import FASTQGZip, load_read_index, partition_reads_batches
     raw = synth.fastq(20_000, seed=4).tobytes()
-    co = _co(FASTQGZip, gzip.compress(raw, 6), "r.fastq.gz", _mem("gpu_fastq"))
-    co.preprocess()
+    blob = gzip.compress(raw[:1_000_003], 6) + gzip.compress(raw[1_000_003:], 1)     # two members
+    co = _co(FASTQGZip, blob, "r.fastq.gz", _mem("gpu_fastq"))
+    co.preprocess(extra_args={"span": 1 << 16})
+    assert co.attributes.gzip_members == 2
     lines = raw.split(b"\n")[:-1]
     assert co.attributes.total_lines == len(lines) == 80_000
     ends = load_read_index(co)
