@@ -14,14 +14,16 @@ GZ_OUT = os.path.join(HERE, "lib", "libdpgz.so")            # host-side gzip acc
 ARCH = os.environ.get("DPSCAN_ARCH", "gfx950")
 
 
-def build(verbose: bool = False, prof: bool = False) -> str:
-    out = OUT_PROF if prof else OUT
+def build(verbose: bool = False, prof: bool = False, defines=(), out=None) -> str:
+    out = out or (OUT_PROF if prof else OUT)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
            "-Wno-unused-result", "-o", out + ".tmp", SRC]
     if prof:
         cmd.insert(1, "-DDP_PROF")
+    for d in defines:                      # tuning variants, e.g. DP_RING=5 (tools/probe_perf.py)
+        cmd.insert(1, f"-D{d}")
     if verbose:
         cmd.append("-Rpass-analysis=kernel-resource-usage")
     subprocess.run(cmd, check=True)

@@ -41,9 +41,16 @@ constexpr int kRowBytes = kWave * 16;              // one dwordx4 per lane
 constexpr int kRows = 8;                           // rows per wave per unit
 constexpr int kWaveBytes = kRowBytes * kRows;      // 8 KiB
 constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 120 KiB look-back unit
-constexpr int kRing = 4;                           // LDS ring depth (units in flight per workgroup)
+#ifndef DP_RING
+#define DP_RING 4
+#endif
+#ifndef DP_PRIO
+#define DP_PRIO 1
+#endif
+constexpr int kRing = DP_RING;                     // LDS ring depth (units in flight per workgroup)
 constexpr int kLag = 2;                            // resolve(j) once AGG(j + kLag) is out
-constexpr int kBLag = kLag + 1;                    // data waves run phase B(j) after phase A(j + kBLag)
+constexpr int kBLag = kRing - 1;                   // data waves run phase B(j) after phase A(j + kBLag)
+static_assert(kBLag < kRing && kLag < kBLag, "ring slots: A(k+1) reuses the slot of B(k+1-kRing)");
 constexpr uint32_t kGT = 0x3E3E3E3Eu;              // '>'
 constexpr uint32_t kNL = 0x0A0A0A0Au;              // '\n'
 constexpr uint32_t kOdd = 0xAAAAAAAAu, kEven = 0x55555555u;
@@ -105,10 +112,18 @@ __device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t pat) {
   const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
   return ~(t | x) & 0x80808080u;
 }
+// v_mul_u32_u24 with a literal multiplier.  The compiler otherwise hoists the constant into an SGPR and
+// emits the quarter-rate v_mul_lo_u32.
+template <uint32_t K>
+__device__ __forceinline__ uint32_t mul24k(uint32_t a) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "i"(K), "v"(a));
+  return r;
+}
 __device__ __forceinline__ uint32_t pack4(uint32_t e) {
   // bits 7,15,23,31 -> bits 0..3 (mul_u32_u24 gather)
   const uint32_t f = e >> 7;
-  return ((((f & 0x10101u) * 0x4081u) >> 14) & 7u) | (f >> 21);
+  return ((mul24k<0x4081u>(f & 0x10101u) >> 14) & 7u) | (f >> 21);
 }
 __device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t pat) {
   return pack4(eq4(v.x, pat)) | (pack4(eq4(v.y, pat)) << 4) | (pack4(eq4(v.z, pat)) << 8) |
@@ -118,7 +133,7 @@ __device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t pat) {
 // bytes 0..2 are gathered by one mul_u32_u24 (partial products land on disjoint bits: no carries).
 __device__ __forceinline__ uint32_t pair8(uint32_t w) {
   const uint32_t c = (eq4(w, kGT) | (eq4(w, kNL) >> 1)) >> 6;   // byte j: bit 8j = nl, 8j+1 = gt
-  const uint32_t t = (((c & 0x30303u) * 0x41041u) >> 18) & 0x3Fu;
+  const uint32_t t = (mul24k<0x41041u>(c & 0x30303u) >> 18) & 0x3Fu;
   return t | ((c >> 18) & 0xC0u);
 }
 __device__ __forceinline__ uint32_t pairs32(const uint4& v) {
@@ -197,6 +212,22 @@ __device__ __forceinline__ void lds_add(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
+// Issue priority (s_setprio takes an immediate).  The 4 data waves sharing a SIMD (w, w+4, w+8, w+12)
+// otherwise get issue slots by age: the youngest is starved, and as every unit waits for its slowest
+// wave the older ones idle.  Rotating the priority per unit gives each wave every rank once in 4 units.
+__device__ __forceinline__ void set_prio(uint32_t p) {
+#if DP_PRIO
+  switch (p & 3u) {
+    case 0: __builtin_amdgcn_s_setprio(0); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    default: __builtin_amdgcn_s_setprio(3); break;
+  }
+#else
+  (void)p;
+#endif
+}
+
 // Summary of a byte range as a function of the incoming line state S (does the current line already
 // hold an emitted header?): count and outgoing state for S = false (F) and S = true (T).
 struct Func {
@@ -204,11 +235,15 @@ struct Func {
   uint32_t sF, sT;
 };
 __device__ __forceinline__ Func f_then(const Func& a, const Func& b) {   // a, then b
+  const uint64_t bF = b.cF, bT = b.cT;
+  const uint32_t bsF = b.sF, bsT = b.sT;
+  const uint32_t mF = 0u - (a.sF & 1u), mT = 0u - (a.sT & 1u);
+  const uint64_t mF64 = 0ull - (uint64_t)(a.sF & 1u), mT64 = 0ull - (uint64_t)(a.sT & 1u);
   Func r;
-  r.cF = a.cF + (a.sF ? b.cT : b.cF);
-  r.sF = a.sF ? b.sT : b.sF;
-  r.cT = a.cT + (a.sT ? b.cT : b.cF);
-  r.sT = a.sT ? b.sT : b.sF;
+  r.cF = a.cF + ((bT & mF64) | (bF & ~mF64));
+  r.sF = (bsT & mF) | (bsF & ~mF);
+  r.cT = a.cT + ((bT & mT64) | (bF & ~mT64));
+  r.sT = (bsT & mT) | (bsF & ~mT);
   return r;
 }
 __device__ __forceinline__ uint64_t pack_agg(const Func& f) {
@@ -233,14 +268,24 @@ struct LB {
   uint32_t fl;     // bit0 sF, bit1 sT, bit2 inclusive prefix
 };
 __device__ __forceinline__ LB lb_ident() { return LB{0, 0, 2u}; }
+// mask selects: `c ? x : y` on struct members otherwise becomes an indexed stack copy (scratch)
+__device__ __forceinline__ uint64_t sel64(uint32_t c, uint64_t x, uint64_t y) {
+  const uint64_t m = 0ull - (uint64_t)(c & 1u);
+  return (x & m) | (y & ~m);
+}
+__device__ __forceinline__ uint32_t sel32(uint32_t c, uint32_t x, uint32_t y) {
+  const uint32_t m = 0u - (c & 1u);
+  return (x & m) | (y & ~m);
+}
 __device__ __forceinline__ LB lb_then(const LB& a, const LB& b) {   // a (farther), then b (nearer)
-  if (b.fl & 4u) return b;
   const uint32_t asF = a.fl & 1u, asT = (a.fl >> 1) & 1u;
   const uint32_t bsF = b.fl & 1u, bsT = (b.fl >> 1) & 1u;
+  const uint32_t bp = (b.fl >> 2) & 1u;              // b is an inclusive prefix: absorbs a
+  const uint64_t bF = b.cF, bT = b.cT;
   LB r;
-  r.cF = a.cF + (asF ? b.cT : b.cF);
-  r.cT = a.cT + (asT ? b.cT : b.cF);
-  r.fl = (asF ? bsT : bsF) | ((asT ? bsT : bsF) << 1) | (a.fl & 4u);
+  r.cF = sel64(bp, bF, a.cF + sel64(asF, bT, bF));
+  r.cT = sel64(bp, bT, a.cT + sel64(asT, bT, bF));
+  r.fl = sel32(bp, b.fl, sel32(asF, bsT, bsF) | (sel32(asT, bsT, bsF) << 1) | (a.fl & 4u));
   return r;
 }
 __device__ __forceinline__ LB lb_from_desc(uint64_t d) {
@@ -253,10 +298,36 @@ __device__ __forceinline__ LB lb_from_desc(uint64_t d) {
   }
   return lb_ident();
 }
-__device__ __forceinline__ uint64_t shfl_down64(uint64_t x, int s) {
-  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)x, s);
-  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(x >> 32), s);
-  return ((uint64_t)hi << 32) | lo;
+
+// DPP lane moves (VALU, no LDS round trip).  Lanes whose source is outside the pattern get `old`.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)x, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t x, uint64_t old) {
+  return ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(x >> 32), (uint32_t)(old >> 32)) << 32) |
+         dpp32<CTRL, ROWS>((uint32_t)x, (uint32_t)old);
+}
+constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
+constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;   // gfx9 DPP: lane 15 / 31 to the next row(s)
+
+template <int CTRL, int ROWS>
+__device__ __forceinline__ LB lb_dpp(const LB& f) {       // identity where there is no source lane
+  LB o;
+  o.cF = dpp64<CTRL, ROWS>(f.cF, 0ull);
+  o.cT = dpp64<CTRL, ROWS>(f.cT, 0ull);
+  o.fl = dpp32<CTRL, ROWS>(f.fl, 2u);
+  return o;
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ Func fn_dpp(const Func& f) {
+  Func o;
+  o.cF = dpp64<CTRL, ROWS>(f.cF, 0ull);
+  o.cT = dpp64<CTRL, ROWS>(f.cT, 0ull);
+  o.sF = dpp32<CTRL, ROWS>(f.sF, 0u);
+  o.sT = dpp32<CTRL, ROWS>(f.sT, 1u);
+  return o;
 }
 
 constexpr uint64_t kIdentDesc = kStatMask;   // status 3: "no unit here" (identity, always valid)
@@ -269,6 +340,7 @@ __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t
                                       int lane, uint64_t& P, uint32_t& S_in) {
   const uint64_t W = u < G - 1 ? u : G - 1;          // D[k] = desc[u-1-k] for k < W, D[W] = base prefix
   const uint64_t basedesc = pack_prefix(baseP, baseS);
+  const int rl = kWave - 1 - lane;                   // lane 63 holds the nearest descriptors
   LB acc = lb_ident();
   for (uint64_t k0 = 0;; k0 += 4 * kWave) {
     uint64_t d[4];
@@ -277,7 +349,7 @@ __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t
     for (;;) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint64_t k = k0 + 4 * (uint64_t)lane + j;
+        const uint64_t k = k0 + 4 * (uint64_t)rl + j;
         d[j] = k < W ? ld_desc(&A.desc[u - 1 - k]) : (k == W ? basedesc : kIdentDesc);
       }
       uint32_t seen = 0, bad = 0;
@@ -289,8 +361,9 @@ __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t
       }
       PB = __ballot(seen);
       const uint64_t BB = __ballot(bad);
-      const uint64_t upto = PB ? (((PB & (0ull - PB)) << 1) - 1ull) : ~0ull;   // lanes 0..first prefix lane
-      if ((BB & upto) == 0ull) break;
+      // lanes from the nearest one (63) down to the nearest lane holding a prefix must all be published
+      const uint64_t need = PB ? ~((1ull << (63 - __builtin_clzll(PB))) - 1ull) : ~0ull;
+      if ((BB & need) == 0ull) break;
       if (++spins > kSpinLimit) {
         if (lane == 0) atomicOr(A.err, kErrTimeout);
         d[0] = pack_prefix(0, 0);
@@ -304,18 +377,17 @@ __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t
     f = lb_then(f, lb_from_desc(d[2]));
     f = lb_then(f, lb_from_desc(d[1]));
     f = lb_then(f, lb_from_desc(d[0]));
-#pragma unroll
-    for (int s = 1; s < kWave; s <<= 1) {
-      LB o;
-      o.cF = shfl_down64(f.cF, s);
-      o.cT = shfl_down64(f.cT, s);
-      o.fl = (uint32_t)__shfl_down((int)f.fl, s);
-      if (lane + s < kWave) f = lb_then(o, f);
-    }
+    // inclusive scan, lane 0 (farthest) -> lane 63 (nearest): farther composed in front of nearer
+    f = lb_then(lb_dpp<kRowShr1, 0xF>(f), f);
+    f = lb_then(lb_dpp<kRowShr2, 0xF>(f), f);
+    f = lb_then(lb_dpp<kRowShr4, 0xF>(f), f);
+    f = lb_then(lb_dpp<kRowShr8, 0xF>(f), f);
+    f = lb_then(lb_dpp<kRowBcast15, 0xA>(f), f);
+    f = lb_then(lb_dpp<kRowBcast31, 0xC>(f), f);
     LB F;
-    F.cF = readlane64(f.cF, 0);
-    F.cT = readlane64(f.cT, 0);
-    F.fl = (uint32_t)__builtin_amdgcn_readlane((int)f.fl, 0);
+    F.cF = readlane64(f.cF, kWave - 1);
+    F.cT = readlane64(f.cT, kWave - 1);
+    F.fl = (uint32_t)__builtin_amdgcn_readlane((int)f.fl, kWave - 1);
     acc = lb_then(F, acc);
     if (PB) break;
   }
@@ -452,6 +524,10 @@ struct Pend {
 struct Shared {
   uint64_t cF[kRing][kDataWaves], cT[kRing][kDataWaves];   // per-wave summaries
   uint32_t sF[kRing][kDataWaves], sT[kRing][kDataWaves];
+  uint64_t exF[kRing][kDataWaves], exT[kRing][kDataWaves];  // per-wave exclusive prefix functions (coordinator)
+  uint32_t esF[kRing][kDataWaves], esT[kRing][kDataWaves];
+  uint64_t uF[kRing], uT[kRing];                            // the unit's function
+  uint32_t usF[kRing], usT[kRing];
   uint64_t P[kRing][kDataWaves];                           // per-wave prefixes from the coordinator
   uint32_t S[kRing][kDataWaves];
   uint32_t done[kRing];                                    // data waves finished phase A of the slot's unit
@@ -679,7 +755,7 @@ __device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint3
 // Data wave, phase B of unit j once the coordinator has published its prefixes.
 template <int MODE>
 __device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int lane, int wave, Shared& sh PROF_ARG) {
-  const int s = (int)(j % kRing);
+  const int s = (int)((uint32_t)j % (uint32_t)kRing);
   PROF_MARK(2);
   lds_wait_eq(&sh.ready[s], (uint32_t)j + 1u, A.err);
   PROF_MARK(3);
@@ -700,7 +776,8 @@ template <int MODE>
 __device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint64_t k, uint64_t u0, uint64_t G,
                                           Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh
                                           PROF_ARG) {
-  const int s = (int)(k % kRing);
+  const int s = (int)((uint32_t)k % (uint32_t)kRing);
+  set_prio((uint32_t)(wave >> 2) + (uint32_t)k);
   Pend p;
   const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave PROF_PASS);
   if (lane == 0) {
@@ -717,11 +794,34 @@ __device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint6
   gnext = g2;
 }
 
-__device__ __forceinline__ Func unit_func(const Shared& sh, int s) {
-  Func f = Func{sh.cF[s][0], sh.cT[s][0], sh.sF[s][0], sh.sT[s][0]};
-#pragma unroll
-  for (int i = 1; i < kDataWaves; ++i) f = f_then(f, Func{sh.cF[s][i], sh.cT[s][i], sh.sF[s][i], sh.sT[s][i]});
-  return f;
+// The unit's 15 wave summaries composed lane-parallel: lane i < 15 holds wave i, an inclusive DPP scan over
+// row 0 gives every wave's exclusive prefix function (lane i-1's inclusive) and the unit's function (lane 15,
+// whose own summary is the identity).
+__device__ __forceinline__ Func compose_unit(Shared& sh, int s, int lane) {
+  Func w = Func{0, 0, 0, 1};
+  if (lane < kDataWaves) w = Func{sh.cF[s][lane], sh.cT[s][lane], sh.sF[s][lane], sh.sT[s][lane]};
+  Func inc = w;
+  inc = f_then(fn_dpp<kRowShr1, 0xF>(inc), inc);
+  inc = f_then(fn_dpp<kRowShr2, 0xF>(inc), inc);
+  inc = f_then(fn_dpp<kRowShr4, 0xF>(inc), inc);
+  inc = f_then(fn_dpp<kRowShr8, 0xF>(inc), inc);
+  const Func ex = fn_dpp<kRowShr1, 0xF>(inc);
+  if (lane < kDataWaves) {
+    sh.exF[s][lane] = ex.cF;
+    sh.exT[s][lane] = ex.cT;
+    sh.esF[s][lane] = ex.sF;
+    sh.esT[s][lane] = ex.sT;
+  }
+  const Func unit = Func{readlane64(inc.cF, kDataWaves), readlane64(inc.cT, kDataWaves),
+                         (uint32_t)__builtin_amdgcn_readlane((int)inc.sF, kDataWaves),
+                         (uint32_t)__builtin_amdgcn_readlane((int)inc.sT, kDataWaves)};
+  if (lane == 0) {
+    sh.uF[s] = unit.cF;
+    sh.uT[s] = unit.cT;
+    sh.usF[s] = unit.sF;
+    sh.usT[s] = unit.sT;
+  }
+  return unit;
 }
 
 // Coordinator: publish the aggregate of every unit as soon as its 15 data waves are done with it, and
@@ -731,6 +831,7 @@ template <int MODE>
 __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint64_t u0, uint64_t G, uint64_t K,
                                             int lane, Shared& sh) {
   PROF_DECL;
+  set_prio(3);
   Cursor cur{0, 0, 0, 0, 0, 0};
   uint64_t prevP = 0;
   uint32_t prevS = 0;
@@ -739,18 +840,19 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     // publish aggregates up to j + kLag (inclusive) or the end
     const uint64_t want = (j + kLag + 1 < K) ? j + kLag + 1 : K;
     while (published < want) {
-      const int s = (int)(published % kRing);
+      const int s = (int)((uint32_t)published % (uint32_t)kRing);
       PROF_MARK(3);
       lds_wait_eq(&sh.done[s], (uint32_t)kDataWaves, A.err);
       PROF_MARK(0);
+      const Func f = compose_unit(sh, s, lane);
       const uint64_t u = u0 + published * G;
-      if (u > 0 && lane == 0) st_desc(&A.desc[u], pack_agg(unit_func(sh, s)));
+      if (u > 0 && lane == 0) st_desc(&A.desc[u], pack_agg(f));
       ++published;
       PROF_MARK(1);
     }
-    const int s = (int)(j % kRing);
+    const int s = (int)((uint32_t)j % (uint32_t)kRing);
     const uint64_t u = u0 + j * G;
-    const Func unit = unit_func(sh, s);
+    const Func unit = Func{rfl64(sh.uF[s]), rfl64(sh.uT[s]), rfl(sh.usF[s]), rfl(sh.usT[s])};
     const Geo g = geo_of(T, A.nchunks, A.nunits, u, cur);
     uint64_t P;
     uint32_t S_in;
@@ -761,21 +863,22 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     const uint32_t S_out = S_in ? unit.sT : unit.sF;
     prevP = P_incl;
     prevS = S_out;
+    const uint32_t st0 = g.first ? 0u : S_in;
+    if (lane < kDataWaves) {                          // per-wave prefixes, one lane per wave
+      sh.P[s][lane] = P + (st0 ? sh.exT[s][lane] : sh.exF[s][lane]);
+      sh.S[s][lane] = st0 ? sh.esT[s][lane] : sh.esF[s][lane];
+    }
     if (lane == 0) {
       st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
-      uint64_t p = P;
-      uint32_t st = g.first ? 0u : S_in;
-      for (int i = 0; i < kDataWaves; ++i) {
-        sh.P[s][i] = p;
-        sh.S[s][i] = st;
-        p += st ? sh.cT[s][i] : sh.cF[s][i];
-        st = st ? sh.sT[s][i] : sh.sF[s][i];
-      }
       if (u + 1 == A.nunits) A.total[0] = P_incl;
       if (g.last) {
         A.chunk_end[g.c] = P_incl;
         if constexpr (MODE == kFasta) A.pending[g.c] = S_out ? (long long)P_incl - 1 : -1ll;
       }
+    }
+    // LDS ops of one wave complete in order: every lane's P/S write lands before lane 0's flag
+    cbar();
+    if (lane == 0) {
       sh.done[s] = 0;                                // slot free for unit j + kRing
       cbar();
       lds_st(&sh.ready[s], (uint32_t)j + 1u);

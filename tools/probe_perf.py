@@ -38,14 +38,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4 << 30)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--no-stream", action="store_true", help="skip the stream-read calibration")
     args = ap.parse_args()
     size = args.size
     ctx = ScanContext(0)
     host = synth.tiled_fasta_host(size, seed=1)
     d = ctx.workspace("in", size + 64)
     ctx.h2d(d.ptr, host)
-    res = {}
-    for bpc in (1, 2, 4, 8, 16):
+    res = {"lib": os.path.basename(os.environ.get("DPSCAN_LIB", "libdpscan.so"))}
+    for bpc in (() if args.no_stream else (1, 2, 4, 8, 16)):
         k, w = timed(ctx, lambda: ctx.stream_read(d.ptr, size, bpc), args.reps)
         res[f"stream_read_bpc{bpc}_GBps"] = round(size / k / 1e9, 1)
         print(bpc, res, flush=True)

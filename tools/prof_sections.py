@@ -45,6 +45,12 @@ def summarize(p):
     out = {"data_ticks_per_wave": float(dtot.mean())}
     out.update({f"data_{n}": round(float((data / dtot)[..., i].mean()), 3) for i, n in enumerate(DATA) if n != "-"})
     out.update({f"coord_{n}": round(float((coord / ctot)[..., i].mean()), 3) for i, n in enumerate(COORD) if n != "-"})
+    busy = data[..., 1] + data[..., 2] + data[..., 4]          # phase A + post + phase B, per (wg, wave)
+    out["busy_by_wave"] = [round(float(x), 3) for x in (busy / dtot[..., 0]).mean(0)]
+    out["wait_ready_by_wave"] = [round(float(x), 3) for x in (data[..., 3] / dtot[..., 0]).mean(0)]
+    tot_wg = dtot[..., 0].mean(1)
+    out["wg_time_spread"] = [round(float(np.percentile(tot_wg, q) / tot_wg.mean()), 3) for q in (0, 50, 100)]
+    out["busy_wg_spread"] = [round(float(np.percentile(busy.sum(1), q) / busy.sum(1).mean()), 3) for q in (0, 50, 100)]
     return out
 
 
