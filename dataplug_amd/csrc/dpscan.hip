@@ -26,6 +26,7 @@
 #include <string.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/dpscan.h"
@@ -47,10 +48,19 @@ constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 120 KiB look-back unit
 #ifndef DP_PRIO
 #define DP_PRIO 1
 #endif
+#ifndef DP_STEAL            // phase-B tasks shared by all data waves (else each wave runs its own, lagged)
+#define DP_STEAL 0
+#endif
+#ifndef DP_WAVEPUB          // the last data wave of a unit composes and publishes its AGG (else the coordinator)
+#define DP_WAVEPUB 0
+#endif
+#ifndef DP_LBPREFETCH       // the coordinator prefetches the next unit's look-back window
+#define DP_LBPREFETCH 1
+#endif
 constexpr int kRing = DP_RING;                     // LDS ring depth (units in flight per workgroup)
-constexpr int kLag = 2;                            // resolve(j) once AGG(j + kLag) is out
-constexpr int kBLag = kRing - 1;                   // data waves run phase B(j) after phase A(j + kBLag)
-static_assert(kBLag < kRing && kLag < kBLag, "ring slots: A(k+1) reuses the slot of B(k+1-kRing)");
+constexpr int kLag = 2;                            // resolve(j) once unit j + kLag is composed (its AGG out)
+[[maybe_unused]] constexpr int kBLag = kRing - 1;  // !DP_STEAL: data waves run phase B(j) after phase A(j + kBLag)
+static_assert(kLag < kRing, "slot j + kLag must still hold that unit when the coordinator waits on it");
 constexpr uint32_t kGT = 0x3E3E3E3Eu;              // '>'
 constexpr uint32_t kNL = 0x0A0A0A0Au;              // '\n'
 constexpr uint32_t kOdd = 0xAAAAAAAAu, kEven = 0x55555555u;
@@ -161,6 +171,11 @@ __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
 // exclusive wave prefix + total of small per-lane counts (< 2^BITS), bit-sliced ballots
 template <int BITS>
 __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& total) {
+  const uint64_t any1 = __ballot(c != 0u);
+  if (__ballot(c > 1u) == 0ull) {                    // common: at most one per lane
+    total = (uint32_t)__popcll(any1);
+    return mbcnt(any1);
+  }
   uint32_t ex = 0, tot = 0;
 #pragma unroll
   for (int b = 0; b < BITS; ++b) {
@@ -207,8 +222,8 @@ __device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
 __device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-__device__ __forceinline__ void lds_add(uint32_t* p, uint32_t v) {
-  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+__device__ __forceinline__ uint32_t lds_add(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
@@ -336,22 +351,40 @@ constexpr uint64_t kIdentDesc = kStatMask;   // status 3: "no unit here" (identi
 // workgroup's previous unit (u - G, whose inclusive prefix the coordinator holds in registers) and u,
 // all published by running workgroups: one parallel load (4 descriptors per lane for G <= 256) and a
 // 6-step ordered tree reduction resolve it — no serial chain of prefixes.  Spins are bounded.
+// First window of descriptors for unit u (lane 63 = nearest): D[k] = desc[u-1-k] for k < W, D[W] = the
+// workgroup's own previous unit's inclusive prefix (base), identity past it.
+__device__ __forceinline__ void lb_load(const ScanArgs& A, uint64_t u, uint64_t G, uint64_t k0, uint64_t basedesc,
+                                        int lane, uint64_t (&d)[4]) {
+  const uint64_t W = u < G - 1 ? u : G - 1;
+  const int rl = kWave - 1 - lane;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint64_t k = k0 + 4 * (uint64_t)rl + j;
+    d[j] = k < W ? ld_desc(&A.desc[u - 1 - k]) : (k == W ? basedesc : kIdentDesc);
+  }
+}
+
+// One wave: prefix count P and line state S entering unit u.  The window is every unit between this
+// workgroup's previous unit (u - G, whose inclusive prefix the coordinator holds in registers) and u,
+// all published by running workgroups: one parallel load (4 descriptors per lane for G <= 256; the
+// caller may pass it in already loaded, `pre`) and a DPP scan resolve it — no serial chain of prefixes.
+// Spins are bounded.
 __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t G, uint64_t baseP, uint32_t baseS,
-                                      int lane, uint64_t& P, uint32_t& S_in) {
-  const uint64_t W = u < G - 1 ? u : G - 1;          // D[k] = desc[u-1-k] for k < W, D[W] = base prefix
+                                      int lane, uint64_t& P, uint32_t& S_in, uint64_t (&pre)[4], bool have_pre
+                                      PROF_ARG) {
   const uint64_t basedesc = pack_prefix(baseP, baseS);
-  const int rl = kWave - 1 - lane;                   // lane 63 holds the nearest descriptors
   LB acc = lb_ident();
   for (uint64_t k0 = 0;; k0 += 4 * kWave) {
     uint64_t d[4];
     uint64_t PB;
     uint32_t spins = 0;
-    for (;;) {
+    if (k0 == 0 && have_pre) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t k = k0 + 4 * (uint64_t)rl + j;
-        d[j] = k < W ? ld_desc(&A.desc[u - 1 - k]) : (k == W ? basedesc : kIdentDesc);
-      }
+      for (int j = 0; j < 4; ++j) d[j] = pre[j];
+    } else {
+      lb_load(A, u, G, k0, basedesc, lane, d);
+    }
+    for (;;) {
       uint32_t seen = 0, bad = 0;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {                   // nearest first
@@ -371,8 +404,13 @@ __device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t
         PB = 1ull;
         break;
       }
-      __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_s_sleep(8);                    // back off: reloads compete with the stream
+      lb_load(A, u, G, k0, basedesc, lane, d);
+#ifdef DP_PROF
+      prof_acc[4] += 1;                               // spin count (not time)
+#endif
     }
+    PROF_MARK(6);                                     // first valid window (load latency + spins)
     LB f = lb_from_desc(d[3]);
     f = lb_then(f, lb_from_desc(d[2]));
     f = lb_then(f, lb_from_desc(d[1]));
@@ -531,7 +569,10 @@ struct Shared {
   uint64_t P[kRing][kDataWaves];                           // per-wave prefixes from the coordinator
   uint32_t S[kRing][kDataWaves];
   uint32_t done[kRing];                                    // data waves finished phase A of the slot's unit
+  uint32_t composed[kRing];                                // = unit index + 1 once its AGG is composed/published
   uint32_t ready[kRing];                                   // = unit index + 1 once P/S of the slot are set
+  uint32_t bclaim;                                         // phase-B tasks handed out (task = unit*15 + wave)
+  uint32_t bdone[kRing];                                   // phase-B tasks finished per slot (monotonic)
   Pend pend[kRing][kDataWaves];
   uint32_t m[kRing][kDataWaves][kRows][kWave];             // 120 KiB
 };
@@ -662,10 +703,20 @@ __device__ __forceinline__ Func phase_a(const ScanArgs& A, const Geo& g, Buf& b,
 }
 
 // Phase B: offsets from the masks, given the wave's true prefix count and incoming line state.
-template <int MODE>
+// Stores go to min(index, cap - 1) (the host guarantees cap >= 1): an overflowing launch reports
+// DP_ERR_CAPACITY and its output is discarded, so the clamp replaces a per-store branch.  The uint32
+// overflow check (offset >= 2^32) only runs in rows whose offsets can reach 2^32.
+template <typename T>
+__device__ __forceinline__ void put_at(void* out, uint64_t i, uint64_t v) {
+  reinterpret_cast<T*>(out)[i] = (T)v;
+}
+
+template <int MODE, int OUT64>
 __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const uint32_t (&ms)[kRows][kWave],
                                         uint64_t count, uint32_t S_w, int lane) {
+  typedef typename std::conditional<OUT64 != 0, uint64_t, uint32_t>::type OutT;
   const uint64_t obase = A.obj_base - A.shift;      // object offset = obase + aligned coordinate
+  const uint64_t last = A.cap - 1;
   bool ovf = false;
   if constexpr (MODE == kFasta) {
     // entering inside a line that already emitted: its first '>' is not a header, its first '\n' ends
@@ -689,24 +740,22 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
       uint32_t tot;
       const uint32_t ex = wave_excl<3>((uint32_t)__popc(e), tot);
       const uint64_t i0 = count + ex;
-      const uint64_t ob = obase + p.wbase + (uint64_t)r * kRowBytes + (uint64_t)lane * 16;
+      const uint64_t rowb = obase + p.wbase + (uint64_t)r * kRowBytes;
+      const uint64_t ob = rowb + (uint64_t)lane * 16;
+      const bool near4g = !OUT64 && rowb + kRowBytes + 1 > 0xFFFFFFFFull;   // wave-uniform
       for (uint32_t x = e; x; x &= x - 1u) {
         const int bb = __builtin_ctz(x);
         const uint64_t i = i0 + (uint32_t)__popc(e & ((1u << bb) - 1u));
         const uint64_t val = ob + (uint64_t)(bb >> 1);
-        if (i < A.cap) {
-          if (A.out_u64) put<uint64_t>(A.out, 2 * i, val);
-          else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, 2 * i, val); }
-        }
+        if (near4g) ovf |= val > 0xFFFFFFFFull;
+        put_at<OutT>(A.out, 2 * (i < last ? i : last), val);
       }
       for (uint32_t x = n; x; x &= x - 1u) {
         const int bb = __builtin_ctz(x);
         const uint64_t i = i0 + (uint32_t)__popc(e & ((1u << bb) - 1u)) - 1u;
         const uint64_t val = ob + (uint64_t)(bb >> 1) + 1u;
-        if (i < A.cap) {
-          if (A.out_u64) put<uint64_t>(A.out, 2 * i + 1, val);
-          else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, 2 * i + 1, val); }
-        }
+        if (near4g) ovf |= val > 0xFFFFFFFFull;
+        put_at<OutT>(A.out, 2 * (i < last ? i : last) + 1, val);
       }
       count += tot;
     }
@@ -719,18 +768,26 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const 
       uint32_t tot;
       const uint32_t ex = wave_excl<5>((uint32_t)__popc(mm), tot);
       const uint64_t i0 = count + ex;
-      const uint64_t ob = obase + p.wbase + (uint64_t)r * kRowBytes + (uint64_t)lane * 16 + A.emit_add;
-      for (uint32_t x = mm; x; x &= x - 1u) {
-        const int bb = __builtin_ctz(x);
-        uint64_t gi = i0 + (uint32_t)__popc(mm & ((1u << bb) - 1u));
-        if (kk != 1) {
+      const uint64_t rowb = obase + p.wbase + (uint64_t)r * kRowBytes + A.emit_add;
+      const uint64_t ob = rowb + (uint64_t)lane * 16;
+      const bool near4g = !OUT64 && rowb + kRowBytes > 0xFFFFFFFFull;
+      if (kk == 1) {
+        for (uint32_t x = mm; x; x &= x - 1u) {
+          const int bb = __builtin_ctz(x);
+          const uint64_t gi = i0 + (uint32_t)__popc(mm & ((1u << bb) - 1u));
+          const uint64_t val = ob + (uint64_t)bb;
+          if (near4g) ovf |= val > 0xFFFFFFFFull;
+          put_at<OutT>(A.out, gi < last ? gi : last, val);
+        }
+      } else {
+        for (uint32_t x = mm; x; x &= x - 1u) {
+          const int bb = __builtin_ctz(x);
+          uint64_t gi = i0 + (uint32_t)__popc(mm & ((1u << bb) - 1u));
           if (gi % kk != kk - 1) continue;
           gi /= kk;
-        }
-        const uint64_t val = ob + (uint64_t)bb;
-        if (gi < A.cap) {
-          if (A.out_u64) put<uint64_t>(A.out, gi, val);
-          else { ovf |= val > 0xFFFFFFFFull; put<uint32_t>(A.out, gi, val); }
+          const uint64_t val = ob + (uint64_t)bb;
+          if (near4g) ovf |= val > 0xFFFFFFFFull;
+          put_at<OutT>(A.out, gi < last ? gi : last, val);
         }
       }
       count += tot;
@@ -752,8 +809,8 @@ __device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint3
   return true;
 }
 
-// Data wave, phase B of unit j once the coordinator has published its prefixes.
-template <int MODE>
+// !DP_STEAL: the data wave's own phase B of unit j, once the coordinator has published its prefixes.
+template <int MODE, int OUT64>
 __device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int lane, int wave, Shared& sh PROF_ARG) {
   const int s = (int)((uint32_t)j % (uint32_t)kRing);
   PROF_MARK(2);
@@ -766,33 +823,75 @@ __device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int l
   p.fn_off = (int)rfl((uint32_t)p.fn_off);
   const uint64_t P = rfl64(sh.P[s][wave]);
   const uint32_t S = rfl(sh.S[s][wave]);
-  phase_b<MODE>(A, p, sh.m[s][wave], P, S, lane);
+  phase_b<MODE, OUT64>(A, p, sh.m[s][wave], P, S, lane);
   PROF_MARK(4);
 }
 
-// One data-wave step with unit k: phase A(k) on buffer b -> post -> prefetch the unit after next into
-// b -> phase B(k - kBLag).
-template <int MODE>
-__device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint64_t k, uint64_t u0, uint64_t G,
-                                          Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh
-                                          PROF_ARG) {
-  const int s = (int)((uint32_t)k % (uint32_t)kRing);
-  set_prio((uint32_t)(wave >> 2) + (uint32_t)k);
-  Pend p;
-  const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave PROF_PASS);
-  if (lane == 0) {
-    sh.cF[s][wave] = ws.cF; sh.cT[s][wave] = ws.cT; sh.sF[s][wave] = ws.sF; sh.sT[s][wave] = ws.sT;
-    sh.pend[s][wave] = p;
-    cbar();
-    lds_add(&sh.done[s], 1u);
-  }
-  const Geo g2 = geo_of(T, A.nchunks, A.nunits, u0 + (k + 2) * (uint64_t)G, cur);
-  load_buf(b, A, g2, wave, lane);
-  if (k >= (uint64_t)kBLag) data_finish<MODE>(A, k - kBLag, lane, wave, sh PROF_PASS);
-  else PROF_MARK(2);
-  g = gnext;
-  gnext = g2;
+#if DP_STEAL
+__device__ __forceinline__ uint32_t lds_cas(uint32_t* p, uint32_t expect, uint32_t desired) {
+  __hip_atomic_compare_exchange_strong(p, &expect, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+  return expect;                                     // the value seen (== old expect on success)
 }
+
+// Phase B is work-shared: task t = (unit t/15, wave t%15) needs only LDS state (masks, pend, the wave's
+// prefix), so whichever data wave is free runs it.  Tasks are claimed in order, and only once their
+// unit is resolved (ready).  A fast wave thus takes over the slow waves' phase B instead of idling.
+template <int MODE, int OUT64>
+__device__ __forceinline__ bool try_b_task(const ScanArgs& A, uint64_t K, int lane, Shared& sh PROF_ARG) {
+  uint32_t t = 0, got = 0;
+  if (lane == 0) {
+    uint32_t cur = lds_ld(&sh.bclaim);
+    for (;;) {
+      const uint32_t j = cur / (uint32_t)kDataWaves;
+      if ((uint64_t)j >= K || lds_ld(&sh.ready[j % (uint32_t)kRing]) != j + 1u) break;
+      const uint32_t seen = lds_cas(&sh.bclaim, cur, cur + 1u);
+      if (seen == cur) {
+        got = 1;
+        t = cur;
+        break;
+      }
+      cur = seen;
+    }
+  }
+  if (!rfl(got)) return false;
+  t = rfl(t);
+  PROF_MARK(3);
+  const uint32_t j = t / (uint32_t)kDataWaves, w = t % (uint32_t)kDataWaves;
+  const int s = (int)(j % (uint32_t)kRing);
+  cbar();
+  Pend p = sh.pend[s][w];
+  p.wbase = rfl64(p.wbase);
+  p.rows = rfl(p.rows);
+  p.fV = rfl(p.fV);
+  p.fn_off = (int)rfl((uint32_t)p.fn_off);
+  const uint64_t P = rfl64(sh.P[s][w]);
+  const uint32_t S = rfl(sh.S[s][w]);
+  phase_b<MODE, OUT64>(A, p, sh.m[s][w], P, S, lane);
+  cbar();
+  if (lane == 0) lds_add(&sh.bdone[s], 1u);
+  PROF_MARK(4);
+  return true;
+}
+
+// Before phase A of unit k reuses its ring slot, every phase-B task of unit k - kRing must be finished;
+// meanwhile, do phase-B work.  Bounded wait.
+template <int MODE, int OUT64>
+__device__ __forceinline__ void wait_slot(const ScanArgs& A, uint64_t k, uint64_t K, int lane, Shared& sh PROF_ARG) {
+  if (k < (uint64_t)kRing) return;
+  const int s = (int)((uint32_t)k % (uint32_t)kRing);
+  const uint32_t target = (uint32_t)kDataWaves * (uint32_t)(k / kRing);
+  for (uint32_t spins = 0; lds_ld(&sh.bdone[s]) < target;) {
+    if (try_b_task<MODE, OUT64>(A, K, lane, sh PROF_PASS)) continue;
+    if (++spins > kSpinLimit) {
+      if (lane == 0) atomicOr(A.err, kErrTimeout);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  cbar();
+}
+#endif  // DP_STEAL
 
 // The unit's 15 wave summaries composed lane-parallel: lane i < 15 holds wave i, an inclusive DPP scan over
 // row 0 gives every wave's exclusive prefix function (lane i-1's inclusive) and the unit's function (lane 15,
@@ -824,9 +923,57 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, int s, int lane) {
   return unit;
 }
 
-// Coordinator: publish the aggregate of every unit as soon as its 15 data waves are done with it, and
-// resolve unit j (look-back -> inclusive prefix, per-wave prefixes, per-chunk results) once the
-// aggregate of unit j + kLag is out.
+// One data-wave step with unit k: wait for its ring slot (doing phase-B tasks meanwhile) -> phase A(k) on
+// buffer b -> post (the last wave composes and publishes the unit) -> prefetch the unit after next into b
+// -> phase-B tasks while any are ready.
+template <int MODE, int OUT64>
+__device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint64_t k, uint64_t K, uint64_t u0,
+                                          uint64_t G,
+                                          Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh
+                                          PROF_ARG) {
+  const int s = (int)((uint32_t)k % (uint32_t)kRing);
+  set_prio(((uint32_t)(wave >> 2) + (uint32_t)k) % 3u);   // 0..2: the coordinator (3) always wins
+#if DP_STEAL
+  PROF_MARK(2);
+  wait_slot<MODE, OUT64>(A, k, K, lane, sh PROF_PASS);
+  PROF_MARK(3);
+#endif
+  Pend p;
+  const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave PROF_PASS);
+  uint32_t before = 0;
+  if (lane == 0) {
+    sh.cF[s][wave] = ws.cF; sh.cT[s][wave] = ws.cT; sh.sF[s][wave] = ws.sF; sh.sT[s][wave] = ws.sT;
+    sh.pend[s][wave] = p;
+    cbar();
+    before = lds_add(&sh.done[s], 1u);
+  }
+  // the last data wave of the unit composes it and publishes its AGG at once: publication never waits
+  // behind the coordinator's look-back (a coordinator that spun would delay every higher workgroup)
+  if (DP_WAVEPUB && rfl(before) == (uint32_t)kDataWaves - 1u) {
+    const Func f = compose_unit(sh, s, lane);
+    const uint64_t u = u0 + k * G;
+    if (lane == 0) {
+      if (u > 0) st_desc(&A.desc[u], pack_agg(f));
+      sh.done[s] = 0;                                  // slot's counter free for unit k + kRing
+      cbar();
+      lds_st(&sh.composed[s], (uint32_t)k + 1u);
+    }
+  }
+  const Geo g2 = geo_of(T, A.nchunks, A.nunits, u0 + (k + 2) * (uint64_t)G, cur);
+  load_buf(b, A, g2, wave, lane);
+#if DP_STEAL
+  PROF_MARK(2);
+  while (try_b_task<MODE, OUT64>(A, K, lane, sh PROF_PASS)) {}
+#else
+  if (k >= (uint64_t)kBLag) data_finish<MODE, OUT64>(A, k - kBLag, lane, wave, sh PROF_PASS);
+  else PROF_MARK(2);
+#endif
+  g = gnext;
+  gnext = g2;
+}
+
+// Coordinator: resolve unit j (look-back -> inclusive prefix, per-wave prefixes, per-chunk results) as
+// soon as its data waves have composed it.
 template <int MODE>
 __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint64_t u0, uint64_t G, uint64_t K,
                                             int lane, Shared& sh) {
@@ -835,29 +982,39 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
   Cursor cur{0, 0, 0, 0, 0, 0};
   uint64_t prevP = 0;
   uint32_t prevS = 0;
+  uint64_t pre[4] = {0, 0, 0, 0};
+  bool have_pre = false;
   uint64_t published = 0;
+  (void)published;
   for (uint64_t j = 0; j < K; ++j) {
-    // publish aggregates up to j + kLag (inclusive) or the end
-    const uint64_t want = (j + kLag + 1 < K) ? j + kLag + 1 : K;
-    while (published < want) {
-      const int s = (int)((uint32_t)published % (uint32_t)kRing);
+    const int s = (int)((uint32_t)j % (uint32_t)kRing);
+    // by the time this workgroup has composed unit j + kLag, the lower workgroups have almost always
+    // published unit j's round: resolving earlier only spins on their descriptors
+    const uint64_t jw = j + kLag < K ? j + kLag : K - 1;
+#if DP_WAVEPUB
+    PROF_MARK(3);
+    lds_wait_eq(&sh.composed[(uint32_t)jw % (uint32_t)kRing], (uint32_t)jw + 1u, A.err);
+    PROF_MARK(0);
+#else
+    while (published <= jw) {
+      const int sp = (int)((uint32_t)published % (uint32_t)kRing);
       PROF_MARK(3);
-      lds_wait_eq(&sh.done[s], (uint32_t)kDataWaves, A.err);
+      lds_wait_eq(&sh.done[sp], (uint32_t)kDataWaves, A.err);
       PROF_MARK(0);
-      const Func f = compose_unit(sh, s, lane);
-      const uint64_t u = u0 + published * G;
-      if (u > 0 && lane == 0) st_desc(&A.desc[u], pack_agg(f));
+      const Func f = compose_unit(sh, sp, lane);
+      const uint64_t up = u0 + published * G;
+      if (up > 0 && lane == 0) st_desc(&A.desc[up], pack_agg(f));
       ++published;
       PROF_MARK(1);
     }
-    const int s = (int)((uint32_t)j % (uint32_t)kRing);
+#endif
     const uint64_t u = u0 + j * G;
     const Func unit = Func{rfl64(sh.uF[s]), rfl64(sh.uT[s]), rfl(sh.usF[s]), rfl(sh.usT[s])};
     const Geo g = geo_of(T, A.nchunks, A.nunits, u, cur);
     uint64_t P;
     uint32_t S_in;
     PROF_MARK(3);
-    lookback(A, u, G, u >= G ? prevP : 0ull, u >= G ? prevS : 0u, lane, P, S_in);
+    lookback(A, u, G, u >= G ? prevP : 0ull, u >= G ? prevS : 0u, lane, P, S_in, pre, have_pre PROF_PASS);
     PROF_MARK(2);
     const uint64_t P_incl = P + (S_in ? unit.cT : unit.cF);
     const uint32_t S_out = S_in ? unit.sT : unit.sF;
@@ -879,16 +1036,23 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     // LDS ops of one wave complete in order: every lane's P/S write lands before lane 0's flag
     cbar();
     if (lane == 0) {
-      sh.done[s] = 0;                                // slot free for unit j + kRing
+#if !DP_WAVEPUB
+      sh.done[s] = 0;                                // slot's counter free for unit j + kRing
       cbar();
+#endif
       lds_st(&sh.ready[s], (uint32_t)j + 1u);
     }
+#if DP_LBPREFETCH
+    // prefetch the next unit's look-back window: its latency overlaps the wait for the data waves
+    have_pre = j + 1 < K;
+    if (have_pre) lb_load(A, u + G, G, 0, pack_prefix(P_incl, S_out), lane, pre);
+#endif
   }
   PROF_MARK(3);
   PROF_FLUSH(kCoord);
 }
 
-template <int MODE>
+template <int MODE, int OUT64>
 __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64_t* __restrict__ tab_lo,
                                                         const uint64_t* __restrict__ tab_hi,
                                                         const uint64_t* __restrict__ tab_u0) {
@@ -901,8 +1065,11 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   const uint64_t K = u0 < A.nunits ? (A.nunits - u0 + G - 1) / G : 0;   // units of this workgroup
   if (threadIdx.x < kRing) {
     sh.done[threadIdx.x] = 0;
+    sh.composed[threadIdx.x] = 0;
+    sh.bdone[threadIdx.x] = 0;
     sh.ready[threadIdx.x] = 0;
   }
+  if (threadIdx.x == 0) sh.bclaim = 0;
   __syncthreads();
   if (wave == kCoord) {
     coordinator<MODE>(A, T, u0, G, K, lane, sh);
@@ -917,15 +1084,28 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
     uint64_t k = 0;
     PROF_MARK(5);
     while (k < K) {
-      data_step<MODE>(A, T, k, u0, G, g, gnext, bA, cur, lane, wave, sh PROF_PASS);
+      data_step<MODE, OUT64>(A, T, k, K, u0, G, g, gnext, bA, cur, lane, wave, sh PROF_PASS);
       if (++k == K) break;
-      data_step<MODE>(A, T, k, u0, G, g, gnext, bB, cur, lane, wave, sh PROF_PASS);
+      data_step<MODE, OUT64>(A, T, k, K, u0, G, g, gnext, bB, cur, lane, wave, sh PROF_PASS);
       ++k;
     }
     drain_bufs(bA, bB);
     PROF_MARK(6);
+#if !DP_STEAL
     const uint64_t j0 = K > (uint64_t)kBLag ? K - kBLag : 0;
-    for (uint64_t j = j0; j < K; ++j) data_finish<MODE>(A, j, lane, wave, sh PROF_PASS);   // drain
+    for (uint64_t j = j0; j < K; ++j) data_finish<MODE, OUT64>(A, j, lane, wave, sh PROF_PASS);
+#else
+    // drain: phase-B tasks until every task of the workgroup's K units has been claimed
+    const uint32_t all = (uint32_t)kDataWaves * (uint32_t)K;
+    for (uint32_t spins = 0; lds_ld(&sh.bclaim) < all;) {
+      if (try_b_task<MODE, OUT64>(A, K, lane, sh PROF_PASS)) continue;
+      if (++spins > kSpinLimit) {
+        if (lane == 0) atomicOr(A.err, kErrTimeout);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#endif
     PROF_MARK(6);
     PROF_FLUSH(wave);
   }
@@ -1159,6 +1339,10 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.nchunks = n;
   a.nunits = units;
   a.desc = c->d_desc;
+  if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
+    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
+    cap = 1;
+  }
   a.out = d_out;
   a.cap = cap;
   a.out_u64 = out_u64;
@@ -1181,10 +1365,14 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   const uint64_t* tlo = c->d_tab;
   const uint64_t* thi = c->d_tab + n;
   const uint64_t* tu0 = c->d_tab + 2 * n;
-  if (mode == kFasta)
-    hipLaunchKernelGGL(scan_kernel<kFasta>, dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+  if (mode == kFasta && !out_u64)
+    hipLaunchKernelGGL((scan_kernel<kFasta, 0>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+  else if (mode == kFasta)
+    hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+  else if (!out_u64)
+    hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   else
-    hipLaunchKernelGGL(scan_kernel<kDelim>, dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+    hipLaunchKernelGGL((scan_kernel<kDelim, 1>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   HIPCHK(hipGetLastError());
   return ev_end(c);
 }
@@ -1238,10 +1426,14 @@ int dp_ctx_create(int device, dp_ctx** out) {
   HIPCHK(hipGetDeviceProperties(&prop, device));
   c->cus = prop.multiProcessorCount;
   int occ = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, scan_kernel<kFasta>, kThreads, 0));
-  int occ2 = 0;
-  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ2, scan_kernel<kDelim>, kThreads, 0));
-  if (occ2 < occ) occ = occ2;
+  HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (scan_kernel<kFasta, 0>), kThreads, 0));
+  const void* others[] = {(const void*)scan_kernel<kFasta, 1>, (const void*)scan_kernel<kDelim, 0>,
+                          (const void*)scan_kernel<kDelim, 1>};
+  for (const void* k : others) {
+    int o = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, kThreads, 0));
+    if (o < occ) occ = o;
+  }
   // every workgroup of the persistent grid must be resident (look-back waits on lower units): stay one
   // block per CU under the occupancy answer (it can over-report by one, MI355X_MICROARCH.md §Residency)
   // one workgroup (8 waves) per CU: the look-back window is the grid, so G <= 256 keeps it one load

@@ -25,7 +25,7 @@ from dataplug_amd.scan import ScanContext, _lib  # noqa: E402
 from dataplug_amd.scan._lib import check  # noqa: E402
 
 DATA = ["wait_buf", "phase_a", "post_prefetch", "wait_ready", "phase_b", "setup", "drain", "-"]
-COORD = ["wait_done", "publish", "lookback", "rest", "-", "-", "-", "-"]
+COORD = ["wait_done", "publish", "lookback_scan", "rest", "-", "-", "lookback_wait", "-"]
 
 
 def read(ctx, grid):
@@ -41,10 +41,14 @@ def summarize(p):
     data = p[:, :15, :]
     coord = p[:, 15, :]
     dtot = data.sum(-1, keepdims=True)
+    coord = coord.copy()
+    spins = coord[:, 4].copy()
+    coord[:, 4] = 0
     ctot = coord.sum(-1, keepdims=True)
     out = {"data_ticks_per_wave": float(dtot.mean())}
     out.update({f"data_{n}": round(float((data / dtot)[..., i].mean()), 3) for i, n in enumerate(DATA) if n != "-"})
     out.update({f"coord_{n}": round(float((coord / ctot)[..., i].mean()), 3) for i, n in enumerate(COORD) if n != "-"})
+    out["coord_spins_per_wg"] = round(float(spins.mean()), 1)
     busy = data[..., 1] + data[..., 2] + data[..., 4]          # phase A + post + phase B, per (wg, wave)
     out["busy_by_wave"] = [round(float(x), 3) for x in (busy / dtot[..., 0]).mean(0)]
     out["wait_ready_by_wave"] = [round(float(x), 3) for x in (data[..., 3] / dtot[..., 0]).mean(0)]
