@@ -1,25 +1,32 @@
 // dpscan.hip — MI355X (gfx950, CDNA4) record-boundary scan kernels + the C ABI of libdpscan.so.
 //
-// What runs here (DESIGN.md §3):
+// What runs here (DESIGN.md §3-4):
 //   * scan_kernel<FASTA>: the FASTA header index of dataplug/formats/genomics/fasta.py:24-63 for a whole
 //     chunk plan in ONE pass over HBM; emits (start, end) offset pairs bit-exact to the reference.
 //   * scan_kernel<DELIM>: sorted offsets of a delimiter byte (CSV/VCF newline index, FASTQ read ends).
 //   * fasta_resolve_kernel / find_kernel: the "header cut by the chunk end" fix-up (fasta.py:45-56).
 //
 // Single pass, memory-bound (no MFMA):
-//   * persistent grid, one 1024-thread workgroup per CU = 15 data waves + 1 coordinator wave; the
-//     workgroup owns the 120 KiB units u = blockIdx.x + k*G (each data wave 8 rows of 1 KiB = 64 lanes
-//     x 16 B bounds-checked buffer loads, double-buffered in VGPRs, hand-waited).
-//   * per 16-byte lane: SWAR exact byte matches packed into one interleaved 32-bit mask ('\n' at even,
-//     '>' at odd bits), a carry trick that marks the first valid '>' of every line segment, and the
-//     lane-level line state from one 64-bit carry trick on the wave's ballots (SGPRs).
-//   * phase A summarises a wave's 8 KiB as a FUNCTION of the incoming line state and parks its masks in
-//     LDS; the coordinator chains unit summaries across workgroups with a decoupled look-back over
-//     8-byte {status, value} descriptors (agent-scope relaxed atomics = sc1; cdna_hip_programming.md G16
-//     R2) and hands prefixes back through LDS flags; phase B turns masks into offsets.  Input bytes are
-//     read from HBM exactly once; data waves never wait on each other (no workgroup barrier per unit).
-//   * every wait is bounded (DP_ERR_TIMEOUT); units are statically strided over a grid of one
-//     workgroup per CU, so a unit only ever waits on lower units owned by running workgroups.
+//   * persistent grid, one 1024-thread workgroup per CU = 15 data waves + 1 coordinator wave.  Workgroup b
+//     owns the 120 KiB units u = b + k*G; data wave w owns 8 KiB of each (8 rows of 64 lanes x 16 B,
+//     bounds-checked buffer loads, double-buffered in VGPRs, hand-waited).
+//   * byte classes: v_perm_b32 with all-ones data sources returns 0x00 for selector byte 12 and 0xFF for
+//     every other selector, so perm(-1, -1, w ^ (pattern ^ 0x0C0C0C0C)) flags the pattern bytes of w
+//     exactly (2 VALU per dword); v_dot4_i32_i8 packs 4 flags into a nibble.
+//   * phase A (data wave, per unit): the wave range's events — FASTA header starts/ends under the
+//     hypothesis "no header pending at the range start", DELIM delimiters — go to the wave's circular list
+//     of 16-bit positions in LDS, and the range's summary (count and line state as a function of the
+//     incoming state) to the unit's ring slot.
+//   * coordinator wave: composes the 15 summaries (DPP scan), publishes the unit aggregate, resolves the
+//     unit prefix by a decoupled look-back over 8-byte descriptors (agent-scope relaxed atomics,
+//     cdna_hip_programming.md G16 R2) and hands per-wave prefixes back through LDS flags.  It runs as an
+//     event loop and never blocks on a single unit.
+//   * phase B (same data wave, as soon as the unit's prefix is there): a coalesced copy of the event list
+//     to the output at its final index (+ the state fix-up at the range start).  A data wave only waits for
+//     the coordinator once it is kRing units ahead.  Ranges with more than kDenseMax events ("dense") keep
+//     no list; their phase B rescans the range from the input with the now known state.
+//   * every wait is bounded (DP_ERR_TIMEOUT); units are statically strided over a grid of one workgroup
+//     per CU, so a unit only ever waits on lower units owned by running workgroups.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,27 +50,27 @@ constexpr int kRows = 8;                           // rows per wave per unit
 constexpr int kWaveBytes = kRowBytes * kRows;      // 8 KiB
 constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 120 KiB look-back unit
 #ifndef DP_RING
-#define DP_RING 4
+#define DP_RING 32
+#endif
+#ifndef DP_EVCAP
+#define DP_EVCAP 4096
 #endif
 #ifndef DP_PRIO
 #define DP_PRIO 1
 #endif
-#ifndef DP_STEAL            // phase-B tasks shared by all data waves (else each wave runs its own, lagged)
-#define DP_STEAL 0
+#ifndef DP_PRIO_LEVELS
+#define DP_PRIO_LEVELS 4u
 #endif
-#ifndef DP_WAVEPUB          // the last data wave of a unit composes and publishes its AGG (else the coordinator)
-#define DP_WAVEPUB 0
-#endif
-#ifndef DP_LBPREFETCH       // the coordinator prefetches the next unit's look-back window
-#define DP_LBPREFETCH 1
-#endif
-constexpr int kRing = DP_RING;                     // LDS ring depth (units in flight per workgroup)
-constexpr int kLag = 2;                            // resolve(j) once unit j + kLag is composed (its AGG out)
-[[maybe_unused]] constexpr int kBLag = kRing - 1;  // !DP_STEAL: data waves run phase B(j) after phase A(j + kBLag)
-static_assert(kLag < kRing, "slot j + kLag must still hold that unit when the coordinator waits on it");
-constexpr uint32_t kGT = 0x3E3E3E3Eu;              // '>'
-constexpr uint32_t kNL = 0x0A0A0A0Au;              // '\n'
-constexpr uint32_t kOdd = 0xAAAAAAAAu, kEven = 0x55555555u;
+constexpr uint32_t kRing = DP_RING;                // unit slots per workgroup (units in flight)
+constexpr uint32_t kEvCap = DP_EVCAP;              // 16-bit event entries per data wave (circular)
+constexpr uint32_t kEvMask = kEvCap - 1;
+constexpr uint32_t kDenseMax = 1024;               // events kept per wave range; more = dense
+static_assert((kEvCap & kEvMask) == 0 && kEvCap >= 2 * kDenseMax, "event list: power of two, >= 2 ranges");
+static_assert((kRing & (kRing - 1)) == 0 && kRing >= 2, "ring: power of two");
+
+constexpr uint32_t kSel12 = 0x0C0C0C0Cu;           // v_perm selector that yields 0x00
+constexpr uint32_t kKeyGT = 0x3E3E3E3Eu ^ kSel12;  // '>'
+constexpr uint32_t kKeyNL = 0x0A0A0A0Au ^ kSel12;  // '\n'
 
 constexpr uint32_t kErrTimeout = 1u;
 constexpr uint32_t kErrOverflow = 2u;
@@ -116,54 +123,26 @@ struct ScanArgs {
 };
 
 // ------------------------------------------------------------------------------------------ helpers
-__device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t pat) {
-  // exact: bit 8j+7 set iff byte j of w equals the pattern byte
-  const uint32_t x = w ^ pat;
-  const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
-  return ~(t | x) & 0x80808080u;
+// 0x00 in every byte of w that equals the key's pattern byte, 0xFF in every other byte (exact).
+__device__ __forceinline__ uint32_t match4(uint32_t w, uint32_t key) {
+  return __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, w ^ key);
 }
-// v_mul_u32_u24 with a literal multiplier.  The compiler otherwise hoists the constant into an SGPR and
-// emits the quarter-rate v_mul_lo_u32.
-template <uint32_t K>
-__device__ __forceinline__ uint32_t mul24k(uint32_t a) {
-  uint32_t r;
-  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "i"(K), "v"(a));
-  return r;
+// match4 bytes (0x00 = 0, 0xFF = -1 as i8) -> 4-bit mask, bit j = byte j matched: 15 - sum of the
+// non-matching weights 1, 2, 4, 8 (v_dot4_i32_i8).
+__device__ __forceinline__ uint32_t nib(uint32_t p) {
+  return (uint32_t)__builtin_amdgcn_sdot4((int)p, 0x08040201, 15, false);
 }
-__device__ __forceinline__ uint32_t pack4(uint32_t e) {
-  // bits 7,15,23,31 -> bits 0..3 (mul_u32_u24 gather)
-  const uint32_t f = e >> 7;
-  return ((mul24k<0x4081u>(f & 0x10101u) >> 14) & 7u) | (f >> 21);
+__device__ __forceinline__ uint32_t pack16(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
+  return nib(p0) | (nib(p1) << 4) | (nib(p2) << 8) | (nib(p3) << 12);
 }
-__device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t pat) {
-  return pack4(eq4(v.x, pat)) | (pack4(eq4(v.y, pat)) << 4) | (pack4(eq4(v.z, pat)) << 8) |
-         (pack4(eq4(v.w, pat)) << 12);
+__device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t key) {
+  return pack16(match4(v.x, key), match4(v.y, key), match4(v.z, key), match4(v.w, key));
 }
-// 4 bytes -> 8 interleaved flags: bit 2j = (byte j == '\n'), bit 2j+1 = (byte j == '>').  The pairs of
-// bytes 0..2 are gathered by one mul_u32_u24 (partial products land on disjoint bits: no carries).
-__device__ __forceinline__ uint32_t pair8(uint32_t w) {
-  const uint32_t c = (eq4(w, kGT) | (eq4(w, kNL) >> 1)) >> 6;   // byte j: bit 8j = nl, 8j+1 = gt
-  const uint32_t t = (mul24k<0x41041u>(c & 0x30303u) >> 18) & 0x3Fu;
-  return t | ((c >> 18) & 0xC0u);
-}
-__device__ __forceinline__ uint32_t pairs32(const uint4& v) {
-  return pair8(v.x) | (pair8(v.y) << 8) | (pair8(v.z) << 16) | (pair8(v.w) << 24);
-}
-__device__ __forceinline__ bool maybe_has(const uint4& v, uint32_t pat) {
-  // no false negatives (classic haszero); false positives only make the exact path run
-  auto hz = [](uint32_t x) { return (x - 0x01010101u) & ~x; };
-  return ((hz(v.x ^ pat) | hz(v.y ^ pat) | hz(v.z ^ pat) | hz(v.w ^ pat)) & 0x80808080u) != 0;
-}
-// bytes [a, b) of a 16-byte lane (a, b clamped to 0..16) as 16 single / 32 paired bits
-__device__ __forceinline__ uint32_t range16(int64_t a, int64_t b) {
+// bytes [a, b) of a 16-byte lane (a, b clamped to 0..16) as 16 bits
+__device__ __forceinline__ uint32_t range16(int a, int b) {
   a = a < 0 ? 0 : (a > 16 ? 16 : a);
   b = b < 0 ? 0 : (b > 16 ? 16 : b);
   return b <= a ? 0u : ((0xFFFFu >> (16 - (b - a))) << a);
-}
-__device__ __forceinline__ uint32_t range32(int64_t a, int64_t b) {
-  a = a < 0 ? 0 : (a > 16 ? 16 : a);
-  b = b < 0 ? 0 : (b > 16 ? 16 : b);
-  return b <= a ? 0u : (uint32_t)((0xFFFFFFFFull >> (32 - 2 * (b - a))) << (2 * a));
 }
 __device__ __forceinline__ uint32_t mbcnt(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -186,16 +165,6 @@ __device__ __forceinline__ uint32_t wave_excl(uint32_t c, uint32_t& total) {
   total = tot;
   return ex;
 }
-template <int BITS>
-__device__ __forceinline__ uint32_t wave_total(uint32_t c) {
-  const uint64_t any2 = __ballot(c > 1u);
-  const uint64_t any1 = __ballot(c != 0u);
-  if (!any2) return (uint32_t)__popcll(any1);        // common: at most one per lane
-  uint32_t tot = 0;
-#pragma unroll
-  for (int b = 0; b < BITS; ++b) tot += (uint32_t)__popcll(__ballot((c >> b) & 1u)) << b;
-  return tot;
-}
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int l) {
   const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, l);
   const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), l);
@@ -207,6 +176,18 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return ((uint64_t)hi << 32) | lo;
 }
 __device__ __forceinline__ uint32_t rfl(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+// this lane's bit of a wave-uniform 64-bit mask, as 1 - bit (one v_cndmask on the SGPR pair)
+__device__ __forceinline__ uint32_t not_bit(uint64_t m) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, 1, 0, %1" : "=v"(r) : "s"(rfl64(m)));
+  return r;
+}
+// 0 in lanes whose bit of m is set, -1 elsewhere
+__device__ __forceinline__ uint32_t neg_notbit(uint64_t m) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, -1, 0, %1" : "=v"(r) : "s"(rfl64(m)));
+  return r;
+}
 __device__ __forceinline__ uint64_t ld_desc(unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -227,9 +208,8 @@ __device__ __forceinline__ uint32_t lds_add(uint32_t* p, uint32_t v) {
 }
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
-// Issue priority (s_setprio takes an immediate).  The 4 data waves sharing a SIMD (w, w+4, w+8, w+12)
-// otherwise get issue slots by age: the youngest is starved, and as every unit waits for its slowest
-// wave the older ones idle.  Rotating the priority per unit gives each wave every rank once in 4 units.
+// Issue priority (s_setprio takes an immediate).  The 4 data waves sharing a SIMD otherwise get issue
+// slots by age; rotating the priority per unit gives each wave every rank in turn.
 __device__ __forceinline__ void set_prio(uint32_t p) {
 #if DP_PRIO
   switch (p & 3u) {
@@ -243,6 +223,11 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 #endif
 }
 
+template <typename T>
+__device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
+  reinterpret_cast<T*>(out)[i] = (T)v;
+}
+
 // Summary of a byte range as a function of the incoming line state S (does the current line already
 // hold an emitted header?): count and outgoing state for S = false (F) and S = true (T).
 struct Func {
@@ -250,15 +235,13 @@ struct Func {
   uint32_t sF, sT;
 };
 __device__ __forceinline__ Func f_then(const Func& a, const Func& b) {   // a, then b
-  const uint64_t bF = b.cF, bT = b.cT;
-  const uint32_t bsF = b.sF, bsT = b.sT;
   const uint32_t mF = 0u - (a.sF & 1u), mT = 0u - (a.sT & 1u);
   const uint64_t mF64 = 0ull - (uint64_t)(a.sF & 1u), mT64 = 0ull - (uint64_t)(a.sT & 1u);
   Func r;
-  r.cF = a.cF + ((bT & mF64) | (bF & ~mF64));
-  r.sF = (bsT & mF) | (bsF & ~mF);
-  r.cT = a.cT + ((bT & mT64) | (bF & ~mT64));
-  r.sT = (bsT & mT) | (bsF & ~mT);
+  r.cF = a.cF + ((b.cT & mF64) | (b.cF & ~mF64));
+  r.sF = (b.sT & mF) | (b.sF & ~mF);
+  r.cT = a.cT + ((b.cT & mT64) | (b.cF & ~mT64));
+  r.sT = (b.sT & mT) | (b.sF & ~mT);
   return r;
 }
 __device__ __forceinline__ uint64_t pack_agg(const Func& f) {
@@ -267,11 +250,6 @@ __device__ __forceinline__ uint64_t pack_agg(const Func& f) {
 }
 __device__ __forceinline__ uint64_t pack_prefix(uint64_t count, uint32_t s) {
   return kStatPrefix | ((uint64_t)s << 48) | (count & 0xFFFFFFFFFFFFull);
-}
-
-template <typename T>
-__device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
-  reinterpret_cast<T*>(out)[i] = (T)v;
 }
 
 // ------------------------------------------------------------------------------------------ look-back
@@ -296,10 +274,9 @@ __device__ __forceinline__ LB lb_then(const LB& a, const LB& b) {   // a (farthe
   const uint32_t asF = a.fl & 1u, asT = (a.fl >> 1) & 1u;
   const uint32_t bsF = b.fl & 1u, bsT = (b.fl >> 1) & 1u;
   const uint32_t bp = (b.fl >> 2) & 1u;              // b is an inclusive prefix: absorbs a
-  const uint64_t bF = b.cF, bT = b.cT;
   LB r;
-  r.cF = sel64(bp, bF, a.cF + sel64(asF, bT, bF));
-  r.cT = sel64(bp, bT, a.cT + sel64(asT, bT, bF));
+  r.cF = sel64(bp, b.cF, a.cF + sel64(asF, b.cT, b.cF));
+  r.cT = sel64(bp, b.cT, a.cT + sel64(asT, b.cT, b.cF));
   r.fl = sel32(bp, b.fl, sel32(asF, bsT, bsF) | (sel32(asT, bsT, bsF) << 1) | (a.fl & 4u));
   return r;
 }
@@ -326,6 +303,7 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t x, uint64_t old) {
 }
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;   // gfx9 DPP: lane 15 / 31 to the next row(s)
+constexpr int kWaveShl1 = 0x130;                          // lane l <- lane l + 1
 
 template <int CTRL, int ROWS>
 __device__ __forceinline__ LB lb_dpp(const LB& f) {       // identity where there is no source lane
@@ -347,97 +325,60 @@ __device__ __forceinline__ Func fn_dpp(const Func& f) {
 
 constexpr uint64_t kIdentDesc = kStatMask;   // status 3: "no unit here" (identity, always valid)
 
-// One wave: prefix count P and line state S entering unit u.  The window is every unit between this
-// workgroup's previous unit (u - G, whose inclusive prefix the coordinator holds in registers) and u,
-// all published by running workgroups: one parallel load (4 descriptors per lane for G <= 256) and a
-// 6-step ordered tree reduction resolve it — no serial chain of prefixes.  Spins are bounded.
-// First window of descriptors for unit u (lane 63 = nearest): D[k] = desc[u-1-k] for k < W, D[W] = the
-// workgroup's own previous unit's inclusive prefix (base), identity past it.
-__device__ __forceinline__ void lb_load(const ScanArgs& A, uint64_t u, uint64_t G, uint64_t k0, uint64_t basedesc,
-                                        int lane, uint64_t (&d)[4]) {
-  const uint64_t W = u < G - 1 ? u : G - 1;
-  const int rl = kWave - 1 - lane;
+// Look-back window of unit u (lane 63 = nearest): slot k = desc[u-1-k] for k < W = min(u, G-1), slot W =
+// the workgroup's own previous unit (u - G), whose inclusive prefix the coordinator substitutes when it
+// reduces the window (it may not be known yet when the loads are issued), identity past it.
+__device__ __forceinline__ void lb_load(const ScanArgs& A, uint32_t u, uint32_t G, int lane, uint64_t (&d)[4]) {
+  const uint32_t W = u < G - 1 ? u : G - 1;
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const uint64_t k = k0 + 4 * (uint64_t)rl + j;
-    d[j] = k < W ? ld_desc(&A.desc[u - 1 - k]) : (k == W ? basedesc : kIdentDesc);
+    const uint32_t k = 4 * rl + j;
+    d[j] = k < W ? ld_desc(&A.desc[u - 1 - k]) : kIdentDesc;
   }
 }
 
-// One wave: prefix count P and line state S entering unit u.  The window is every unit between this
-// workgroup's previous unit (u - G, whose inclusive prefix the coordinator holds in registers) and u,
-// all published by running workgroups: one parallel load (4 descriptors per lane for G <= 256; the
-// caller may pass it in already loaded, `pre`) and a DPP scan resolve it — no serial chain of prefixes.
-// Spins are bounded.
-__device__ __forceinline__ void lookback(const ScanArgs& A, uint64_t u, uint64_t G, uint64_t baseP, uint32_t baseS,
-                                      int lane, uint64_t& P, uint32_t& S_in, uint64_t (&pre)[4], bool have_pre
-                                      PROF_ARG) {
-  const uint64_t basedesc = pack_prefix(baseP, baseS);
-  LB acc = lb_ident();
-  for (uint64_t k0 = 0;; k0 += 4 * kWave) {
-    uint64_t d[4];
-    uint64_t PB;
-    uint32_t spins = 0;
-    if (k0 == 0 && have_pre) {
+// Reduce one loaded window (one wave): prefix count P and line state S entering unit u, if every
+// descriptor it needs is published (nearest first, down to the nearest inclusive prefix or the base).
+// One parallel load + a DPP scan: no serial chain of prefixes.  Needs G <= 257 (one window).
+__device__ __forceinline__ bool lb_reduce(uint64_t (&d)[4], uint32_t u, uint32_t G, uint64_t basedesc, int lane,
+                                          uint64_t& P, uint32_t& S_in) {
+  const uint32_t W = u < G - 1 ? u : G - 1;
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+  uint32_t seen = 0, bad = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) d[j] = pre[j];
-    } else {
-      lb_load(A, u, G, k0, basedesc, lane, d);
-    }
-    for (;;) {
-      uint32_t seen = 0, bad = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {                   // nearest first
-        const uint64_t st = d[j] & kStatMask;
-        if (!seen && st == 0ull) bad = 1;
-        if (st == kStatPrefix) seen = 1;
-      }
-      PB = __ballot(seen);
-      const uint64_t BB = __ballot(bad);
-      // lanes from the nearest one (63) down to the nearest lane holding a prefix must all be published
-      const uint64_t need = PB ? ~((1ull << (63 - __builtin_clzll(PB))) - 1ull) : ~0ull;
-      if ((BB & need) == 0ull) break;
-      if (++spins > kSpinLimit) {
-        if (lane == 0) atomicOr(A.err, kErrTimeout);
-        d[0] = pack_prefix(0, 0);
-        d[1] = d[2] = d[3] = kIdentDesc;
-        PB = 1ull;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(8);                    // back off: reloads compete with the stream
-      lb_load(A, u, G, k0, basedesc, lane, d);
-#ifdef DP_PROF
-      prof_acc[4] += 1;                               // spin count (not time)
-#endif
-    }
-    PROF_MARK(6);                                     // first valid window (load latency + spins)
-    LB f = lb_from_desc(d[3]);
-    f = lb_then(f, lb_from_desc(d[2]));
-    f = lb_then(f, lb_from_desc(d[1]));
-    f = lb_then(f, lb_from_desc(d[0]));
-    // inclusive scan, lane 0 (farthest) -> lane 63 (nearest): farther composed in front of nearer
-    f = lb_then(lb_dpp<kRowShr1, 0xF>(f), f);
-    f = lb_then(lb_dpp<kRowShr2, 0xF>(f), f);
-    f = lb_then(lb_dpp<kRowShr4, 0xF>(f), f);
-    f = lb_then(lb_dpp<kRowShr8, 0xF>(f), f);
-    f = lb_then(lb_dpp<kRowBcast15, 0xA>(f), f);
-    f = lb_then(lb_dpp<kRowBcast31, 0xC>(f), f);
-    LB F;
-    F.cF = readlane64(f.cF, kWave - 1);
-    F.cT = readlane64(f.cT, kWave - 1);
-    F.fl = (uint32_t)__builtin_amdgcn_readlane((int)f.fl, kWave - 1);
-    acc = lb_then(F, acc);
-    if (PB) break;
+  for (int j = 0; j < 4; ++j) {                     // nearest first
+    if (4 * rl + j == W) d[j] = basedesc;
+    const uint64_t st = d[j] & kStatMask;
+    if (!seen && st == 0ull) bad = 1;
+    if (st == kStatPrefix) seen = 1;
   }
-  P = acc.cF;
-  S_in = acc.fl & 1u;
+  const uint64_t PB = __ballot(seen);
+  const uint64_t BB = __ballot(bad);
+  // lanes from the nearest one (63) down to the nearest lane holding a prefix must all be published
+  const uint64_t need = PB ? ~((1ull << (63 - __builtin_clzll(PB))) - 1ull) : ~0ull;
+  if (BB & need) return false;
+  LB f = lb_from_desc(d[3]);
+  f = lb_then(f, lb_from_desc(d[2]));
+  f = lb_then(f, lb_from_desc(d[1]));
+  f = lb_then(f, lb_from_desc(d[0]));
+  // inclusive scan, lane 0 (farthest) -> lane 63 (nearest): farther composed in front of nearer
+  f = lb_then(lb_dpp<kRowShr1, 0xF>(f), f);
+  f = lb_then(lb_dpp<kRowShr2, 0xF>(f), f);
+  f = lb_then(lb_dpp<kRowShr4, 0xF>(f), f);
+  f = lb_then(lb_dpp<kRowShr8, 0xF>(f), f);
+  f = lb_then(lb_dpp<kRowBcast15, 0xA>(f), f);
+  f = lb_then(lb_dpp<kRowBcast31, 0xC>(f), f);
+  P = readlane64(f.cF, kWave - 1);
+  S_in = (uint32_t)__builtin_amdgcn_readlane((int)f.fl, kWave - 1) & 1u;
+  return true;
 }
 
 // ------------------------------------------------------------------------------------------ geometry
 // Unit -> chunk lookup over the chunk table (read-only, read through the constant address space so it
 // compiles to scalar loads and never enters the vector-memory counter the data waves' hand-waited loads
-// rely on).  A cursor follows
-// the increasing units of one wave, falling back to a binary search when it would skip chunks.
+// rely on).  A cursor follows the increasing units of one wave, falling back to a binary search when it
+// would skip chunks.
 typedef __attribute__((address_space(4))) const uint64_t cu64;   // constant address space: s_load
 struct Tab {
   cu64* lo;
@@ -445,45 +386,54 @@ struct Tab {
   cu64* u0;                          // [nchunks + 1]
 };
 struct Cursor {
-  uint64_t c, u0, u1, lo, hi;        // chunk c = [lo, hi) covers units [u0, u1)
-  uint32_t valid;
+  uint64_t lo, hi;                   // chunk c = [lo, hi) covers units [u0, u1)
+  uint32_t c, u0, u1, valid;
 };
-struct Geo {                          // one unit (wave-uniform)
-  uint64_t lo, hi, ubase, c;
-  uint32_t first, last, valid;
+struct Geo {                          // one unit (wave-uniform); lo_u / hi_u relative to ubase
+  uint64_t ubase;
+  uint32_t lo_u, hi_u, c, fl;         // fl: bit0 first unit of its chunk, bit1 last, bit2 valid
 };
-__device__ __forceinline__ Geo geo_of(const Tab& T, uint64_t nchunks, uint64_t nunits, uint64_t u, Cursor& cur) {
+constexpr uint32_t kGeoFirst = 1u, kGeoLast = 2u, kGeoValid = 4u;
+__device__ __forceinline__ Geo geo_of(const Tab& T, uint32_t nchunks, uint32_t nunits, uint32_t u, Cursor& cur) {
   Geo g;
   if (u >= nunits) {
-    g.lo = g.hi = g.ubase = g.c = 0;
-    g.first = g.last = g.valid = 0;
+    g.ubase = 0;
+    g.lo_u = g.hi_u = g.c = g.fl = 0;
     return g;
   }
   if (!cur.valid || u < cur.u0 || u >= cur.u1) {
-    uint64_t c = 0, cn = nchunks;
-    if (cur.valid && u >= cur.u1 && cur.c + 1 < nchunks && T.u0[cur.c + 2] > u) {
+    uint32_t c = 0, cn = nchunks;
+    if (cur.valid && u >= cur.u1 && cur.c + 1 < nchunks && (uint32_t)T.u0[cur.c + 2] > u) {
       c = cur.c + 1;                                   // common case: the next chunk
     } else {
       while (cn - c > 1) {
-        const uint64_t m = (c + cn) >> 1;
-        if (T.u0[m] <= u) c = m; else cn = m;
+        const uint32_t m = (c + cn) >> 1;
+        if ((uint32_t)T.u0[m] <= u) c = m; else cn = m;
       }
     }
     cur.c = c;
-    cur.u0 = T.u0[c];
-    cur.u1 = T.u0[c + 1];
+    cur.u0 = (uint32_t)T.u0[c];
+    cur.u1 = (uint32_t)T.u0[c + 1];
     cur.lo = T.lo[c];
     cur.hi = T.hi[c];
     cur.valid = 1;
   }
   g.c = cur.c;
-  g.lo = cur.lo;
-  g.hi = cur.hi;
-  g.first = (u == cur.u0);
-  g.last = (u + 1 == cur.u1);
-  g.valid = 1;
-  g.ubase = (g.lo & ~15ull) + (u - cur.u0) * (uint64_t)kUnitBytes;
+  g.ubase = (cur.lo & ~15ull) + (uint64_t)(u - cur.u0) * (uint64_t)kUnitBytes;
+  g.lo_u = cur.lo > g.ubase ? (uint32_t)(cur.lo - g.ubase) : 0u;      // 0..15, first unit only
+  const uint64_t hu = cur.hi - g.ubase;                                // > 0: a unit holds chunk bytes
+  g.hi_u = hu < (uint64_t)(kUnitBytes + 64) ? (uint32_t)hu : (uint32_t)(kUnitBytes + 64);
+  g.fl = kGeoValid | (u == cur.u0 ? kGeoFirst : 0u) | (u + 1 == cur.u1 ? kGeoLast : 0u);
   return g;
+}
+// the chunk bounds [lo_w, hi_w) relative to data wave w's 8 KiB range of unit g
+__device__ __forceinline__ int wave_lo(const Geo& g, int wave) {
+  const int v = (int)g.lo_u - wave * kWaveBytes;
+  return v > 0 ? v : 0;
+}
+__device__ __forceinline__ int wave_hi(const Geo& g, int wave) {
+  const int v = (int)g.hi_u - wave * kWaveBytes;
+  return v < 0 ? 0 : (v > kWaveBytes + 16 ? kWaveBytes + 16 : v);
 }
 
 // ------------------------------------------------------------------------------------------ input loads
@@ -498,22 +448,26 @@ struct Buf {
 // Unconditional bounds-checked loads of one wave's 8 KiB (+ lookahead): bytes at or past the 16-byte
 // block holding the chunk end read as 0 (num_records), so every wave always has exactly kLoadsPerBuf
 // loads in flight per buffer.  Issued as inline asm: the compiler inserts no wait for them, and the
-// data waves wait with ONE explicit `s_waitcnt vmcnt(kLoadsPerBuf)` at the top of phase A (the only
-// younger vector-memory ops are the other buffer's loads plus stores, which only make it conservative).
-// tools/isa_guard.py checks the compiled code never touches a destination before that wait.
+// data waves wait with ONE explicit `s_waitcnt vmcnt(kLoadsPerBuf)` at the top of phase A.  Phase-B
+// stores are issued before the next prefetch, so the kLoadsPerBuf youngest vector-memory operations at
+// that wait are exactly the other buffer's loads.  tools/isa_guard.py checks the compiled code never
+// touches a destination before that wait.
 constexpr int kLoadsPerBuf = kRows + 1;
 
-__device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const Geo& g, int wave, int lane) {
-  const uint64_t wbase = g.valid ? g.ubase + (uint64_t)wave * kWaveBytes : 0ull;
-  const uint64_t hi16 = (g.hi + 15) & ~15ull;
-  uint32_t nrec = 0;
-  if (g.valid && hi16 > wbase) nrec = (uint32_t)((hi16 - wbase) < (uint64_t)(kWaveBytes + 16) ? (hi16 - wbase) : (kWaveBytes + 16));
-  const uint64_t addr = (uint64_t)(uintptr_t)(A.base + wbase);
+// buffer resource for one wave range: num_records ends at the 16-byte block holding the chunk end
+__device__ __forceinline__ v4i buf_rsrc(const uint8_t* base, uint64_t wbase, int hi_w) {
+  const uint32_t nrec = (uint32_t)((hi_w + 15) & ~15);
+  const uint64_t addr = (uint64_t)(uintptr_t)(base + wbase);
   v4i r;
   r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)addr);
   r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(addr >> 32) & 0xFFFF);   // stride 0
   r[2] = __builtin_amdgcn_readfirstlane((int)nrec);
   r[3] = 0x00020000;
+  return r;
+}
+
+__device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const Geo& g, int wave, int lane) {
+  const v4i r = buf_rsrc(A.base, g.ubase + (uint64_t)wave * kWaveBytes, (g.fl & kGeoValid) ? wave_hi(g, wave) : 0);
   const uint32_t off0 = (uint32_t)lane * 16u, off1 = off0 + 4096u, offla = (uint32_t)kWaveBytes;
   static_assert(kRows == 8 && kRowBytes == 1024, "load_buf offsets assume 8 rows of 1 KiB");
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:0" : "=v"(b.x[0]) : "v"(off0), "s"(r) : "memory");
@@ -549,248 +503,299 @@ __device__ __forceinline__ void drain_bufs(Buf& a, Buf& b) {
 }
 
 // ------------------------------------------------------------------------------------------ LDS state
-// Phase-B state of a unit (wave-uniform; the per lane-row masks wait in LDS too: FASTA interleaved
-// emits (odd bits) | ends (even bits), DELIM delimiter bits).
-struct Pend {
-  uint64_t wbase;
-  uint32_t rows;             // bit r: row r has a nonzero mask in some lane
-  uint32_t fV;               // FASTA: first segment of the wave range held a valid '>'
-  int fn_off;                // FASTA: first '\n' of the wave range (byte offset in the range) or -1
-  uint32_t pad;
+struct WaveRec {                   // one data wave's phase-A result for one unit (written by its lane 0)
+  uint64_t wbase;                  // aligned coordinate of the wave range's first byte
+  uint32_t lohi;                   // the chunk bounds in the range: lo_w | hi_w << 16 (dense rescan)
+  uint32_t cF, cT;                 // count if the range is entered with state false / true
+  uint32_t fl;                     // bit0 sF, bit1 sT (state after the range), bit2 fV, bit3 dense
+  uint32_t fn;                     // FASTA: 1 + offset of the range's first '\n', 0 if none
+  uint32_t ev0, nev;               // the range's events in the wave's circular list (running index, count)
 };
+constexpr uint32_t kFlDense = 8u;
 
 struct Shared {
-  uint64_t cF[kRing][kDataWaves], cT[kRing][kDataWaves];   // per-wave summaries
-  uint32_t sF[kRing][kDataWaves], sT[kRing][kDataWaves];
-  uint64_t exF[kRing][kDataWaves], exT[kRing][kDataWaves];  // per-wave exclusive prefix functions (coordinator)
-  uint32_t esF[kRing][kDataWaves], esT[kRing][kDataWaves];
-  uint64_t uF[kRing], uT[kRing];                            // the unit's function
-  uint32_t usF[kRing], usT[kRing];
-  uint64_t P[kRing][kDataWaves];                           // per-wave prefixes from the coordinator
-  uint32_t S[kRing][kDataWaves];
-  uint32_t done[kRing];                                    // data waves finished phase A of the slot's unit
-  uint32_t composed[kRing];                                // = unit index + 1 once its AGG is composed/published
-  uint32_t ready[kRing];                                   // = unit index + 1 once P/S of the slot are set
-  uint32_t bclaim;                                         // phase-B tasks handed out (task = unit*15 + wave)
-  uint32_t bdone[kRing];                                   // phase-B tasks finished per slot (monotonic)
-  Pend pend[kRing][kDataWaves];
-  uint32_t m[kRing][kDataWaves][kRows][kWave];             // 120 KiB
+  uint16_t ev[kDataWaves][kEvCap];                          // per-wave circular event lists
+  WaveRec rec[kRing][kDataWaves];
+  uint32_t exF[kRing][kDataWaves], exT[kRing][kDataWaves];  // per-wave exclusive prefix functions
+  uint32_t es[kRing][kDataWaves];                           // bit0 esF, bit1 esT
+  uint32_t uF[kRing], uT[kRing], us[kRing];                 // the unit's function (us: bit0 sF, bit1 sT)
+  uint64_t P[kRing][kDataWaves];                            // per-wave true prefix (coordinator)
+  uint32_t S[kRing][kDataWaves];                            // per-wave true incoming line state
+  uint32_t done[kRing];                                     // data waves finished phase A of the slot's unit
+  uint32_t ready[kRing];                                    // = unit index + 1 once P/S of the slot are set
 };
 
-// ------------------------------------------------------------------------------------------ FASTA row
-// One row (64 lanes x 16 bytes) under the wave-uniform incoming line state S.  Interleaved masks:
-// bit 2i = byte i is '\n', bit 2i+1 = byte i is a valid '>' (followed by a non-'\n' byte inside the chunk).
-struct FRow {
-  uint32_t m;                // emits (odd bits) | ends (even bits)
-  uint32_t nemit;            // emits in this lane
-  uint32_t s_before_nl;      // line state just before this lane's first '\n'
-  uint32_t first_nl;         // bit index (even) of this lane's first '\n', or 32
-  uint64_t H;                // ballot: lanes holding a '\n'
-  uint32_t S_out;            // wave-uniform state after the row
+// ------------------------------------------------------------------------------------------ rows
+// Events of one row: per-lane mask em (bit i = byte i of the lane), ranks from rank0 in byte order.
+// store(rank, byte offset in the lane) per event; returns the wave's event count in the row.
+template <class Store>
+__device__ __forceinline__ uint32_t emit_row(uint32_t em, uint32_t rank0, Store&& store) {
+  uint32_t tot;
+  const uint32_t ex = wave_excl<5>((uint32_t)__popc(em), tot);
+  uint32_t rk = rank0 + ex;
+  for (uint32_t x = em; x; x &= x - 1u, ++rk) store(rk, (uint32_t)__builtin_ctz(x));
+  return tot;
+}
+
+struct FState {                    // wave-uniform FASTA scan state over one wave range
+  uint32_t S;                      // the current line already holds an emitted header
+  uint32_t nlseen;                 // a '\n' was seen in the range
+  uint32_t fV;                     // state just before the range's first '\n'
+  int fn;                          // offset of the range's first '\n' in the range, -1 if none
+  uint32_t cnt;                    // emitted headers
+  uint32_t nev;                    // events (starts and ends)
 };
-__device__ __forceinline__ FRow fasta_row(uint32_t M, uint32_t nxt63, int last_bit, uint32_t S, int lane) {
-  FRow f;
-  const uint32_t NL = M & kEven, GT = M & kOdd;
-  // next lane's byte 0 is '\n'? (wave_shl:1 DPP; lane 63 takes the lookahead byte)
-  const uint32_t nb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(NL & 1u), 0x130, 0xF, 0xF, false);
-  const uint32_t nxt = (lane == kWave - 1) ? nxt63 : nb;
-  uint32_t V = GT & ~((NL >> 1) | (nxt << 31));      // '>' followed by a non-'\n' byte
-  if (last_bit >= 0) V &= ~(1u << last_bit);          // p + 1 < c1
-  const uint32_t X = V | NL;
-  // first X bit at/after every line start (lane start, byte after each '\n'): carries run through ~X
-  const uint64_t R64 = (uint64_t)(~X) + ((((uint64_t)NL) << 2) | 1ull);
-  const uint32_t R = (uint32_t)R64;
-  const uint32_t s_last = (uint32_t)(R64 >> 32) ^ 1u;    // a valid '>' after the lane's last '\n'
-  const uint64_t H = __ballot(NL != 0u);
-  const uint64_t SB = __ballot(s_last);
-  // line state at each lane's start: exit(p) = H(p) ? SB(p) : exit(p-1) | SB(p), start(0) = S — a
-  // carry chain over the 64 lanes: generate = SB, propagate = ~H (wave-uniform, scalar unit)
-  const uint64_t a = SB | ~H;
-  const uint64_t s1 = a + SB;
-  const uint64_t c1 = s1 < a;
-  const uint64_t s2 = s1 + (uint64_t)S;
-  const uint64_t c2 = s2 < s1;
-  const uint64_t Sstart = s2 ^ a ^ SB;
-  f.S_out = (uint32_t)(c1 | c2);
-  const uint32_t S_lane = (uint32_t)((Sstart >> lane) & 1ull);
-  const uint32_t low = NL & (0u - NL);
-  const uint32_t fs = low ? low - 1u : 0xFFFFFFFFu;   // bits before the lane's first '\n'
-  const uint32_t emits = V & R & (S_lane ? ~fs : 0xFFFFFFFFu);
-  const uint32_t ends = NL & (~R | (S_lane ? low : 0u));
-  f.m = emits | ends;
-  f.nemit = (uint32_t)__popc(emits);
-  f.s_before_nl = S_lane | ((V & fs) != 0u);
-  f.first_nl = low ? (uint32_t)__builtin_ctz(low) : 32u;
-  f.H = H;
-  return f;
+
+// FASTA rows of one wave range ([wbase, wbase + 8 KiB) in aligned coordinates, chunk [lo, hi)).
+// fasta.py:36 emits at p iff d[p] == '>', no header was emitted earlier on p's line inside the chunk,
+// p + 1 < c1 and d[p + 1] != '\n'; its end is the next '\n' + 1.  Per lane, 16-bit masks
+// NL / GT; V = valid '>' bits.  "First valid '>' of every line segment" is one carry trick:
+// R = ~(V | NL) + (NL << 1) + [segment start at the lane start]: carries run through bytes that are
+// neither, so R has a 1 exactly where the carry from each line start stops.  The line state at each lane
+// start is a 64-bit carry chain over two ballots (generate: a valid '>' after the lane's last '\n';
+// propagate: no '\n' in the lane), on the scalar unit.  Rows entered with S = false and without any '>'
+// are skipped after one exact test.
+// One row r (row0 = r KiB into the range): xr = the lane's 16 bytes, wn = a word whose lane-0 byte 0 is the
+// byte after the row (only read when that byte is inside the chunk).
+template <class Store>
+__device__ __forceinline__ void fasta_row(const v4u& xr, uint32_t wn, int r, int lo, int hi, int lane, FState& st,
+                                          Store&& store) {
+  {
+    const int row0 = r * kRowBytes;
+    const bool edge = row0 < lo || row0 + kRowBytes >= hi;
+    const uint32_t g0 = match4(xr[0], kKeyGT), g1 = match4(xr[1], kKeyGT);
+    const uint32_t g2 = match4(xr[2], kKeyGT), g3 = match4(xr[3], kKeyGT);
+    const bool anygt = __ballot((g0 & g1 & g2 & g3) != 0xFFFFFFFFu) != 0ull;
+    if (!edge && !st.S && st.nlseen && !anygt) return;
+    uint32_t NL = pack16(match4(xr[0], kKeyNL), match4(xr[1], kKeyNL), match4(xr[2], kKeyNL), match4(xr[3], kKeyNL));
+    uint32_t GT = anygt ? pack16(g0, g1, g2, g3) : 0u;
+    uint32_t nxt63 = 0, lastm = 0;
+    if (row0 + kRowBytes < hi) nxt63 = ((uint32_t)__builtin_amdgcn_readlane((int)wn, 0) & 0xFFu) == 10u;
+    if (edge) {
+      const int rel_lo = lo - row0 - 16 * lane;
+      const int rel_hi = hi - row0 - 16 * lane;
+      const uint32_t rm = range16(rel_lo, rel_hi);
+      NL &= rm;
+      GT &= rm;
+      if (rel_hi >= 1 && rel_hi <= 16) lastm = 1u << (rel_hi - 1);   // p + 1 < c1
+    }
+    // next byte is '\n': this lane's bits shifted down, the next lane's bit 0 on top (lane 63: the byte
+    // after the row); bits above 15 of the shifted-in word do not matter (GT is 16 bits)
+    const uint32_t dn = dpp32<kWaveShl1, 0xF>(NL, nxt63);
+    const uint32_t V = GT & ~((NL >> 1) | (dn << 15) | lastm);
+    const uint64_t H = __ballot(NL != 0u);
+    const uint32_t m1 = neg_notbit(H);                            // -1: no '\n' in the lane (lane start = segment start)
+    const uint32_t R1 = (((V | NL) ^ 0xFFFFu) + (NL << 1)) - m1;
+    const uint64_t SB = __ballot(R1 < 0x10000u);                  // a valid '>' after the lane's last '\n'
+    // start(p + 1) = SB(p) | (~H(p) & start(p)), start(0) = S: the carries of a + SB + S with a = SB | ~H
+    const uint64_t a = SB | ~H;
+    const uint64_t Sst = (a + SB + (uint64_t)st.S) ^ a ^ SB;     // line state at each lane start
+    // the lane start opens a segment only if its state is false: add it there, take it back elsewhere
+    const uint32_t R = R1 + not_bit(Sst) + m1;
+    const uint32_t emits = V & R;
+    const uint32_t em = emits | (NL & ~R);
+    if (!st.nlseen && H) {
+      const int j0 = (int)__builtin_ctzll(H);
+      const uint32_t low = NL & (0u - NL);
+      const uint32_t vb = (V & (low - 1u)) != 0u;
+      st.fV = (uint32_t)((Sst >> j0) & 1ull) | (uint32_t)__builtin_amdgcn_readlane((int)vb, j0);
+      st.fn = r * kRowBytes + j0 * 16 + __builtin_ctz((uint32_t)__builtin_amdgcn_readlane((int)NL, j0));
+      st.nlseen = 1;
+    }
+    if (__ballot(em != 0u)) {
+      const uint32_t pos0 = (uint32_t)(r * kRowBytes + lane * 16);
+      const uint32_t tot = emit_row(em, st.nev, [&](uint32_t rk, uint32_t b) { store(rk, pos0 + b); });
+      st.cnt += (tot + (st.S ^ 1u)) >> 1;                         // events alternate start, end, ...
+      st.nev += tot;
+    }
+    st.S = (uint32_t)((SB | (~H & Sst)) >> 63);                 // the state after lane 63
+  }
+}
+template <class Store>
+__device__ __forceinline__ void fasta_rows(const v4u (&x)[kRows], uint32_t la, int lo, int hi, int lane, FState& st,
+                                           Store&& store) {
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    if (r * kRowBytes >= hi) break;
+    fasta_row(x[r], (r + 1 < kRows) ? x[(r + 1) & (kRows - 1)][0] : la, r, lo, hi, lane, st, store);
+  }
+}
+
+// Delimiter rows of one wave range: events = delimiter bytes.  nev counts them.
+template <class Store>
+__device__ __forceinline__ void delim_row(const v4u& xr, int r, int lo, int hi, uint32_t key, int lane, uint32_t& nev,
+                                          Store&& store) {
+  const int row0 = r * kRowBytes;
+  const bool edge = row0 < lo || row0 + kRowBytes >= hi;
+  const uint32_t p0 = match4(xr[0], key), p1 = match4(xr[1], key);
+  const uint32_t p2 = match4(xr[2], key), p3 = match4(xr[3], key);
+  if (!edge && __ballot((p0 & p1 & p2 & p3) != 0xFFFFFFFFu) == 0ull) return;
+  uint32_t M = pack16(p0, p1, p2, p3);
+  if (edge) M &= range16(lo - row0 - 16 * lane, hi - row0 - 16 * lane);
+  if (__ballot(M != 0u)) {
+    const uint32_t pos0 = (uint32_t)(row0 + lane * 16);
+    nev += emit_row(M, nev, [&](uint32_t rk, uint32_t b) { store(rk, pos0 + b); });
+  }
+}
+template <class Store>
+__device__ __forceinline__ void delim_rows(const v4u (&x)[kRows], int lo, int hi, uint32_t key, int lane, uint32_t& nev,
+                                           Store&& store) {
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) {
+    if (r * kRowBytes >= hi) break;
+    delim_row(x[r], r, lo, hi, key, lane, nev, store);
+  }
 }
 
 // ------------------------------------------------------------------------------------------ phase A / B
-// Phase A of one unit on one data wave: masks (to LDS) + the wave's summary as a function of the
-// incoming line state (hypothesis: the wave's range starts with S = false).
+// Phase A of one unit on one data wave: events to the wave's list (ranks from ev_head), summary to rec.
 template <int MODE>
-__device__ __forceinline__ Func phase_a(const ScanArgs& A, const Geo& g, Buf& b, Pend& p, uint32_t (&ms)[kRows][kWave],
-                                        int lane, int wave PROF_ARG) {
-  uint64_t cnt = 0;
-  uint32_t S = 0, nlseen = 0, fV = 0;
-  int fn_off = -1;
-  const uint64_t lo = g.lo, hi = g.hi;
-  const uint64_t wbase = g.ubase + (uint64_t)wave * kWaveBytes;
-  uint32_t rows = 0;
+__device__ __forceinline__ void phase_a(const ScanArgs& A, const Geo& g, Buf& b, int wave, int lane, Shared& sh,
+                                        uint32_t ev_head, WaveRec& rec PROF_ARG) {
   wait_buf(b);                                       // this buffer landed; the other one stays in flight
   PROF_MARK(0);
-  uint4 v[kRows];
+  const uint64_t wbase = g.ubase + (uint64_t)wave * kWaveBytes;
+  const int lo = wave_lo(g, wave), hi = wave_hi(g, wave);
+  v4u x[kRows];
 #pragma unroll
-  for (int r = 0; r < kRows; ++r) v[r] = make_uint4(b.x[r][0], b.x[r][1], b.x[r][2], b.x[r][3]);
-  const uint32_t la = b.la;
-#pragma unroll
-  for (int r = 0; r < kRows; ++r) {
-    const uint64_t row0 = wbase + (uint64_t)r * kRowBytes;
-    if (!g.valid || row0 >= hi) continue;
-    // edge row: touches the chunk start, or holds the chunk's last byte (never a header: p+1 < c1)
-    const bool edge = row0 < lo || row0 + kRowBytes >= hi;
-    const int64_t rel_lo = (int64_t)lo - (int64_t)row0 - 16 * lane;   // chunk bounds relative to the lane
-    const int64_t rel_hi = (int64_t)hi - (int64_t)row0 - 16 * lane;
-    uint32_t mr;
-    if constexpr (MODE == kFasta) {
-      if (!S && nlseen && __ballot(maybe_has(v[r], kGT)) == 0ull) continue;
-      uint32_t nxt = 0;
-      if (row0 + kRowBytes < hi) {
-        const uint32_t w = (r + 1 < kRows) ? v[(r + 1) & (kRows - 1)].x : la;
-        nxt = ((uint32_t)__builtin_amdgcn_readlane((int)w, 0) & 0xFFu) == 10u;
-      }
-      uint32_t M = pairs32(v[r]);
-      int last_bit = -1;
-      if (edge) {
-        M &= range32(rel_lo, rel_hi);
-        last_bit = (rel_hi >= 1 && rel_hi <= 16) ? (int)(2 * (rel_hi - 1) + 1) : -1;
-      }
-      const FRow f = fasta_row(M, nxt, last_bit, S, lane);
-      if (!nlseen && f.H) {
-        const int j0 = (int)__builtin_ctzll(f.H);
-        fV = __builtin_amdgcn_readlane((int)f.s_before_nl, j0);
-        fn_off = r * kRowBytes + j0 * 16 + (int)(__builtin_amdgcn_readlane((int)f.first_nl, j0) >> 1);
-        nlseen = 1;
-      }
-      mr = f.m;
-      cnt += wave_total<3>(f.nemit);
-      S = f.S_out;
-    } else {
-      mr = mask16(v[r], A.delim);
-      if (edge) mr &= range16(rel_lo, rel_hi);
-      cnt += wave_total<5>((uint32_t)__popc(mr));
-    }
-    if (__ballot(mr != 0u)) {
-      rows |= 1u << r;
-      ms[r][lane] = mr;
-    }
-  }
-  Func ws;
+  for (int r = 0; r < kRows; ++r) x[r] = b.x[r];
+  uint16_t* evw = sh.ev[wave];
+  auto keep = [&](uint32_t rk, uint32_t pos) {
+    if (rk < kDenseMax) evw[(ev_head + rk) & kEvMask] = (uint16_t)pos;
+  };
+  uint32_t nev, fl;
   if constexpr (MODE == kFasta) {
-    if (!nlseen) fV = S;
-    ws = Func{cnt, cnt - fV, S, nlseen ? S : 1u};
-    if (g.first && wave == 0) { ws.cT = ws.cF; ws.sT = ws.sF; }
+    FState st{0u, 0u, 0u, -1, 0u, 0u};
+    fasta_rows(x, b.la, lo, hi, lane, st, keep);
+    if (!st.nlseen) st.fV = st.S;
+    uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
+    if ((g.fl & kGeoFirst) && wave == 0) { cT = st.cnt; sT = st.S; }   // chunk start: the state is reset
+    rec.cF = st.cnt;
+    rec.cT = cT;
+    fl = st.S | (sT << 1) | (st.fV << 2);
+    rec.fn = (uint32_t)(st.fn + 1);
+    nev = st.nev;
   } else {
-    ws = Func{cnt, cnt, 0u, 0u};
+    nev = 0;
+    delim_rows(x, lo, hi, A.delim ^ kSel12, lane, nev, keep);
+    rec.cF = rec.cT = nev;
+    fl = 0;
+    rec.fn = 0;
   }
-  p.wbase = wbase;
-  p.rows = rows;
-  p.fV = fV;
-  p.fn_off = fn_off;
-  p.pad = 0;
+  const bool dense = nev > kDenseMax;
+  rec.wbase = wbase;
+  rec.lohi = (uint32_t)lo | ((uint32_t)hi << 16);
+  rec.fl = fl | (dense ? kFlDense : 0u);
+  rec.ev0 = ev_head;
+  rec.nev = dense ? 0u : nev;
   PROF_MARK(1);
-  return ws;
 }
 
-// Phase B: offsets from the masks, given the wave's true prefix count and incoming line state.
-// Stores go to min(index, cap - 1) (the host guarantees cap >= 1): an overflowing launch reports
-// DP_ERR_CAPACITY and its output is discarded, so the clamp replaces a per-store branch.  The uint32
-// overflow check (offset >= 2^32) only runs in rows whose offsets can reach 2^32.
-template <typename T>
-__device__ __forceinline__ void put_at(void* out, uint64_t i, uint64_t v) {
-  reinterpret_cast<T*>(out)[i] = (T)v;
-}
-
+// Dense phase B: rescan the range from the input with its true state and count, writing the output
+// directly.  Plain loads (the compiler waits for them; the older in-flight prefetch only makes those
+// waits conservative).  Runs only where the other buffer's registers are free (after phase A).
 template <int MODE, int OUT64>
-__device__ __forceinline__ void phase_b(const ScanArgs& A, const Pend& p, const uint32_t (&ms)[kRows][kWave],
-                                        uint64_t count, uint32_t S_w, int lane) {
+__device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint32_t lohi, uint64_t P, uint32_t S,
+                                        int lane) {
   typedef typename std::conditional<OUT64 != 0, uint64_t, uint32_t>::type OutT;
-  const uint64_t obase = A.obj_base - A.shift;      // object offset = obase + aligned coordinate
-  const uint64_t last = A.cap - 1;
+  const int lo = (int)(lohi & 0xFFFFu), hi = (int)(lohi >> 16);
+  const int hi16 = (hi + 15) & ~15;
+  const uint8_t* src = A.base + wbase;
+  auto row_in = [&](int r) {
+    const int a = r * kRowBytes + lane * 16;
+    return a + 16 <= hi16 ? *reinterpret_cast<const v4u*>(src + a) : v4u{0u, 0u, 0u, 0u};
+  };
+  const uint64_t obj_off = A.obj_base - A.shift + wbase;
+  const bool near4g = !OUT64 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
   bool ovf = false;
   if constexpr (MODE == kFasta) {
-    // entering inside a line that already emitted: its first '>' is not a header, its first '\n' ends
-    // the pending header of an earlier range
-    bool drop = S_w && p.fV;
-    const int fn_off = p.fn_off;
-    const bool add_end = S_w && fn_off >= 0;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-      const uint32_t mr = (p.rows >> r) & 1u ? ms[r][lane] : 0u;
-      uint32_t e = mr & kOdd, n = mr & kEven;
-      if (add_end && (fn_off >> 10) == r && lane == ((fn_off >> 4) & 63)) n |= 1u << (2 * (fn_off & 15));
-      if (drop) {
-        const uint64_t bal = __ballot(e != 0u);
-        if (bal) {
-          if (lane == (int)__builtin_ctzll(bal)) e &= e - 1u;
-          drop = false;
-        }
-      }
-      if (__ballot((e | n) != 0u) == 0ull) continue;
-      uint32_t tot;
-      const uint32_t ex = wave_excl<3>((uint32_t)__popc(e), tot);
-      const uint64_t i0 = count + ex;
-      const uint64_t rowb = obase + p.wbase + (uint64_t)r * kRowBytes;
-      const uint64_t ob = rowb + (uint64_t)lane * 16;
-      const bool near4g = !OUT64 && rowb + kRowBytes + 1 > 0xFFFFFFFFull;   // wave-uniform
-      for (uint32_t x = e; x; x &= x - 1u) {
-        const int bb = __builtin_ctz(x);
-        const uint64_t i = i0 + (uint32_t)__popc(e & ((1u << bb) - 1u));
-        const uint64_t val = ob + (uint64_t)(bb >> 1);
-        if (near4g) ovf |= val > 0xFFFFFFFFull;
-        put_at<OutT>(A.out, 2 * (i < last ? i : last), val);
-      }
-      for (uint32_t x = n; x; x &= x - 1u) {
-        const int bb = __builtin_ctz(x);
-        const uint64_t i = i0 + (uint32_t)__popc(e & ((1u << bb) - 1u)) - 1u;
-        const uint64_t val = ob + (uint64_t)(bb >> 1) + 1u;
-        if (near4g) ovf |= val > 0xFFFFFFFFull;
-        put_at<OutT>(A.out, 2 * (i < last ? i : last) + 1, val);
-      }
-      count += tot;
+    const uint64_t b0 = 2 * P - S, last = 2 * A.cap - 1;
+    FState st{S, 1u, 0u, -1, 0u, 0u};
+    auto out = [&](uint32_t rk, uint32_t pos) {
+      const uint64_t slot = b0 + rk;
+      const uint64_t val = obj_off + pos + (slot & 1u);
+      if (near4g) ovf |= val > 0xFFFFFFFFull;
+      put<OutT>(A.out, slot < last ? slot : last, val);
+    };
+#pragma unroll 1
+    for (int r = 0; r < kRows && r * kRowBytes < hi; ++r) {
+      const int an = (r + 1) * kRowBytes;
+      const uint32_t wn = an + 4 <= hi16 ? *reinterpret_cast<const uint32_t*>(src + an) : 0u;
+      fasta_row(row_in(r), wn, r, lo, hi, lane, st, out);
     }
   } else {
-    const uint32_t kk = A.every_k;
-#pragma unroll
-    for (int r = 0; r < kRows; ++r) {
-      if (!((p.rows >> r) & 1u)) continue;
-      const uint32_t mm = ms[r][lane];
-      uint32_t tot;
-      const uint32_t ex = wave_excl<5>((uint32_t)__popc(mm), tot);
-      const uint64_t i0 = count + ex;
-      const uint64_t rowb = obase + p.wbase + (uint64_t)r * kRowBytes + A.emit_add;
-      const uint64_t ob = rowb + (uint64_t)lane * 16;
-      const bool near4g = !OUT64 && rowb + kRowBytes > 0xFFFFFFFFull;
-      if (kk == 1) {
-        for (uint32_t x = mm; x; x &= x - 1u) {
-          const int bb = __builtin_ctz(x);
-          const uint64_t gi = i0 + (uint32_t)__popc(mm & ((1u << bb) - 1u));
-          const uint64_t val = ob + (uint64_t)bb;
-          if (near4g) ovf |= val > 0xFFFFFFFFull;
-          put_at<OutT>(A.out, gi < last ? gi : last, val);
-        }
-      } else {
-        for (uint32_t x = mm; x; x &= x - 1u) {
-          const int bb = __builtin_ctz(x);
-          uint64_t gi = i0 + (uint32_t)__popc(mm & ((1u << bb) - 1u));
-          if (gi % kk != kk - 1) continue;
-          gi /= kk;
-          const uint64_t val = ob + (uint64_t)bb;
-          if (near4g) ovf |= val > 0xFFFFFFFFull;
-          put_at<OutT>(A.out, gi < last ? gi : last, val);
-        }
-      }
-      count += tot;
+    const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
+    const uint32_t k = A.every_k;
+    // every k-th delimiter overall: rank rk is kept iff rk >= r0 and (rk - r0) % k == 0, at q0 + (rk - r0) / k
+    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - P % k);
+    const uint64_t q0 = (P + r0) / k;
+    uint32_t n = 0;
+    auto out = [&](uint32_t rk, uint32_t pos) {
+      if (rk < r0) return;
+      const uint32_t d = rk - r0;
+      const uint32_t t = k == 1u ? d : d / k;
+      if (t * k != d) return;
+      const uint64_t q = q0 + t;
+      const uint64_t val = add + pos;
+      if (near4g) ovf |= val > 0xFFFFFFFFull;
+      put<OutT>(A.out, q < last ? q : last, val);
+    };
+    const uint32_t key = A.delim ^ kSel12;
+#pragma unroll 1
+    for (int r = 0; r < kRows && r * kRowBytes < hi; ++r) delim_row(row_in(r), r, lo, hi, key, lane, n, out);
+  }
+  if (ovf) atomicOr(A.err, kErrOverflow);
+}
+
+// Phase B of one unit on one data wave, once its prefix is set: the event list copied to the output at
+// its final index.  FASTA: the list was built under "no header pending at the range start"; if the true
+// state S says one is pending, the range's first segment emits nothing (drop its start, fV) and its first
+// '\n' ends the pending header (prepend it unless already listed).  Output slot of event i: 2P - S + i
+// (u32 slots, starts even, ends odd = '\n' + 1).  Stores go to min(slot, last): an overflowing launch
+// reports DP_ERR_CAPACITY and its output is discarded, so the clamp replaces a per-store branch.
+template <int MODE, int OUT64>
+__device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t s, int wave, int lane,
+                                        uint32_t& ev_tail) {
+  typedef typename std::conditional<OUT64 != 0, uint64_t, uint32_t>::type OutT;
+  const WaveRec& rr = sh.rec[s][wave];
+  const uint64_t wbase = rfl64(rr.wbase);
+  const uint32_t fl = rfl(rr.fl), ev0 = rfl(rr.ev0), nev = rfl(rr.nev);
+  const uint64_t P = rfl64(sh.P[s][wave]);
+  const uint32_t S = rfl(sh.S[s][wave]);
+  ev_tail = ev0 + nev;
+  if (fl & kFlDense) {
+    dense_b<MODE, OUT64>(A, wbase, rfl(rr.lohi), P, S, lane);
+    return;
+  }
+  const uint64_t obj_off = A.obj_base - A.shift + wbase;
+  const bool near4g = !OUT64 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+  const uint16_t* evw = sh.ev[wave];
+  bool ovf = false;
+  if constexpr (MODE == kFasta) {
+    const uint32_t fn = rfl(rr.fn);
+    const uint32_t skip = S & (fl >> 2) & 1u;
+    const uint32_t pre = (S && !((fl >> 2) & 1u) && fn) ? 1u : 0u;
+    const uint32_t n = nev - skip + pre;
+    const uint64_t b0 = 2 * P - S, last = 2 * A.cap - 1;
+    for (uint32_t i = (uint32_t)lane; i < n; i += kWave) {
+      const uint32_t e = (pre && i == 0) ? fn - 1u : (uint32_t)evw[(ev0 + i + skip - pre) & kEvMask];
+      const uint64_t slot = b0 + i;
+      const uint64_t val = obj_off + e + (slot & 1u);
+      if (near4g) ovf |= val > 0xFFFFFFFFull;
+      put<OutT>(A.out, slot < last ? slot : last, val);
+    }
+  } else {
+    const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
+    const uint32_t k = A.every_k;
+    // every k-th delimiter overall (FASTQ read ends): list entries r0, r0 + k, ... go to q0, q0 + 1, ...
+    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - P % k);
+    const uint64_t q0 = (P + r0) / k;
+    const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
+    for (uint32_t t = (uint32_t)lane; t < nq; t += kWave) {
+      const uint64_t q = q0 + t;
+      const uint64_t val = add + evw[(ev0 + r0 + t * k) & kEvMask];
+      if (near4g) ovf |= val > 0xFFFFFFFFull;
+      put<OutT>(A.out, q < last ? q : last, val);
     }
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
@@ -809,96 +814,16 @@ __device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint3
   return true;
 }
 
-// !DP_STEAL: the data wave's own phase B of unit j, once the coordinator has published its prefixes.
-template <int MODE, int OUT64>
-__device__ __forceinline__ void data_finish(const ScanArgs& A, uint64_t j, int lane, int wave, Shared& sh PROF_ARG) {
-  const int s = (int)((uint32_t)j % (uint32_t)kRing);
-  PROF_MARK(2);
-  lds_wait_eq(&sh.ready[s], (uint32_t)j + 1u, A.err);
-  PROF_MARK(3);
-  Pend p = sh.pend[s][wave];
-  p.wbase = rfl64(p.wbase);
-  p.rows = rfl(p.rows);
-  p.fV = rfl(p.fV);
-  p.fn_off = (int)rfl((uint32_t)p.fn_off);
-  const uint64_t P = rfl64(sh.P[s][wave]);
-  const uint32_t S = rfl(sh.S[s][wave]);
-  phase_b<MODE, OUT64>(A, p, sh.m[s][wave], P, S, lane);
-  PROF_MARK(4);
-}
-
-#if DP_STEAL
-__device__ __forceinline__ uint32_t lds_cas(uint32_t* p, uint32_t expect, uint32_t desired) {
-  __hip_atomic_compare_exchange_strong(p, &expect, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-  return expect;                                     // the value seen (== old expect on success)
-}
-
-// Phase B is work-shared: task t = (unit t/15, wave t%15) needs only LDS state (masks, pend, the wave's
-// prefix), so whichever data wave is free runs it.  Tasks are claimed in order, and only once their
-// unit is resolved (ready).  A fast wave thus takes over the slow waves' phase B instead of idling.
-template <int MODE, int OUT64>
-__device__ __forceinline__ bool try_b_task(const ScanArgs& A, uint64_t K, int lane, Shared& sh PROF_ARG) {
-  uint32_t t = 0, got = 0;
-  if (lane == 0) {
-    uint32_t cur = lds_ld(&sh.bclaim);
-    for (;;) {
-      const uint32_t j = cur / (uint32_t)kDataWaves;
-      if ((uint64_t)j >= K || lds_ld(&sh.ready[j % (uint32_t)kRing]) != j + 1u) break;
-      const uint32_t seen = lds_cas(&sh.bclaim, cur, cur + 1u);
-      if (seen == cur) {
-        got = 1;
-        t = cur;
-        break;
-      }
-      cur = seen;
-    }
-  }
-  if (!rfl(got)) return false;
-  t = rfl(t);
-  PROF_MARK(3);
-  const uint32_t j = t / (uint32_t)kDataWaves, w = t % (uint32_t)kDataWaves;
-  const int s = (int)(j % (uint32_t)kRing);
-  cbar();
-  Pend p = sh.pend[s][w];
-  p.wbase = rfl64(p.wbase);
-  p.rows = rfl(p.rows);
-  p.fV = rfl(p.fV);
-  p.fn_off = (int)rfl((uint32_t)p.fn_off);
-  const uint64_t P = rfl64(sh.P[s][w]);
-  const uint32_t S = rfl(sh.S[s][w]);
-  phase_b<MODE, OUT64>(A, p, sh.m[s][w], P, S, lane);
-  cbar();
-  if (lane == 0) lds_add(&sh.bdone[s], 1u);
-  PROF_MARK(4);
-  return true;
-}
-
-// Before phase A of unit k reuses its ring slot, every phase-B task of unit k - kRing must be finished;
-// meanwhile, do phase-B work.  Bounded wait.
-template <int MODE, int OUT64>
-__device__ __forceinline__ void wait_slot(const ScanArgs& A, uint64_t k, uint64_t K, int lane, Shared& sh PROF_ARG) {
-  if (k < (uint64_t)kRing) return;
-  const int s = (int)((uint32_t)k % (uint32_t)kRing);
-  const uint32_t target = (uint32_t)kDataWaves * (uint32_t)(k / kRing);
-  for (uint32_t spins = 0; lds_ld(&sh.bdone[s]) < target;) {
-    if (try_b_task<MODE, OUT64>(A, K, lane, sh PROF_PASS)) continue;
-    if (++spins > kSpinLimit) {
-      if (lane == 0) atomicOr(A.err, kErrTimeout);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  cbar();
-}
-#endif  // DP_STEAL
-
 // The unit's 15 wave summaries composed lane-parallel: lane i < 15 holds wave i, an inclusive DPP scan over
 // row 0 gives every wave's exclusive prefix function (lane i-1's inclusive) and the unit's function (lane 15,
 // whose own summary is the identity).
-__device__ __forceinline__ Func compose_unit(Shared& sh, int s, int lane) {
+__device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
   Func w = Func{0, 0, 0, 1};
-  if (lane < kDataWaves) w = Func{sh.cF[s][lane], sh.cT[s][lane], sh.sF[s][lane], sh.sT[s][lane]};
+  if (lane < kDataWaves) {
+    const WaveRec& r = sh.rec[s][lane];
+    const uint32_t fl = r.fl;
+    w = Func{r.cF, r.cT, fl & 1u, (fl >> 1) & 1u};
+  }
   Func inc = w;
   inc = f_then(fn_dpp<kRowShr1, 0xF>(inc), inc);
   inc = f_then(fn_dpp<kRowShr2, 0xF>(inc), inc);
@@ -906,151 +831,215 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, int s, int lane) {
   inc = f_then(fn_dpp<kRowShr8, 0xF>(inc), inc);
   const Func ex = fn_dpp<kRowShr1, 0xF>(inc);
   if (lane < kDataWaves) {
-    sh.exF[s][lane] = ex.cF;
-    sh.exT[s][lane] = ex.cT;
-    sh.esF[s][lane] = ex.sF;
-    sh.esT[s][lane] = ex.sT;
+    sh.exF[s][lane] = (uint32_t)ex.cF;
+    sh.exT[s][lane] = (uint32_t)ex.cT;
+    sh.es[s][lane] = (ex.sF & 1u) | ((ex.sT & 1u) << 1);
   }
   const Func unit = Func{readlane64(inc.cF, kDataWaves), readlane64(inc.cT, kDataWaves),
                          (uint32_t)__builtin_amdgcn_readlane((int)inc.sF, kDataWaves),
                          (uint32_t)__builtin_amdgcn_readlane((int)inc.sT, kDataWaves)};
   if (lane == 0) {
-    sh.uF[s] = unit.cF;
-    sh.uT[s] = unit.cT;
-    sh.usF[s] = unit.sF;
-    sh.usT[s] = unit.sT;
+    sh.uF[s] = (uint32_t)unit.cF;
+    sh.uT[s] = (uint32_t)unit.cT;
+    sh.us[s] = (unit.sF & 1u) | ((unit.sT & 1u) << 1);
   }
   return unit;
 }
 
-// One data-wave step with unit k: wait for its ring slot (doing phase-B tasks meanwhile) -> phase A(k) on
-// buffer b -> post (the last wave composes and publishes the unit) -> prefetch the unit after next into b
-// -> phase-B tasks while any are ready.
-template <int MODE, int OUT64>
-__device__ __forceinline__ void data_step(const ScanArgs& A, const Tab& T, uint64_t k, uint64_t K, uint64_t u0,
-                                          uint64_t G,
-                                          Geo& g, Geo& gnext, Buf& b, Cursor& cur, int lane, int wave, Shared& sh
-                                          PROF_ARG) {
-  const int s = (int)((uint32_t)k % (uint32_t)kRing);
-  set_prio(((uint32_t)(wave >> 2) + (uint32_t)k) % 3u);   // 0..2: the coordinator (3) always wins
-#if DP_STEAL
-  PROF_MARK(2);
-  wait_slot<MODE, OUT64>(A, k, K, lane, sh PROF_PASS);
-  PROF_MARK(3);
+#ifndef DP_LBDEPTH
+#define DP_LBDEPTH 8
 #endif
-  Pend p;
-  const Func ws = phase_a<MODE>(A, g, b, p, sh.m[s][wave], lane, wave PROF_PASS);
-  uint32_t before = 0;
-  if (lane == 0) {
-    sh.cF[s][wave] = ws.cF; sh.cT[s][wave] = ws.cT; sh.sF[s][wave] = ws.sF; sh.sT[s][wave] = ws.sT;
-    sh.pend[s][wave] = p;
-    cbar();
-    before = lds_add(&sh.done[s], 1u);
-  }
-  // the last data wave of the unit composes it and publishes its AGG at once: publication never waits
-  // behind the coordinator's look-back (a coordinator that spun would delay every higher workgroup)
-  if (DP_WAVEPUB && rfl(before) == (uint32_t)kDataWaves - 1u) {
-    const Func f = compose_unit(sh, s, lane);
-    const uint64_t u = u0 + k * G;
-    if (lane == 0) {
-      if (u > 0) st_desc(&A.desc[u], pack_agg(f));
-      sh.done[s] = 0;                                  // slot's counter free for unit k + kRing
-      cbar();
-      lds_st(&sh.composed[s], (uint32_t)k + 1u);
-    }
-  }
-  const Geo g2 = geo_of(T, A.nchunks, A.nunits, u0 + (k + 2) * (uint64_t)G, cur);
-  load_buf(b, A, g2, wave, lane);
-#if DP_STEAL
-  PROF_MARK(2);
-  while (try_b_task<MODE, OUT64>(A, K, lane, sh PROF_PASS)) {}
-#else
-  if (k >= (uint64_t)kBLag) data_finish<MODE, OUT64>(A, k - kBLag, lane, wave, sh PROF_PASS);
-  else PROF_MARK(2);
+#ifndef DP_COORD_PRIO
+#define DP_COORD_PRIO 0
 #endif
-  g = gnext;
-  gnext = g2;
-}
+constexpr uint32_t kLbDepth = DP_LBDEPTH;          // look-back windows in flight per coordinator attempt
 
-// Coordinator: resolve unit j (look-back -> inclusive prefix, per-wave prefixes, per-chunk results) as
-// soon as its data waves have composed it.
+// Coordinator event loop.  Its descriptor loads queue behind the CU's in-flight input stream (~5 us),
+// so it never waits on one unit: each round it issues the look-back windows of up to kLbDepth composed
+// units at once, composes + publishes every unit whose 15 data waves are done while they travel (other
+// workgroups' look-backs wait on those), then resolves the windows in order until one is incomplete.
 template <int MODE>
-__device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint64_t u0, uint64_t G, uint64_t K,
+__device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint32_t u0, uint32_t G, uint32_t K,
                                             int lane, Shared& sh) {
   PROF_DECL;
-  set_prio(3);
+  set_prio(DP_COORD_PRIO);
   Cursor cur{0, 0, 0, 0, 0, 0};
   uint64_t prevP = 0;
   uint32_t prevS = 0;
-  uint64_t pre[4] = {0, 0, 0, 0};
-  bool have_pre = false;
-  uint64_t published = 0;
-  (void)published;
-  for (uint64_t j = 0; j < K; ++j) {
-    const int s = (int)((uint32_t)j % (uint32_t)kRing);
-    // by the time this workgroup has composed unit j + kLag, the lower workgroups have almost always
-    // published unit j's round: resolving earlier only spins on their descriptors
-    const uint64_t jw = j + kLag < K ? j + kLag : K - 1;
-#if DP_WAVEPUB
-    PROF_MARK(3);
-    lds_wait_eq(&sh.composed[(uint32_t)jw % (uint32_t)kRing], (uint32_t)jw + 1u, A.err);
+  uint32_t pub = 0, res = 0;
+  uint32_t idle = 0;
+  auto compose_ready = [&]() {
+    bool any = false;
+    while (pub < K && lds_ld(&sh.done[pub % kRing]) == (uint32_t)kDataWaves) {
+      const uint32_t s = pub % kRing;
+      cbar();
+      const Func f = compose_unit(sh, s, lane);
+      const uint32_t up = u0 + pub * G;
+      if (lane == 0) {
+        if (up > 0) st_desc(&A.desc[up], pack_agg(f));
+        sh.done[s] = 0;                               // slot's counter free for unit pub + kRing
+      }
+      ++pub;
+      any = true;
+    }
+    return any;
+  };
+  while (res < K) {
+    bool prog = compose_ready();
     PROF_MARK(0);
+    if (res < pub) {
+      const uint32_t D = pub - res < kLbDepth ? pub - res : kLbDepth;
+#ifdef DP_PROF
+      prof_acc[4] += 1;                               // look-back attempts (count)
+#endif
+      uint64_t d[kLbDepth][4];
+#pragma unroll
+      for (uint32_t j = 0; j < kLbDepth; ++j) {
+#ifndef DP_NOSYNC
+        if (j < D) lb_load(A, u0 + (res + j) * G, G, lane, d[j]);
 #else
-    while (published <= jw) {
-      const int sp = (int)((uint32_t)published % (uint32_t)kRing);
-      PROF_MARK(3);
-      lds_wait_eq(&sh.done[sp], (uint32_t)kDataWaves, A.err);
+        d[j][0] = d[j][1] = d[j][2] = d[j][3] = kIdentDesc;   // perf probe: no cross-workgroup dependency
+#endif
+      }
+      prog |= compose_ready();                        // while the windows travel
       PROF_MARK(0);
-      const Func f = compose_unit(sh, sp, lane);
-      const uint64_t up = u0 + published * G;
-      if (up > 0 && lane == 0) st_desc(&A.desc[up], pack_agg(f));
-      ++published;
+#pragma unroll
+      for (uint32_t j = 0; j < kLbDepth; ++j) {
+        if (j >= D) break;
+        const uint32_t u = u0 + res * G;
+        uint64_t P;
+        uint32_t S_in;
+        if (!lb_reduce(d[j], u, G, pack_prefix(u >= G ? prevP : 0ull, u >= G ? prevS : 0u), lane, P, S_in)) {
+#ifdef DP_PROF
+          prof_acc[5] += 1;                           // incomplete windows (count)
+#endif
+          break;
+        }
+#ifdef DP_PROF
+        prof_acc[6] += 1;                             // resolved units (count)
+#endif
+        const uint32_t s = res % kRing;
+        const Geo g = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u, cur);
+        const uint32_t usv = sh.us[s];
+        const uint64_t P_incl = P + (S_in ? sh.uT[s] : sh.uF[s]);
+        const uint32_t S_out = S_in ? (usv >> 1) & 1u : usv & 1u;
+        prevP = P_incl;
+        prevS = S_out;
+        const uint32_t st0 = (g.fl & kGeoFirst) ? 0u : S_in;
+        if (lane < kDataWaves) {                      // per-wave prefixes, one lane per wave
+          const uint32_t es = sh.es[s][lane];
+          sh.P[s][lane] = P + (st0 ? sh.exT[s][lane] : sh.exF[s][lane]);
+          sh.S[s][lane] = st0 ? (es >> 1) & 1u : es & 1u;
+        }
+        if (lane == 0) {
+          st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
+          if (u + 1 == A.nunits) A.total[0] = P_incl;
+          if (g.fl & kGeoLast) {
+            A.chunk_end[g.c] = P_incl;
+            if constexpr (MODE == kFasta) A.pending[g.c] = S_out ? (long long)P_incl - 1 : -1ll;
+          }
+        }
+        // LDS ops of one wave complete in order: every lane's P/S write lands before lane 0's flag
+        cbar();
+        if (lane == 0) lds_st(&sh.ready[s], res + 1u);
+        ++res;
+        prog = true;
+      }
       PROF_MARK(1);
     }
-#endif
-    const uint64_t u = u0 + j * G;
-    const Func unit = Func{rfl64(sh.uF[s]), rfl64(sh.uT[s]), rfl(sh.usF[s]), rfl(sh.usT[s])};
-    const Geo g = geo_of(T, A.nchunks, A.nunits, u, cur);
-    uint64_t P;
-    uint32_t S_in;
-    PROF_MARK(3);
-    lookback(A, u, G, u >= G ? prevP : 0ull, u >= G ? prevS : 0u, lane, P, S_in, pre, have_pre PROF_PASS);
-    PROF_MARK(2);
-    const uint64_t P_incl = P + (S_in ? unit.cT : unit.cF);
-    const uint32_t S_out = S_in ? unit.sT : unit.sF;
-    prevP = P_incl;
-    prevS = S_out;
-    const uint32_t st0 = g.first ? 0u : S_in;
-    if (lane < kDataWaves) {                          // per-wave prefixes, one lane per wave
-      sh.P[s][lane] = P + (st0 ? sh.exT[s][lane] : sh.exF[s][lane]);
-      sh.S[s][lane] = st0 ? sh.esT[s][lane] : sh.esF[s][lane];
-    }
-    if (lane == 0) {
-      st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
-      if (u + 1 == A.nunits) A.total[0] = P_incl;
-      if (g.last) {
-        A.chunk_end[g.c] = P_incl;
-        if constexpr (MODE == kFasta) A.pending[g.c] = S_out ? (long long)P_incl - 1 : -1ll;
+    if (prog) {
+      idle = 0;
+    } else {
+      if (++idle > kSpinLimit) {
+        if (lane == 0) atomicOr(A.err, kErrTimeout);
+        break;
       }
+      __builtin_amdgcn_s_sleep(1);
+      PROF_MARK(3);
     }
-    // LDS ops of one wave complete in order: every lane's P/S write lands before lane 0's flag
-    cbar();
-    if (lane == 0) {
-#if !DP_WAVEPUB
-      sh.done[s] = 0;                                // slot's counter free for unit j + kRing
-      cbar();
-#endif
-      lds_st(&sh.ready[s], (uint32_t)j + 1u);
-    }
-#if DP_LBPREFETCH
-    // prefetch the next unit's look-back window: its latency overlaps the wait for the data waves
-    have_pre = j + 1 < K;
-    if (have_pre) lb_load(A, u + G, G, 0, pack_prefix(P_incl, S_out), lane, pre);
-#endif
   }
-  PROF_MARK(3);
   PROF_FLUSH(kCoord);
 }
+
+// Data wave: phase A of every unit of the workgroup in order (double-buffered loads two units ahead),
+// phase B of each unit as soon as its prefix is ready, waiting only when kRing units or the event list
+// would be exceeded.
+template <int MODE, int OUT64>
+struct DataWave {
+  const ScanArgs& A;
+  const Tab& T;
+  Shared& sh;
+  uint32_t u0, G, K;
+  int lane, wave;
+  uint32_t ev_head = 0, ev_tail = 0;
+  uint32_t jt = 0;                                   // oldest unit whose phase B is not done
+
+  __device__ DataWave(const ScanArgs& a, const Tab& t, Shared& s, uint32_t u0_, uint32_t g_, uint32_t k_, int l, int w)
+      : A(a), T(t), sh(s), u0(u0_), G(g_), K(k_), lane(l), wave(w) {}
+
+  __device__ __forceinline__ void finish(bool block, int wslot PROF_ARG) {
+    const uint32_t s = jt % kRing;
+    if (block) {
+      PROF_MARK(2);
+      lds_wait_eq(&sh.ready[s], jt + 1u, A.err);
+      PROF_MARK(wslot);
+    }
+    phase_b<MODE, OUT64>(A, sh, s, wave, lane, ev_tail);
+    ++jt;
+    PROF_MARK(4);
+  }
+
+  __device__ __forceinline__ void step(uint32_t k, Geo& g, Geo& gnext, Buf& b, Cursor& cur PROF_ARG) {
+    set_prio(((uint32_t)(wave >> 2) + k) % DP_PRIO_LEVELS);   // the 4 data waves of a SIMD take turns
+    const uint32_t s = k % kRing;
+    WaveRec rec;
+    phase_a<MODE>(A, g, b, wave, lane, sh, ev_head, rec PROF_PASS);
+    ev_head += rec.nev;
+    if (lane == 0) {
+      sh.rec[s][wave] = rec;
+      cbar();
+      lds_add(&sh.done[s], 1u);
+    }
+    // phase B of every unit whose prefix is already there, and (waiting) of the oldest ones until unit
+    // k + 1 has a ring slot and kDenseMax free list entries.  Here, between phase A and the prefetch, this
+    // buffer's registers are free (dense rescans use them) and the next wait_buf's kLoadsPerBuf youngest
+    // vector-memory operations are exactly the prefetch's loads.
+    while (jt <= k) {
+      const bool room = k + 1u - jt < kRing && ev_head - ev_tail <= kEvCap - kDenseMax;
+      const bool rdy = lds_ld(&sh.ready[jt % kRing]) == jt + 1u;
+      if (!rdy && room) break;
+      cbar();
+      finish(!rdy, 3 PROF_PASS);
+    }
+    const Geo g2 = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0 + (k + 2u) * G, cur);
+    load_buf(b, A, g2, wave, lane);
+    g = gnext;
+    gnext = g2;
+    PROF_MARK(5);
+  }
+
+  __device__ void run() {
+    PROF_DECL;
+    Cursor cur{0, 0, 0, 0, 0, 0};
+    Geo g = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0, cur);
+    Geo gnext = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0 + G, cur);
+    Buf bA, bB;
+    load_buf(bA, A, g, wave, lane);
+    load_buf(bB, A, gnext, wave, lane);
+    uint32_t k = 0;
+    while (k < K) {
+      step(k, g, gnext, bA, cur PROF_PASS);
+      if (++k == K) break;
+      step(k, g, gnext, bB, cur PROF_PASS);
+      ++k;
+    }
+    drain_bufs(bA, bB);
+    PROF_MARK(6);
+    while (jt < K) finish(true, 7 PROF_PASS);         // the tail: wait for the workgroup's last prefixes
+    PROF_MARK(6);
+    PROF_FLUSH(wave);
+  }
+};
 
 template <int MODE, int OUT64>
 __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64_t* __restrict__ tab_lo,
@@ -1060,63 +1049,54 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __shared__ Shared sh;
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_u0};
-  const uint64_t G = gridDim.x;
-  const uint64_t u0 = blockIdx.x;
-  const uint64_t K = u0 < A.nunits ? (A.nunits - u0 + G - 1) / G : 0;   // units of this workgroup
+  const uint32_t G = gridDim.x;
+  const uint32_t u0 = blockIdx.x;
+  const uint32_t nunits = (uint32_t)A.nunits;                 // host: < 2^31 units
+  const uint32_t K = u0 < nunits ? (nunits - u0 + G - 1) / G : 0;   // units of this workgroup
   if (threadIdx.x < kRing) {
     sh.done[threadIdx.x] = 0;
-    sh.composed[threadIdx.x] = 0;
-    sh.bdone[threadIdx.x] = 0;
     sh.ready[threadIdx.x] = 0;
   }
-  if (threadIdx.x == 0) sh.bclaim = 0;
   __syncthreads();
-  if (wave == kCoord) {
-    coordinator<MODE>(A, T, u0, G, K, lane, sh);
-  } else {
-    PROF_DECL;
+#ifdef DP_LOADONLY
+  // perf probe only (never a shipped build): the data waves' load structure without any compute or
+  // synchronisation — the ceiling this grid/unit geometry can stream at
+  if (wave != kCoord) {
     Cursor cur{0, 0, 0, 0, 0, 0};
-    Geo g = geo_of(T, A.nchunks, A.nunits, u0, cur);
-    Geo gnext = geo_of(T, A.nchunks, A.nunits, u0 + G, cur);
+    Geo g = geo_of(T, (uint32_t)A.nchunks, nunits, u0, cur);
+    Geo gnext = geo_of(T, (uint32_t)A.nchunks, nunits, u0 + G, cur);
     Buf bA, bB;
     load_buf(bA, A, g, wave, lane);
     load_buf(bB, A, gnext, wave, lane);
-    uint64_t k = 0;
-    PROF_MARK(5);
-    while (k < K) {
-      data_step<MODE, OUT64>(A, T, k, K, u0, G, g, gnext, bA, cur, lane, wave, sh PROF_PASS);
-      if (++k == K) break;
-      data_step<MODE, OUT64>(A, T, k, K, u0, G, g, gnext, bB, cur, lane, wave, sh PROF_PASS);
-      ++k;
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+      Buf& b = (k & 1) ? bB : bA;
+      wait_buf(b);
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) acc ^= b.x[r][0] ^ b.x[r][1] ^ b.x[r][2] ^ b.x[r][3];
+      const Geo g2 = geo_of(T, (uint32_t)A.nchunks, nunits, u0 + (k + 2) * G, cur);
+      load_buf(b, A, g2, wave, lane);
     }
     drain_bufs(bA, bB);
-    PROF_MARK(6);
-#if !DP_STEAL
-    const uint64_t j0 = K > (uint64_t)kBLag ? K - kBLag : 0;
-    for (uint64_t j = j0; j < K; ++j) data_finish<MODE, OUT64>(A, j, lane, wave, sh PROF_PASS);
-#else
-    // drain: phase-B tasks until every task of the workgroup's K units has been claimed
-    const uint32_t all = (uint32_t)kDataWaves * (uint32_t)K;
-    for (uint32_t spins = 0; lds_ld(&sh.bclaim) < all;) {
-      if (try_b_task<MODE, OUT64>(A, K, lane, sh PROF_PASS)) continue;
-      if (++spins > kSpinLimit) {
-        if (lane == 0) atomicOr(A.err, kErrTimeout);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    if (acc == 0x9E3779B9u) atomicOr(A.err, 4u);
+  }
+  return;
 #endif
-    PROF_MARK(6);
-    PROF_FLUSH(wave);
+  if (wave == kCoord) {
+    coordinator<MODE>(A, T, u0, G, K, lane, sh);
+  } else {
+    DataWave<MODE, OUT64> dw(A, T, sh, u0, G, K, lane, wave);
+    dw.run();
   }
 }
 
 // first position >= from (aligned coords) holding the delimiter, inside [from, end); -1 if none.  One wave.
 __device__ uint64_t wave_find(const uint8_t* base, uint64_t from, uint64_t end, uint32_t pat, int lane, bool& found) {
+  const uint32_t key = pat ^ kSel12;
   for (uint64_t a = from & ~15ull; a < end; a += kRowBytes) {
     const uint64_t pa = a + (uint64_t)lane * 16;
     uint32_t m = 0;
-    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), pat) & range16((int64_t)from - (int64_t)pa, (int64_t)end - (int64_t)pa);
+    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), key) & range16((int64_t)from - (int64_t)pa, (int64_t)end - (int64_t)pa);
     const uint64_t bal = __ballot(m != 0u);
     if (bal) {
       const int l = (int)__builtin_ctzll(bal);
@@ -1148,7 +1128,7 @@ __global__ void __launch_bounds__(kWave) fasta_resolve_kernel(ResolveArgs R) {
     const long long idx = R.pending[c];
     if (idx < 0) continue;
     bool found;
-    const uint64_t p = wave_find(R.base, R.chunk_hi[c], R.buf_end, kNL, lane, found);
+    const uint64_t p = wave_find(R.base, R.chunk_hi[c], R.buf_end, 0x0A0A0A0Au, lane, found);
     uint64_t val;
     if (found) val = R.obj_base - R.shift + p + 1;
     else if (R.at_obj_end) val = R.obj_size;
@@ -1443,6 +1423,7 @@ int dp_ctx_create(int device, dp_ctx** out) {
   if (per_cu > occ - 1) per_cu = occ - 1;
   if (per_cu < 1) per_cu = 1;
   c->grid = c->cus * per_cu;
+  if (c->grid > 256) c->grid = 256;   // one look-back window (G <= 256) per unit
   *out = c;
   return DP_OK;
 }

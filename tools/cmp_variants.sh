@@ -1,7 +1,10 @@
+#!/bin/bash
+# Same-box comparison of perf-probe variants (built by tools/build_variants.py): run on the GPU box.
+#   bash tools/cmp_variants.sh name1 name2 ...      (names of dataplug_amd/lib/libdpscan_v_<name>.so; "base" = default)
 mkdir -p gpurun_out && rm -f gpurun_out/cmp.log
-timeout -k 10 300 python -m pytest tests/test_gpu_scan.py -m gpu -x -q > gpurun_out/tcmp.log 2>&1 || exit 1
 for r in 1 2; do
-for L in libdpscan.so libdpscan_head.so libdpscan_v_steal.so libdpscan_v_coordpub.so libdpscan_v_coordpub_nopf.so libdpscan_v_nopf.so libdpscan_v_noprio.so libdpscan_v_coordpub_nopf_noprio.so; do
-  DPSCAN_LIB=dataplug_amd/lib/$L timeout -k 10 120 python tools/probe_perf.py --no-stream --reps 8 | tail -1 >> gpurun_out/cmp.log || exit 1
+for n in "$@"; do
+  L=dataplug_amd/lib/libdpscan_v_$n.so; [ "$n" = base ] && L=dataplug_amd/lib/libdpscan.so
+  DPSCAN_LIB=$L timeout -k 10 120 python tools/probe_perf.py --no-stream --reps 8 | tail -1 >> gpurun_out/cmp.log || exit 1
 done; done
-tail -1 gpurun_out/tcmp.log
+cat gpurun_out/cmp.log

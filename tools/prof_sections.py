@@ -2,9 +2,10 @@
 
     DPSCAN_LIB=dataplug_amd/lib/libdpscan_prof.so python tools/prof_sections.py [--size BYTES]
 
-Data waves:   0 wait for the input buffer (vmcnt)  1 phase A  2 post + prefetch issue  3 wait for the
-              coordinator's prefixes  4 phase B  5 setup  6 drain.
-Coordinator:  0 wait for data waves (done)  1 publish AGG  2 look-back  3 the rest (resolve, hand-off).
+Data waves:   0 wait for the input buffer (vmcnt)  1 phase A  2 publish / ready polls before a blocking wait
+              3 blocking wait for the coordinator's prefix  4 phase B  5 ready polls + prefetch issue  6 drain
+              7 the tail's waits for the last prefixes.
+Coordinator:  0 compose + publish AGG  1 look-back attempts  2 resolve + hand-off  3 idle (nothing to do).
 Reported as the mean over workgroups of each slot's share of the wave's total time.
 """
 from __future__ import annotations
@@ -24,8 +25,8 @@ from dataplug_amd import synth  # noqa: E402
 from dataplug_amd.scan import ScanContext, _lib  # noqa: E402
 from dataplug_amd.scan._lib import check  # noqa: E402
 
-DATA = ["wait_buf", "phase_a", "post_prefetch", "wait_ready", "phase_b", "setup", "drain", "-"]
-COORD = ["wait_done", "publish", "lookback_scan", "rest", "-", "-", "lookback_wait", "-"]
+DATA = ["wait_buf", "phase_a", "pre_wait", "wait_ready", "phase_b", "post_prefetch", "drain", "tail_wait"]
+COORD = ["compose", "lookback_try", "resolve", "idle", "-", "-", "-", "-"]
 
 
 def read(ctx, grid):
@@ -43,13 +44,17 @@ def summarize(p):
     dtot = data.sum(-1, keepdims=True)
     coord = coord.copy()
     spins = coord[:, 4].copy()
-    coord[:, 4] = 0
+    failed = coord[:, 5].copy()
+    resolved = coord[:, 6].copy()
+    coord[:, 4:7] = 0
     ctot = coord.sum(-1, keepdims=True)
     out = {"data_ticks_per_wave": float(dtot.mean())}
     out.update({f"data_{n}": round(float((data / dtot)[..., i].mean()), 3) for i, n in enumerate(DATA) if n != "-"})
     out.update({f"coord_{n}": round(float((coord / ctot)[..., i].mean()), 3) for i, n in enumerate(COORD) if n != "-"})
-    out["coord_spins_per_wg"] = round(float(spins.mean()), 1)
-    busy = data[..., 1] + data[..., 2] + data[..., 4]          # phase A + post + phase B, per (wg, wave)
+    out["coord_attempts_per_wg"] = round(float(spins.mean()), 1)
+    out["coord_incomplete_per_wg"] = round(float(failed.mean()), 1)
+    out["coord_resolved_per_wg"] = round(float(resolved.mean()), 1)
+    busy = data[..., 1] + data[..., 4] + data[..., 5]          # phase A + phase B + post, per (wg, wave)
     out["busy_by_wave"] = [round(float(x), 3) for x in (busy / dtot[..., 0]).mean(0)]
     out["wait_ready_by_wave"] = [round(float(x), 3) for x in (data[..., 3] / dtot[..., 0]).mean(0)]
     tot_wg = dtot[..., 0].mean(1)
