@@ -14,12 +14,12 @@ GZ_OUT = os.path.join(HERE, "lib", "libdpgz.so")            # host-side gzip acc
 ARCH = os.environ.get("DPSCAN_ARCH", "gfx950")
 
 
-def build(verbose: bool = False, prof: bool = False, defines=(), out=None) -> str:
+def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=SRC) -> str:
     out = out or (OUT_PROF if prof else OUT)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-result", "-o", out + ".tmp", SRC]
+           "-Wno-unused-result", "-o", out + ".tmp", src]
     if prof:
         cmd.insert(1, "-DDP_PROF")
     for d in defines:                      # tuning variants, e.g. DP_RING=5 (tools/probe_perf.py)

@@ -46,9 +46,12 @@ constexpr int kCoord = kDataWaves;
 constexpr int kWaves = kDataWaves + 1;
 constexpr int kThreads = kWave * kWaves;           // 1024
 constexpr int kRowBytes = kWave * 16;              // one dwordx4 per lane
-constexpr int kRows = 8;                           // rows per wave per unit
-constexpr int kWaveBytes = kRowBytes * kRows;      // 8 KiB
-constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 120 KiB look-back unit
+constexpr int kRows = 8;                           // rows per input buffer (one load batch per wave)
+constexpr int kBufBytes = kRowBytes * kRows;       // 8 KiB
+constexpr int kHalves = 2;                         // buffers per wave range
+constexpr int kRangeRows = kRows * kHalves;        // 16 rows
+constexpr int kWaveBytes = kBufBytes * kHalves;    // 16 KiB wave range per unit
+constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 240 KiB look-back unit
 #ifndef DP_RING
 #define DP_RING 32
 #endif
@@ -57,6 +60,9 @@ constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 120 KiB look-back unit
 #endif
 #ifndef DP_PRIO
 #define DP_PRIO 1
+#endif
+#ifndef DP_LBFAST
+#define DP_LBFAST 1
 #endif
 #ifndef DP_PRIO_LEVELS
 #define DP_PRIO_LEVELS 4u
@@ -127,13 +133,16 @@ struct ScanArgs {
 __device__ __forceinline__ uint32_t match4(uint32_t w, uint32_t key) {
   return __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFFFFu, w ^ key);
 }
-// match4 bytes (0x00 = 0, 0xFF = -1 as i8) -> 4-bit mask, bit j = byte j matched: 15 - sum of the
-// non-matching weights 1, 2, 4, 8 (v_dot4_i32_i8).
-__device__ __forceinline__ uint32_t nib(uint32_t p) {
-  return (uint32_t)__builtin_amdgcn_sdot4((int)p, 0x08040201, 15, false);
-}
+// match4 bytes (0x00 = 0, 0xFF = -1 as i8) of a lane's 4 dwords -> 16-bit mask, bit i = byte i matched.
+// v_dot4_i32_i8 with weights 1, 2, 4, 8 subtracts the non-matching weights of one dword from its
+// accumulator; chained Horner-style (acc << 4 between dwords) it leaves -(non-match mask), and
+// 0xFFFF + that is the match mask.  4 dot4 + 3 shifts + 1 add.
 __device__ __forceinline__ uint32_t pack16(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
-  return nib(p0) | (nib(p1) << 4) | (nib(p2) << 8) | (nib(p3) << 12);
+  int t = __builtin_amdgcn_sdot4((int)p3, 0x08040201, 0, false);
+  t = __builtin_amdgcn_sdot4((int)p2, 0x08040201, t * 16, false);
+  t = __builtin_amdgcn_sdot4((int)p1, 0x08040201, t * 16, false);
+  t = __builtin_amdgcn_sdot4((int)p0, 0x08040201, t * 16, false);
+  return (uint32_t)(t + 0xFFFF);
 }
 __device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t key) {
   return pack16(match4(v.x, key), match4(v.y, key), match4(v.z, key), match4(v.w, key));
@@ -234,16 +243,6 @@ struct Func {
   uint64_t cF, cT;
   uint32_t sF, sT;
 };
-__device__ __forceinline__ Func f_then(const Func& a, const Func& b) {   // a, then b
-  const uint32_t mF = 0u - (a.sF & 1u), mT = 0u - (a.sT & 1u);
-  const uint64_t mF64 = 0ull - (uint64_t)(a.sF & 1u), mT64 = 0ull - (uint64_t)(a.sT & 1u);
-  Func r;
-  r.cF = a.cF + ((b.cT & mF64) | (b.cF & ~mF64));
-  r.sF = (b.sT & mF) | (b.sF & ~mF);
-  r.cT = a.cT + ((b.cT & mT64) | (b.cF & ~mT64));
-  r.sT = (b.sT & mT) | (b.sF & ~mT);
-  return r;
-}
 __device__ __forceinline__ uint64_t pack_agg(const Func& f) {
   return kStatAgg | ((uint64_t)f.sT << 49) | ((uint64_t)f.sF << 48) | ((f.cT & 0xFFFFFFull) << 24) |
          (f.cF & 0xFFFFFFull);
@@ -304,6 +303,7 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t x, uint64_t old) {
 constexpr int kRowShr1 = 0x111, kRowShr2 = 0x112, kRowShr4 = 0x114, kRowShr8 = 0x118;
 constexpr int kRowBcast15 = 0x142, kRowBcast31 = 0x143;   // gfx9 DPP: lane 15 / 31 to the next row(s)
 constexpr int kWaveShl1 = 0x130;                          // lane l <- lane l + 1
+constexpr int kWaveShr1 = 0x138;                          // lane l <- lane l - 1
 
 template <int CTRL, int ROWS>
 __device__ __forceinline__ LB lb_dpp(const LB& f) {       // identity where there is no source lane
@@ -311,15 +311,6 @@ __device__ __forceinline__ LB lb_dpp(const LB& f) {       // identity where ther
   o.cF = dpp64<CTRL, ROWS>(f.cF, 0ull);
   o.cT = dpp64<CTRL, ROWS>(f.cT, 0ull);
   o.fl = dpp32<CTRL, ROWS>(f.fl, 2u);
-  return o;
-}
-template <int CTRL, int ROWS>
-__device__ __forceinline__ Func fn_dpp(const Func& f) {
-  Func o;
-  o.cF = dpp64<CTRL, ROWS>(f.cF, 0ull);
-  o.cT = dpp64<CTRL, ROWS>(f.cT, 0ull);
-  o.sF = dpp32<CTRL, ROWS>(f.sF, 0u);
-  o.sT = dpp32<CTRL, ROWS>(f.sT, 1u);
   return o;
 }
 
@@ -358,6 +349,50 @@ __device__ __forceinline__ bool lb_reduce(uint64_t (&d)[4], uint32_t u, uint32_t
   // lanes from the nearest one (63) down to the nearest lane holding a prefix must all be published
   const uint64_t need = PB ? ~((1ull << (63 - __builtin_clzll(PB))) - 1ull) : ~0ull;
   if (BB & need) return false;
+  // Fast path.  Line-state maps of units are constant (the unit holds a '\n') or the identity (it does
+  // not); with only constant maps between the nearest prefix and u, every unit's incoming state is the
+  // state bit (bit 48 of AGG and PREFIX descriptors alike) of its farther neighbour, so the prefix is a
+  // plain sum of selected counts.  Any identity map in range: the full functional scan below.
+  if (DP_LBFAST) {
+    const int Lp = 63 - __builtin_clzll(PB);          // the base (slot W) is a prefix: PB != 0
+    uint32_t jp = 4;
+#pragma unroll
+    for (int j = 3; j >= 0; --j)
+      if ((d[j] & kStatMask) == kStatPrefix) jp = (uint32_t)j;
+    const uint32_t kP = 4u * (uint32_t)(63 - Lp) + (uint32_t)__builtin_amdgcn_readlane((int)jp, Lp);
+    // state out of each slot and of the farther neighbour of slot 3 (lane - 1's slot 0)
+    uint32_t so[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) so[j] = (uint32_t)(d[j] >> 48) & 1u;
+    const uint32_t so_far = dpp32<kWaveShr1, 0xF>(so[0], 0u);
+    uint32_t sum = 0, ident = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t k = 4 * rl + j;
+      if (k < kP) {
+        const uint32_t sin = j < 3 ? so[j + 1] : so_far;
+        const uint32_t cF = (uint32_t)d[j] & 0xFFFFFFu, cT = (uint32_t)(d[j] >> 24) & 0xFFFFFFu;
+        sum += sin ? cT : cF;
+        ident |= (uint32_t)((d[j] >> 48) ^ (d[j] >> 49)) & 1u;
+      }
+    }
+    if (__ballot(ident) == 0ull) {
+      uint64_t pv = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if ((uint32_t)j == jp) pv = d[j] & 0xFFFFFFFFFFFFull;
+      // wave sum of the selected counts (< 2^32: at most 255 units of < 2^17 events)
+      sum += dpp32<kRowShr1, 0xF>(sum, 0u);
+      sum += dpp32<kRowShr2, 0xF>(sum, 0u);
+      sum += dpp32<kRowShr4, 0xF>(sum, 0u);
+      sum += dpp32<kRowShr8, 0xF>(sum, 0u);
+      sum += dpp32<kRowBcast15, 0xA>(sum, 0u);
+      sum += dpp32<kRowBcast31, 0xC>(sum, 0u);
+      P = readlane64(pv, Lp) + (uint32_t)__builtin_amdgcn_readlane((int)sum, kWave - 1);
+      S_in = (uint32_t)__builtin_amdgcn_readlane((int)so[0], kWave - 1);
+      return true;
+    }
+  }
   LB f = lb_from_desc(d[3]);
   f = lb_then(f, lb_from_desc(d[2]));
   f = lb_then(f, lb_from_desc(d[1]));
@@ -466,9 +501,12 @@ __device__ __forceinline__ v4i buf_rsrc(const uint8_t* base, uint64_t wbase, int
   return r;
 }
 
-__device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const Geo& g, int wave, int lane) {
-  const v4i r = buf_rsrc(A.base, g.ubase + (uint64_t)wave * kWaveBytes, (g.fl & kGeoValid) ? wave_hi(g, wave) : 0);
-  const uint32_t off0 = (uint32_t)lane * 16u, off1 = off0 + 4096u, offla = (uint32_t)kWaveBytes;
+// half h of data wave w's range of unit g (bytes [h*8 KiB, h*8 KiB + 8 KiB + 4))
+__device__ __forceinline__ void load_buf(Buf& b, const ScanArgs& A, const Geo& g, int wave, int lane, int half) {
+  int hb = (g.fl & kGeoValid) ? wave_hi(g, wave) - half * kBufBytes : 0;
+  hb = hb < 0 ? 0 : (hb > kBufBytes + 16 ? kBufBytes + 16 : hb);
+  const v4i r = buf_rsrc(A.base, g.ubase + (uint64_t)wave * kWaveBytes + (uint64_t)half * kBufBytes, hb);
+  const uint32_t off0 = (uint32_t)lane * 16u, off1 = off0 + 4096u, offla = (uint32_t)kBufBytes;
   static_assert(kRows == 8 && kRowBytes == 1024, "load_buf offsets assume 8 rows of 1 KiB");
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:0" : "=v"(b.x[0]) : "v"(off0), "s"(r) : "memory");
   asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:1024" : "=v"(b.x[1]) : "v"(off0), "s"(r) : "memory");
@@ -530,8 +568,14 @@ struct Shared {
 // store(rank, byte offset in the lane) per event; returns the wave's event count in the row.
 template <class Store>
 __device__ __forceinline__ uint32_t emit_row(uint32_t em, uint32_t rank0, Store&& store) {
+  const uint32_t c = (uint32_t)__popc(em);
+  const uint64_t any1 = __ballot(c != 0u);
+  if (__ballot(c > 1u) == 0ull) {                    // common: at most one event per lane, no loop
+    if (em) store(rank0 + mbcnt(any1), (uint32_t)__builtin_ctz(em));
+    return (uint32_t)__popcll(any1);
+  }
   uint32_t tot;
-  const uint32_t ex = wave_excl<5>((uint32_t)__popc(em), tot);
+  const uint32_t ex = wave_excl<5>(c, tot);
   uint32_t rk = rank0 + ex;
   for (uint32_t x = em; x; x &= x - 1u, ++rk) store(rk, (uint32_t)__builtin_ctz(x));
   return tot;
@@ -611,13 +655,18 @@ __device__ __forceinline__ void fasta_row(const v4u& xr, uint32_t wn, int r, int
     st.S = (uint32_t)((SB | (~H & Sst)) >> 63);                 // the state after lane 63
   }
 }
+// one buffer: rows half*8 .. half*8 + 7 of the wave range
 template <class Store>
-__device__ __forceinline__ void fasta_rows(const v4u (&x)[kRows], uint32_t la, int lo, int hi, int lane, FState& st,
-                                           Store&& store) {
+__device__ __forceinline__ void fasta_rows(const v4u (&x)[kRows], uint32_t la, int half, int lo, int hi, int lane,
+                                           FState& st, Store&& store) {
+#ifdef DP_NOROWS
+  return;   // perf probe only: the per-unit machinery without any row work
+#endif
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
-    if (r * kRowBytes >= hi) break;
-    fasta_row(x[r], (r + 1 < kRows) ? x[(r + 1) & (kRows - 1)][0] : la, r, lo, hi, lane, st, store);
+    const int R = half * kRows + r;
+    if (R * kRowBytes >= hi) break;
+    fasta_row(x[r], (r + 1 < kRows) ? x[(r + 1) & (kRows - 1)][0] : la, R, lo, hi, lane, st, store);
   }
 }
 
@@ -638,24 +687,32 @@ __device__ __forceinline__ void delim_row(const v4u& xr, int r, int lo, int hi, 
   }
 }
 template <class Store>
-__device__ __forceinline__ void delim_rows(const v4u (&x)[kRows], int lo, int hi, uint32_t key, int lane, uint32_t& nev,
-                                           Store&& store) {
+__device__ __forceinline__ void delim_rows(const v4u (&x)[kRows], int half, int lo, int hi, uint32_t key, int lane,
+                                           uint32_t& nev, Store&& store) {
+#ifdef DP_NOROWS
+  return;
+#endif
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
-    if (r * kRowBytes >= hi) break;
-    delim_row(x[r], r, lo, hi, key, lane, nev, store);
+    const int R = half * kRows + r;
+    if (R * kRowBytes >= hi) break;
+    delim_row(x[r], R, lo, hi, key, lane, nev, store);
   }
 }
 
 // ------------------------------------------------------------------------------------------ phase A / B
-// Phase A of one unit on one data wave: events to the wave's list (ranks from ev_head), summary to rec.
+// Phase A of one unit on one data wave, one buffer (half) at a time: events to the wave's list (ranks
+// from ev_head), then the range's summary to rec.
+struct PhaseA {
+  FState st;                       // FASTA state; DELIM uses st.nev only
+  uint64_t wbase;
+  int lo, hi;
+};
 template <int MODE>
-__device__ __forceinline__ void phase_a(const ScanArgs& A, const Geo& g, Buf& b, int wave, int lane, Shared& sh,
-                                        uint32_t ev_head, WaveRec& rec PROF_ARG) {
-  wait_buf(b);                                       // this buffer landed; the other one stays in flight
+__device__ __forceinline__ void phase_a_half(const ScanArgs& A, PhaseA& pa, Buf& b, int half, int wave, int lane,
+                                             Shared& sh, uint32_t ev_head PROF_ARG) {
+  wait_buf(b);                                       // this buffer landed; the next one stays in flight
   PROF_MARK(0);
-  const uint64_t wbase = g.ubase + (uint64_t)wave * kWaveBytes;
-  const int lo = wave_lo(g, wave), hi = wave_hi(g, wave);
   v4u x[kRows];
 #pragma unroll
   for (int r = 0; r < kRows; ++r) x[r] = b.x[r];
@@ -663,10 +720,18 @@ __device__ __forceinline__ void phase_a(const ScanArgs& A, const Geo& g, Buf& b,
   auto keep = [&](uint32_t rk, uint32_t pos) {
     if (rk < kDenseMax) evw[(ev_head + rk) & kEvMask] = (uint16_t)pos;
   };
-  uint32_t nev, fl;
   if constexpr (MODE == kFasta) {
-    FState st{0u, 0u, 0u, -1, 0u, 0u};
-    fasta_rows(x, b.la, lo, hi, lane, st, keep);
+    fasta_rows(x, b.la, half, pa.lo, pa.hi, lane, pa.st, keep);
+  } else {
+    delim_rows(x, half, pa.lo, pa.hi, A.delim ^ kSel12, lane, pa.st.nev, keep);
+  }
+  PROF_MARK(1);
+}
+template <int MODE>
+__device__ __forceinline__ void phase_a_rec(PhaseA& pa, const Geo& g, int wave, uint32_t ev_head, WaveRec& rec) {
+  FState& st = pa.st;
+  uint32_t fl;
+  if constexpr (MODE == kFasta) {
     if (!st.nlseen) st.fV = st.S;
     uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
     if ((g.fl & kGeoFirst) && wave == 0) { cT = st.cnt; sT = st.S; }   // chunk start: the state is reset
@@ -674,21 +739,17 @@ __device__ __forceinline__ void phase_a(const ScanArgs& A, const Geo& g, Buf& b,
     rec.cT = cT;
     fl = st.S | (sT << 1) | (st.fV << 2);
     rec.fn = (uint32_t)(st.fn + 1);
-    nev = st.nev;
   } else {
-    nev = 0;
-    delim_rows(x, lo, hi, A.delim ^ kSel12, lane, nev, keep);
-    rec.cF = rec.cT = nev;
+    rec.cF = rec.cT = st.nev;
     fl = 0;
     rec.fn = 0;
   }
-  const bool dense = nev > kDenseMax;
-  rec.wbase = wbase;
-  rec.lohi = (uint32_t)lo | ((uint32_t)hi << 16);
+  const bool dense = st.nev > kDenseMax;
+  rec.wbase = pa.wbase;
+  rec.lohi = (uint32_t)pa.lo | ((uint32_t)pa.hi << 16);
   rec.fl = fl | (dense ? kFlDense : 0u);
   rec.ev0 = ev_head;
-  rec.nev = dense ? 0u : nev;
-  PROF_MARK(1);
+  rec.nev = dense ? 0u : st.nev;
 }
 
 // Dense phase B: rescan the range from the input with its true state and count, writing the output
@@ -718,7 +779,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
       put<OutT>(A.out, slot < last ? slot : last, val);
     };
 #pragma unroll 1
-    for (int r = 0; r < kRows && r * kRowBytes < hi; ++r) {
+    for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) {
       const int an = (r + 1) * kRowBytes;
       const uint32_t wn = an + 4 <= hi16 ? *reinterpret_cast<const uint32_t*>(src + an) : 0u;
       fasta_row(row_in(r), wn, r, lo, hi, lane, st, out);
@@ -742,7 +803,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
     };
     const uint32_t key = A.delim ^ kSel12;
 #pragma unroll 1
-    for (int r = 0; r < kRows && r * kRowBytes < hi; ++r) delim_row(row_in(r), r, lo, hi, key, lane, n, out);
+    for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) delim_row(row_in(r), r, lo, hi, key, lane, n, out);
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
@@ -816,26 +877,43 @@ __device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint3
 
 // The unit's 15 wave summaries composed lane-parallel: lane i < 15 holds wave i, an inclusive DPP scan over
 // row 0 gives every wave's exclusive prefix function (lane i-1's inclusive) and the unit's function (lane 15,
-// whose own summary is the identity).
+// whose own summary is the identity).  Counts of one unit fit 32 bits.
+struct Func32 {
+  uint32_t cF, cT, sF, sT;
+};
+__device__ __forceinline__ Func32 f32_then(const Func32& a, const Func32& b) {   // a, then b
+  Func32 r;
+  r.cF = a.cF + (a.sF ? b.cT : b.cF);
+  r.sF = a.sF ? b.sT : b.sF;
+  r.cT = a.cT + (a.sT ? b.cT : b.cF);
+  r.sT = a.sT ? b.sT : b.sF;
+  return r;
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ Func32 f32_dpp(const Func32& f) {   // identity where there is no source lane
+  return Func32{dpp32<CTRL, ROWS>(f.cF, 0u), dpp32<CTRL, ROWS>(f.cT, 0u), dpp32<CTRL, ROWS>(f.sF, 0u),
+                dpp32<CTRL, ROWS>(f.sT, 1u)};
+}
 __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
-  Func w = Func{0, 0, 0, 1};
+  Func32 w = Func32{0, 0, 0, 1};
   if (lane < kDataWaves) {
     const WaveRec& r = sh.rec[s][lane];
     const uint32_t fl = r.fl;
-    w = Func{r.cF, r.cT, fl & 1u, (fl >> 1) & 1u};
+    w = Func32{r.cF, r.cT, fl & 1u, (fl >> 1) & 1u};
   }
-  Func inc = w;
-  inc = f_then(fn_dpp<kRowShr1, 0xF>(inc), inc);
-  inc = f_then(fn_dpp<kRowShr2, 0xF>(inc), inc);
-  inc = f_then(fn_dpp<kRowShr4, 0xF>(inc), inc);
-  inc = f_then(fn_dpp<kRowShr8, 0xF>(inc), inc);
-  const Func ex = fn_dpp<kRowShr1, 0xF>(inc);
+  Func32 inc = w;
+  inc = f32_then(f32_dpp<kRowShr1, 0xF>(inc), inc);
+  inc = f32_then(f32_dpp<kRowShr2, 0xF>(inc), inc);
+  inc = f32_then(f32_dpp<kRowShr4, 0xF>(inc), inc);
+  inc = f32_then(f32_dpp<kRowShr8, 0xF>(inc), inc);
+  const Func32 ex = f32_dpp<kRowShr1, 0xF>(inc);
   if (lane < kDataWaves) {
-    sh.exF[s][lane] = (uint32_t)ex.cF;
-    sh.exT[s][lane] = (uint32_t)ex.cT;
+    sh.exF[s][lane] = ex.cF;
+    sh.exT[s][lane] = ex.cT;
     sh.es[s][lane] = (ex.sF & 1u) | ((ex.sT & 1u) << 1);
   }
-  const Func unit = Func{readlane64(inc.cF, kDataWaves), readlane64(inc.cT, kDataWaves),
+  const Func unit = Func{(uint32_t)__builtin_amdgcn_readlane((int)inc.cF, kDataWaves),
+                         (uint32_t)__builtin_amdgcn_readlane((int)inc.cT, kDataWaves),
                          (uint32_t)__builtin_amdgcn_readlane((int)inc.sF, kDataWaves),
                          (uint32_t)__builtin_amdgcn_readlane((int)inc.sT, kDataWaves)};
   if (lane == 0) {
@@ -989,11 +1067,23 @@ struct DataWave {
     PROF_MARK(4);
   }
 
-  __device__ __forceinline__ void step(uint32_t k, Geo& g, Geo& gnext, Buf& b, Cursor& cur PROF_ARG) {
+  // Unit k: phase A over buffer A (first 8 KiB of the range) -> prefetch A of unit k + 1 -> phase A over
+  // buffer B -> publish -> phase B of ready units -> prefetch B of unit k + 1.  While either buffer is being
+  // scanned the other one is in flight.
+  __device__ __forceinline__ void step(uint32_t k, Geo& g, Buf& bA, Buf& bB, Cursor& cur PROF_ARG) {
     set_prio(((uint32_t)(wave >> 2) + k) % DP_PRIO_LEVELS);   // the 4 data waves of a SIMD take turns
     const uint32_t s = k % kRing;
+    const Geo gn = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0 + (k + 1u) * G, cur);
+    PhaseA pa;
+    pa.st = FState{0u, 0u, 0u, -1, 0u, 0u};
+    pa.wbase = g.ubase + (uint64_t)wave * kWaveBytes;
+    pa.lo = wave_lo(g, wave);
+    pa.hi = wave_hi(g, wave);
+    phase_a_half<MODE>(A, pa, bA, 0, wave, lane, sh, ev_head PROF_PASS);
+    load_buf(bA, A, gn, wave, lane, 0);
+    phase_a_half<MODE>(A, pa, bB, 1, wave, lane, sh, ev_head PROF_PASS);
     WaveRec rec;
-    phase_a<MODE>(A, g, b, wave, lane, sh, ev_head, rec PROF_PASS);
+    phase_a_rec<MODE>(pa, g, wave, ev_head, rec);
     ev_head += rec.nev;
     if (lane == 0) {
       sh.rec[s][wave] = rec;
@@ -1001,8 +1091,8 @@ struct DataWave {
       lds_add(&sh.done[s], 1u);
     }
     // phase B of every unit whose prefix is already there, and (waiting) of the oldest ones until unit
-    // k + 1 has a ring slot and kDenseMax free list entries.  Here, between phase A and the prefetch, this
-    // buffer's registers are free (dense rescans use them) and the next wait_buf's kLoadsPerBuf youngest
+    // k + 1 has a ring slot and kDenseMax free list entries.  Here, between phase A and the prefetch, B's
+    // registers are free (dense rescans use them) and the next wait_buf's kLoadsPerBuf youngest
     // vector-memory operations are exactly the prefetch's loads.
     while (jt <= k) {
       const bool room = k + 1u - jt < kRing && ev_head - ev_tail <= kEvCap - kDenseMax;
@@ -1011,10 +1101,8 @@ struct DataWave {
       cbar();
       finish(!rdy, 3 PROF_PASS);
     }
-    const Geo g2 = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0 + (k + 2u) * G, cur);
-    load_buf(b, A, g2, wave, lane);
-    g = gnext;
-    gnext = g2;
+    load_buf(bB, A, gn, wave, lane, 1);
+    g = gn;
     PROF_MARK(5);
   }
 
@@ -1022,17 +1110,10 @@ struct DataWave {
     PROF_DECL;
     Cursor cur{0, 0, 0, 0, 0, 0};
     Geo g = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0, cur);
-    Geo gnext = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0 + G, cur);
     Buf bA, bB;
-    load_buf(bA, A, g, wave, lane);
-    load_buf(bB, A, gnext, wave, lane);
-    uint32_t k = 0;
-    while (k < K) {
-      step(k, g, gnext, bA, cur PROF_PASS);
-      if (++k == K) break;
-      step(k, g, gnext, bB, cur PROF_PASS);
-      ++k;
-    }
+    load_buf(bA, A, g, wave, lane, 0);
+    load_buf(bB, A, g, wave, lane, 1);
+    for (uint32_t k = 0; k < K; ++k) step(k, g, bA, bB, cur PROF_PASS);
     drain_bufs(bA, bB);
     PROF_MARK(6);
     while (jt < K) finish(true, 7 PROF_PASS);         // the tail: wait for the workgroup's last prefixes
@@ -1064,18 +1145,20 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   if (wave != kCoord) {
     Cursor cur{0, 0, 0, 0, 0, 0};
     Geo g = geo_of(T, (uint32_t)A.nchunks, nunits, u0, cur);
-    Geo gnext = geo_of(T, (uint32_t)A.nchunks, nunits, u0 + G, cur);
     Buf bA, bB;
-    load_buf(bA, A, g, wave, lane);
-    load_buf(bB, A, gnext, wave, lane);
+    load_buf(bA, A, g, wave, lane, 0);
+    load_buf(bB, A, g, wave, lane, 1);
     uint32_t acc = 0;
     for (uint32_t k = 0; k < K; ++k) {
-      Buf& b = (k & 1) ? bB : bA;
-      wait_buf(b);
+      const Geo gn = geo_of(T, (uint32_t)A.nchunks, nunits, u0 + (k + 1) * G, cur);
+      wait_buf(bA);
 #pragma unroll
-      for (int r = 0; r < kRows; ++r) acc ^= b.x[r][0] ^ b.x[r][1] ^ b.x[r][2] ^ b.x[r][3];
-      const Geo g2 = geo_of(T, (uint32_t)A.nchunks, nunits, u0 + (k + 2) * G, cur);
-      load_buf(b, A, g2, wave, lane);
+      for (int r = 0; r < kRows; ++r) acc ^= bA.x[r][0] ^ bA.x[r][1] ^ bA.x[r][2] ^ bA.x[r][3];
+      load_buf(bA, A, gn, wave, lane, 0);
+      wait_buf(bB);
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) acc ^= bB.x[r][0] ^ bB.x[r][1] ^ bB.x[r][2] ^ bB.x[r][3];
+      load_buf(bB, A, gn, wave, lane, 1);
     }
     drain_bufs(bA, bB);
     if (acc == 0x9E3779B9u) atomicOr(A.err, 4u);

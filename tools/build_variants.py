@@ -1,6 +1,7 @@
 """Build perf-probe variants of libdpscan.so side by side (dataplug_amd/lib/libdpscan_v_<name>.so).
 
     python tools/build_variants.py name=DEF1,DEF2=3 name2=DEF3 ...   # '-' for no defines
+    python tools/build_variants.py head@HEAD=- ...                   # the source as of a git revision
 
 Variants are diagnostics for same-box comparisons (tools/probe_perf.py with DPSCAN_LIB=...); the shipped
 library is always the default build (python -m dataplug_amd.build).
@@ -13,21 +14,33 @@ from concurrent.futures import ThreadPoolExecutor
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from dataplug_amd.build import HERE, build  # noqa: E402
+import subprocess  # noqa: E402
+
+from dataplug_amd.build import HERE, SRC, build  # noqa: E402
 
 
 def main(specs):
     jobs = []
     for s in specs:
         name, _, defs = s.partition("=")
+        name, _, rev = name.partition("@")
         defines = [] if defs in ("", "-") else defs.split(",")
         prof = "DP_PROF" in defines
         defines = [d for d in defines if d != "DP_PROF"]
         out = os.path.join(HERE, "lib", f"libdpscan_v_{name}.so")
-        jobs.append((defines, prof, out))
+        src = SRC
+        if rev:                                  # next to the real source so its #include resolves
+            src = os.path.join(os.path.dirname(SRC), f"_rev_{name}.hip")
+            with open(src, "w") as fh:
+                fh.write(subprocess.run(["git", "show", f"{rev}:dataplug_amd/csrc/dpscan.hip"], check=True,
+                                        capture_output=True, text=True).stdout)
+        jobs.append((defines, prof, out, src))
     with ThreadPoolExecutor(4) as ex:
-        for out in ex.map(lambda j: build(defines=j[0], prof=j[1], out=j[2]), jobs):
+        for out in ex.map(lambda j: build(defines=j[0], prof=j[1], out=j[2], src=j[3]), jobs):
             print(out)
+    for j in jobs:
+        if j[3] != SRC:
+            os.remove(j[3])
 
 
 if __name__ == "__main__":

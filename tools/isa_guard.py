@@ -1,9 +1,9 @@
 """ISA guard for the hand-waited input loads of scan_kernel (dataplug_amd/csrc/dpscan.hip).
 
 The data waves issue their buffer loads as inline asm and wait with one explicit `s_waitcnt vmcnt(9)`.
-The compiler knows nothing about that contract, so this checks the generated gfx950 assembly: between a
-`buffer_load_dword*` into register(s) R and the next `s_waitcnt vmcnt`, no instruction may read or write
-R.  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
+The compiler knows nothing about that contract, so this checks the generated gfx950 assembly: on every
+control-flow path from a `buffer_load_dword*` into register(s) R to the next `s_waitcnt vmcnt`, no
+instruction may read or write R (dataflow over the kernel's basic blocks).  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
 (without an argument it compiles the kernel with -save-temps into a temp dir).
 """
 from __future__ import annotations
@@ -35,44 +35,90 @@ def regs(tok: str):
     return {int(m.group(1))} if m else set()
 
 
+BRANCH_RE = re.compile(r"^s_(cbranch_\w+|branch)\s+(\.?\w+)")
+
+
+def _blocks(body: str):
+    """Split a kernel body into basic blocks: (label, [instructions], successors)."""
+    blocks, cur, label = [], [], "<entry>"
+    for line in body.splitlines():
+        s = line.split(";")[0].strip()
+        if not s:
+            continue
+        if s.endswith(":"):
+            blocks.append([label, cur])
+            label, cur = s[:-1], []
+            continue
+        cur.append(s)
+    blocks.append([label, cur])
+    out = []
+    for i, (lab, ins) in enumerate(blocks):
+        succ = set()
+        fall = True
+        for s in ins:
+            m = BRANCH_RE.match(s)
+            if m:
+                succ.add(m.group(2))
+                if m.group(1) == "branch":
+                    fall = False
+            if s.split()[0] in ("s_endpgm", "s_setpc_b64"):
+                fall = False
+        if fall and i + 1 < len(blocks):
+            succ.add(blocks[i + 1][0])
+        out.append((lab, ins, succ))
+    return out
+
+
+def _scan(ins, pending, problems, k):
+    """Run one block: returns the pending set at its end (registers with an un-waited input load)."""
+    pending = set(pending)
+    for s in ins:
+        if s.startswith("s_waitcnt") and "vmcnt" in s:
+            pending.clear()
+            continue
+        toks = re.split(r"[\s,]+", s)
+        used = set()
+        for t in toks[1:]:
+            used |= regs(t)
+        if toks[0].startswith("buffer_load_dword"):
+            dst = regs(toks[1])
+            srcs = set()
+            for t in toks[2:]:
+                srcs |= regs(t)
+            if problems is not None and srcs & pending:
+                problems.append((k, s))
+            pending |= dst
+            continue
+        if problems is not None and used & pending:
+            problems.append((k, s))
+    return pending
+
+
 def check(asm_path: str):
+    """Dataflow over the control-flow graph: a register written by an input buffer load stays "pending" on
+    every path until an `s_waitcnt vmcnt`; no instruction on any path may read or write it meanwhile."""
     text = open(asm_path).read()
     problems = []
     kernels = KERNEL_RE.findall(text)
     assert len(kernels) == 4, kernels
     for k in kernels:
-        body = text[text.index(k + ":"):]
+        body = text[text.index(k + ":") + len(k) + 1:]
         body = body[:body.index(".Lfunc_end")]
-        pending = set()          # registers with an un-waited input load
-        prev_uncond = False
-        for ln, line in enumerate(body.splitlines()):
-            s = line.split(";")[0].strip()
-            if not s:
-                continue
-            if s.endswith(":"):
-                # conservative: a block can be entered from anywhere, so pending loads stay pending
-                # until a vmcnt wait (textual order; may over-report, never under-reports a path the
-                # layout puts after the loads)
-                continue
-            prev_uncond = s.split()[0] in ("s_branch", "s_endpgm", "s_setpc_b64")
-            if s.startswith("s_waitcnt") and "vmcnt" in s:
-                pending.clear()
-                continue
-            toks = re.split(r"[\s,]+", s)
-            used = set()
-            for t in toks[1:]:
-                used |= regs(t)
-            if toks[0].startswith("buffer_load_dword"):
-                dst = regs(toks[1])
-                srcs = set()
-                for t in toks[2:]:
-                    srcs |= regs(t)
-                if srcs & pending:
-                    problems.append((k, ln, s))
-                pending |= dst
-                continue
-            if used & pending:
-                problems.append((k, ln, s))
+        blocks = _blocks(body)
+        index = {lab: i for i, (lab, _, _) in enumerate(blocks)}
+        pin = [set() for _ in blocks]
+        work = list(range(len(blocks)))
+        while work:
+            i = work.pop()
+            lab, ins, succ = blocks[i]
+            pout = _scan(ins, pin[i], None, k)
+            for t in succ:
+                j = index.get(t)
+                if j is not None and not pout <= pin[j]:
+                    pin[j] |= pout
+                    work.append(j)
+        for i, (lab, ins, succ) in enumerate(blocks):
+            _scan(ins, pin[i], problems, k)
     return problems
 
 

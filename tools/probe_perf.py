@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--size", type=int, default=4 << 30)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-stream", action="store_true", help="skip the stream-read calibration")
+    ap.add_argument("--only", choices=["fasta", "delim", "nogt"], help="run one workload (for rocprofv3 --pmc)")
     args = ap.parse_args()
     size = args.size
     ctx = ScanContext(0)
@@ -59,23 +60,26 @@ def main():
         ctx.fasta_index_async(d.ptr, size, 0, size, chunks, out.ptr, False, cap)
         ctx.fasta_result(len(chunks) // 2)
 
-    k, w = timed(ctx, fasta, args.reps)
-    res["fasta_synth_kernel_GBps"] = round(size / k / 1e9, 1)
-    res["fasta_synth_wall_GBps"] = round(size / w / 1e9, 1)
+    if args.only in (None, "fasta"):
+        k, w = timed(ctx, fasta, args.reps)
+        res["fasta_synth_kernel_GBps"] = round(size / k / 1e9, 1)
+        res["fasta_synth_wall_GBps"] = round(size / w / 1e9, 1)
 
     def delim():
         ctx.delim_index_async(d.ptr, size, 0, 0, size, 10, 1, 0, out.ptr, False, size // 16)
         ctx.delim_result()
 
-    k, w = timed(ctx, delim, args.reps)
-    res["delim_on_fasta_kernel_GBps"] = round(size / k / 1e9, 1)
+    if args.only in (None, "delim"):
+        k, w = timed(ctx, delim, args.reps)
+        res["delim_on_fasta_kernel_GBps"] = round(size / k / 1e9, 1)
 
     # FASTA-shaped bytes without any '>': the row fast path everywhere
     line = np.frombuffer(b"ACGT" * 15 + b"\n", np.uint8)
     plain = np.resize(line, size)
-    ctx.h2d(d.ptr, plain)
-    k, w = timed(ctx, fasta, args.reps)
-    res["fasta_no_gt_kernel_GBps"] = round(size / k / 1e9, 1)
+    if args.only in (None, "nogt"):
+        ctx.h2d(d.ptr, plain)
+        k, w = timed(ctx, fasta, args.reps)
+        res["fasta_no_gt_kernel_GBps"] = round(size / k / 1e9, 1)
     g, ub = ctx.geometry()
     res["grid"] = g
     res["unit_bytes"] = ub
