@@ -8,12 +8,20 @@ that is already resident in HBM: chunk-plan upload, the single-pass scan kernel,
 resolve kernel and the read-back of the pair count / per-chunk state (the index itself stays in HBM;
 the H2D/D2H-inclusive end-to-end rate is reported separately).
 
+Steps are issued the way a caller indexing a stream of objects would: two scan contexts (streams)
+alternate, and step k + 1 is enqueued before step k's result is collected, so one step's host round trip
+hides behind the next step's scan.  Every step does the whole pass and reads back its result.  `value`
+comes from K such steps whose scans may overlap on the GPU (the next object's scan starts on the CUs the
+previous one's last workgroups leave idle); `serialized` repeats the K steps with each scan waiting on the
+device for the previous one.
+
 Multi-GPU (``torch.distributed.run --nproc-per-node N``): one process per GPU, each indexing its own
 object (independent objects/chunks, no collective on the data path; weak scaling).  Barrier + device
 sync bracket the K timed steps; the max time over ranks is reported.
 
 Also measured inside this run: the scan kernel's average duration from HIP events on its own stream
-(-> roofline), and, on rank 0 at N = 1, the reference algorithm on the host cores (cpu_baseline).
+over the K serialized launches (-> roofline), and, on rank 0 at N = 1, the reference algorithm on the
+host cores (cpu_baseline).
 """
 from __future__ import annotations
 
@@ -131,6 +139,7 @@ def main():
     from dataplug_amd.scan import ScanContext
 
     ctx = ScanContext(local)
+    ctx2 = ScanContext(local)       # second stream + workspace: step k+1 is queued while step k's result is read
     size = args.size
     chunk_size = math.ceil(size / args.chunks)
     plan = [(i * chunk_size, size if chunk_size == size // chunk_size - 1 else (i + 1) * chunk_size)
@@ -144,28 +153,58 @@ def main():
     d_in = ctx.workspace("bench_in", size + 64)
     ctx.h2d(d_in.ptr, host)
     cap = size // 256 + 1024
-    d_out = ctx.workspace("bench_out", 8 * cap)
+    ctxs = (ctx, ctx2)
+    d_outs = (ctx.workspace("bench_out", 8 * cap), ctx2.workspace("bench_out", 8 * cap))
 
-    def step():
-        ctx.fasta_index_async(d_in.ptr, size, 0, size, chunks, d_out.ptr, False, cap)
-        return ctx.fasta_result(len(plan))
+    def launch(i):
+        ctxs[i % 2].fasta_index_async(d_in.ptr, size, 0, size, chunks, d_outs[i % 2].ptr, False, cap)
 
-    for _ in range(args.warmup):
-        n_pairs, pending, cend = step()
-    ctx.timing(True)
-    ctx.timing_read()
-    barrier(dist, local)
-    ctx.sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        n_pairs, pending, cend = step()
-    ctx.sync()
-    barrier(dist, local)
-    dt = time.perf_counter() - t0
-    kern_ms, launches = ctx.timing_read()
-    ctx.timing(False)
+    def collect(i):
+        return ctxs[i % 2].fasta_result(len(plan))
+
+    for i in range(max(2, args.warmup)):            # warms both contexts (workspaces, code objects)
+        launch(i)
+        collect(i)
+
+    def run_steps(serialize: bool):
+        """K steps; returns (wall seconds, last result).  Step k + 1 is enqueued on the other context's
+        stream before step k's result is collected, so the host round trip of one step hides behind the
+        next step's scan.  serialize: step k + 1 waits on the device for step k (no kernel overlap)."""
+        barrier(dist, local)
+        ctx.sync()
+        ctx2.sync()
+        t0 = time.perf_counter()
+        launch(0)
+        for i in range(1, args.steps):
+            if serialize:
+                ctxs[i % 2].wait_for(ctxs[(i - 1) % 2])
+            launch(i)
+            collect(i - 1)
+        res = collect(args.steps - 1)
+        ctx.sync()
+        ctx2.sync()
+        barrier(dist, local)
+        return time.perf_counter() - t0, res
+
+    # (1) serialized steps, HIP events on each context's own stream around every scan launch: the scan
+    #     kernel's own duration (roofline.achieved), and the throughput without any kernel overlap
+    for c in ctxs:
+        c.timing(True)
+        c.timing_read()
+    dt_ser, _ = run_steps(serialize=True)
+    kern_ms, launches = 0.0, 0
+    for c in ctxs:
+        ms, n = c.timing_read()
+        c.timing(False)
+        kern_ms += ms
+        launches += n
+    # (2) the K timed steps of `value`: consecutive objects' scans may overlap on the GPU (the next one
+    #     starts on the CUs the previous one's last workgroups leave idle)
+    dt, (n_pairs, pending, cend) = run_steps(serialize=False)
+    d_out = d_outs[(args.steps - 1) % 2]
 
     dt_max = max_over_ranks(dist, local, dt)
+    dt_ser_max = max_over_ranks(dist, local, dt_ser)
     total_bytes = sum_over_ranks(dist, local, float(size) * args.steps)
     total_offsets = sum_over_ranks(dist, local, 2.0 * n_pairs * args.steps)
     kern_avg_s = kern_ms / 1e3 / max(1, launches)
@@ -213,6 +252,9 @@ def main():
                        "object_bytes": size, "chunks": len(plan), "pairs": int(n_pairs),
                        "parallelism": f"independent objects x{world}, no collective"},
             "offsets_per_s": round(total_offsets / dt_max, 1),
+            "serialized": {"value": round(total_bytes / dt_ser_max / GiB, 3), "unit": "GiB/s",
+                           "ms_per_step": round(dt_ser_max / args.steps * 1e3, 4),
+                           "note": "same K steps, each scan waiting on the device for the previous one"},
             "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                          "traffic": None if traffic is None else int(traffic),

@@ -34,6 +34,7 @@ SIGNATURES = [
     ("dp_ctx_get_stream", _c.c_int, [_p, _c.POINTER(_p)]),
     ("dp_ctx_set_stream", _c.c_int, [_p, _p]),
     ("dp_ctx_device", _c.c_int, [_p, _c.POINTER(_c.c_int)]),
+    ("dp_ctx_wait", _c.c_int, [_p, _p]),
     ("dp_malloc", _c.c_int, [_p, _u64, _c.POINTER(_p)]),
     ("dp_free", _c.c_int, [_p, _p]),
     ("dp_host_alloc", _c.c_int, [_u64, _c.POINTER(_p)]),

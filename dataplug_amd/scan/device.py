@@ -133,6 +133,10 @@ class ScanContext:
     def set_stream(self, stream: Optional[int]) -> None:
         check(self.lib.dp_ctx_set_stream(self.handle, ctypes.c_void_p(stream or 0)))
 
+    def wait_for(self, other: "ScanContext") -> None:
+        """This context's stream waits (on the device) for everything enqueued on ``other``'s so far."""
+        check(self.lib.dp_ctx_wait(self.handle, other.handle))
+
     # ---------------------------------------------------------------- FASTA
     def fasta_index(self, d_buf: int, buf_len: int, buf_base: int, obj_size: int,
                     chunks: Sequence[Tuple[int, int]], u64: bool = False, cap: Optional[int] = None):

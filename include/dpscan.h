@@ -48,6 +48,10 @@ int dp_ctx_destroy(dp_ctx* ctx);
 int dp_ctx_get_stream(dp_ctx* ctx, void** stream);
 int dp_ctx_set_stream(dp_ctx* ctx, void* stream);          /* NULL restores the ctx's own stream */
 int dp_ctx_device(dp_ctx* ctx, int* device);
+/* Make ctx's stream wait (on the device, no host sync) for everything enqueued so far on other's
+ * stream: a device-scope event, so a caller alternating two contexts keeps its scans serialized on
+ * the GPU while it collects one result and enqueues the next (bench.py). */
+int dp_ctx_wait(dp_ctx* ctx, dp_ctx* other);
 
 int dp_malloc(dp_ctx* ctx, uint64_t bytes, void** dptr);   /* device memory on the ctx's device */
 int dp_free(dp_ctx* ctx, void* dptr);

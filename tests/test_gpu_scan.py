@@ -158,3 +158,28 @@ def test_find_delim(ctx):
     a = np.frombuffer(b"x" * 5000 + b"\n" + b"y" * 10, np.uint8)
     assert ctx.find_delim_host(a, 100, 100) == 5100
     assert ctx.find_delim_host(a, 100, 5101) == -1
+
+
+def test_two_contexts_ordered_by_ctx_wait():
+    # bench.py's issue pattern: two contexts alternate, each launch behind a device-side wait on the other
+    from dataplug_amd.scan import ScanContext
+    a = synth.fasta((8 << 20) + 99, 11)
+    plan = cpu_ref.chunk_plan(len(a), math.ceil(len(a) / 4))
+    exp = dpref.fasta_pairs(a, plan)
+    ctxs = (ScanContext(0), ScanContext(0))
+    d = ctxs[0].workspace("in", len(a) + 64)
+    ctxs[0].h2d(d.ptr, a)
+    chunks = np.ascontiguousarray(np.asarray(plan, np.uint64).reshape(-1))
+    cap = len(a) // 256
+    outs = [c.workspace("out", 8 * cap) for c in ctxs]
+    ctxs[0].fasta_index_async(d.ptr, len(a), 0, len(a), chunks, outs[0].ptr, False, cap)
+    for i in range(1, 6):
+        ctxs[i % 2].wait_for(ctxs[(i - 1) % 2])
+        ctxs[i % 2].fasta_index_async(d.ptr, len(a), 0, len(a), chunks, outs[i % 2].ptr, False, cap)
+        n, pending, _ = ctxs[(i - 1) % 2].fasta_result(len(plan))
+        got = ctxs[(i - 1) % 2].d2h(np.empty((n, 2), np.uint32), outs[(i - 1) % 2].ptr)
+        assert (pending == -1).all() and np.array_equal(got.astype(np.uint64), exp)
+    n, _, _ = ctxs[1].fasta_result(len(plan))
+    assert n == len(exp)
+    for c in ctxs:
+        c.close()

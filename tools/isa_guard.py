@@ -1,9 +1,11 @@
 """ISA guard for the hand-waited input loads of scan_kernel (dataplug_amd/csrc/dpscan.hip).
 
-The data waves issue their buffer loads as inline asm and wait with one explicit `s_waitcnt vmcnt(9)`.
-The compiler knows nothing about that contract, so this checks the generated gfx950 assembly: on every
-control-flow path from a `buffer_load_dword*` into register(s) R to the next `s_waitcnt vmcnt`, no
-instruction may read or write R (dataflow over the kernel's basic blocks).  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
+The data waves issue their buffer loads as inline asm and wait with one explicit `s_waitcnt vmcnt(N)` per
+buffer, N = the loads of the buffers still in flight.  The compiler knows nothing about that contract, so
+this checks the generated gfx950 assembly: on every control-flow path from a `buffer_load_dword*` (or a
+returning `buffer_atomic_* … sc0`) into register(s) R until a wait that the load is certain to have completed by (vmcnt(N) with fewer than N
+vector-memory operations issued after it), no instruction may read or write R (dataflow over the
+kernel's basic blocks, tracking the ordered queue of outstanding vector-memory operations).  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
 (without an argument it compiles the kernel with -save-temps into a temp dir).
 """
 from __future__ import annotations
@@ -69,34 +71,65 @@ def _blocks(body: str):
     return out
 
 
-def _scan(ins, pending, problems, k):
-    """Run one block: returns the pending set at its end (registers with an un-waited input load)."""
-    pending = set(pending)
+VMEM_RE = re.compile(r"^(buffer|global|flat|scratch)_(load|store|atomic)")
+VMCNT_RE = re.compile(r"vmcnt\((\d+)\)")
+MAXQ = 64          # the vmcnt counter's range: older operations have completed
+
+
+def _join(a, b):
+    n = max(len(a), len(b))
+    e = frozenset()
+    return tuple((a[i] if i < len(a) else e) | (b[i] if i < len(b) else e) for i in range(n))
+
+
+def _le(a, b):
+    return len(a) <= len(b) and all(x <= b[i] for i, x in enumerate(a))
+
+
+def _scan(ins, q, problems, k):
+    """Run one block over q, the outstanding vector-memory operations youngest first (vmcnt decrements
+    in issue order): each entry is the set of VGPRs an input buffer load will still write (empty for
+    any other load/store, which only takes a counter slot).  `s_waitcnt vmcnt(N)` keeps the N youngest."""
+    q = tuple(q)
     for s in ins:
-        if s.startswith("s_waitcnt") and "vmcnt" in s:
-            pending.clear()
-            continue
         toks = re.split(r"[\s,]+", s)
+        op = toks[0]
+        if op == "s_waitcnt":
+            m = VMCNT_RE.search(s)
+            if m:
+                q = q[:int(m.group(1))]
+            continue
+        pending = frozenset().union(*q) if q else frozenset()
+        if VMEM_RE.match(op):
+            # hand-waited destinations: the input buffer loads and the returning (sc0) ticket atomic
+            if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]):
+                dst = regs(toks[1])
+                srcs = set()
+                for t in toks[2:]:
+                    srcs |= regs(t)
+                if problems is not None and srcs & pending:
+                    problems.append((k, s))
+                q = ((frozenset(dst),) + q)[:MAXQ]
+            else:
+                used = set()
+                for t in toks[1:]:
+                    used |= regs(t)
+                if problems is not None and used & pending:
+                    problems.append((k, s))
+                q = ((frozenset(),) + q)[:MAXQ]
+            continue
         used = set()
         for t in toks[1:]:
             used |= regs(t)
-        if toks[0].startswith("buffer_load_dword"):
-            dst = regs(toks[1])
-            srcs = set()
-            for t in toks[2:]:
-                srcs |= regs(t)
-            if problems is not None and srcs & pending:
-                problems.append((k, s))
-            pending |= dst
-            continue
         if problems is not None and used & pending:
             problems.append((k, s))
-    return pending
+    return q
 
 
 def check(asm_path: str):
     """Dataflow over the control-flow graph: a register written by an input buffer load stays "pending" on
-    every path until an `s_waitcnt vmcnt`; no instruction on any path may read or write it meanwhile."""
+    every path until a `s_waitcnt vmcnt(N)` with fewer than N vector-memory operations issued after the
+    load; no instruction on any path may read or write it meanwhile."""
     text = open(asm_path).read()
     problems = []
     kernels = KERNEL_RE.findall(text)
@@ -106,7 +139,7 @@ def check(asm_path: str):
         body = body[:body.index(".Lfunc_end")]
         blocks = _blocks(body)
         index = {lab: i for i, (lab, _, _) in enumerate(blocks)}
-        pin = [set() for _ in blocks]
+        pin = [() for _ in blocks]
         work = list(range(len(blocks)))
         while work:
             i = work.pop()
@@ -114,8 +147,8 @@ def check(asm_path: str):
             pout = _scan(ins, pin[i], None, k)
             for t in succ:
                 j = index.get(t)
-                if j is not None and not pout <= pin[j]:
-                    pin[j] |= pout
+                if j is not None and not _le(pout, pin[j]):
+                    pin[j] = _join(pin[j], pout)
                     work.append(j)
         for i, (lab, ins, succ) in enumerate(blocks):
             _scan(ins, pin[i], problems, k)
