@@ -39,7 +39,8 @@ def main():
     ap.add_argument("--size", type=int, default=4 << 30)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-stream", action="store_true", help="skip the stream-read calibration")
-    ap.add_argument("--only", choices=["fasta", "delim", "nogt"], help="run one workload (for rocprofv3 --pmc)")
+    ap.add_argument("--only", choices=["fasta", "delim", "nogt", "csv", "vcf"],
+                    help="run one workload (for rocprofv3 --pmc)")
     args = ap.parse_args()
     size = args.size
     ctx = ScanContext(0)
@@ -80,6 +81,25 @@ def main():
         ctx.h2d(d.ptr, plain)
         k, w = timed(ctx, fasta, args.reps)
         res["fasta_no_gt_kernel_GBps"] = round(size / k / 1e9, 1)
+    # BASELINE configs[2] / [3] shapes (cities.csv rows, sample.vcf rows): the newline index (uint64) of
+    # [0, size); algorithmic bytes = N + 8 * L
+    for name, gen in (("csv", synth.csv), ("vcf", synth.vcf)):
+        if args.only not in (None, name):
+            continue
+        data = synth.tiled_host(gen(64 * (1 << 20) - 333, 9), size)
+        nl = int(np.count_nonzero(data == 10))
+        ctx.h2d(d.ptr, data)
+        del data
+        out_nl = ctx.workspace("out_nl", 8 * nl + 1024)
+
+        def newline(cap=nl + 64):
+            ctx.delim_index_async(d.ptr, size, 0, 0, size, 10, 1, 0, out_nl.ptr, True, cap)
+            ctx.delim_result()
+
+        k, w = timed(ctx, newline, args.reps)
+        res[f"{name}_newline_kernel_GBps"] = round(size / k / 1e9, 1)
+        res[f"{name}_newline_alg_GBps"] = round((size + 8.0 * nl) / k / 1e9, 1)
+        res[f"{name}_newlines"] = nl
     g, ub = ctx.geometry()
     res["grid"] = g
     res["unit_bytes"] = ub
