@@ -153,6 +153,9 @@ __device__ __forceinline__ uint32_t match4(uint32_t w, uint32_t key) {
 // v_dot4_i32_i8 with weights 1, 2, 4, 8 subtracts the non-matching weights of one dword from its
 // accumulator; chained Horner-style (acc << 4 between dwords) it leaves -(non-match mask), and
 // 0xFFFF + that is the match mask.  4 dot4 + 3 shifts + 1 add.
+#ifndef DP_INTERIOR
+#define DP_INTERIOR 1
+#endif
 #ifndef DP_PACK_IND
 #define DP_PACK_IND 1
 #endif
@@ -659,12 +662,14 @@ struct FState {                    // wave-uniform FASTA scan state over one wav
 // are skipped after one exact test.
 // One row r (row0 = r KiB into the range): xr = the lane's 16 bytes, wn = a word whose lane-0 byte 0 is the
 // byte after the row (only read when that byte is inside the chunk).
-template <class Store>
+// INTERIOR: the whole range and the byte after it lie inside the chunk (no edge rows; every row's next
+// byte is valid): the same code without the per-row edge tests.
+template <bool INTERIOR, class Store>
 __device__ __forceinline__ void fasta_row(const v4u& xr, uint32_t wn, int r, int lo, int hi, int lane, FState& st,
                                           Store&& store) {
   {
     const int row0 = r * kRowBytes;
-    const bool edge = row0 < lo || row0 + kRowBytes >= hi;
+    const bool edge = !INTERIOR && (row0 < lo || row0 + kRowBytes >= hi);
     const uint32_t g0 = match4(xr[0], kKeyGT), g1 = match4(xr[1], kKeyGT);
     const uint32_t g2 = match4(xr[2], kKeyGT), g3 = match4(xr[3], kKeyGT);
     const bool anygt = __ballot((g0 & g1 & g2 & g3) != 0xFFFFFFFFu) != 0ull;
@@ -672,7 +677,7 @@ __device__ __forceinline__ void fasta_row(const v4u& xr, uint32_t wn, int r, int
     uint32_t NL = pack16(match4(xr[0], kKeyNL), match4(xr[1], kKeyNL), match4(xr[2], kKeyNL), match4(xr[3], kKeyNL));
     uint32_t GT = anygt ? pack16(g0, g1, g2, g3) : 0u;
     uint32_t nxt63 = 0, lastm = 0;
-    if (row0 + kRowBytes < hi) nxt63 = ((uint32_t)__builtin_amdgcn_readlane((int)wn, 0) & 0xFFu) == 10u;
+    if (INTERIOR || row0 + kRowBytes < hi) nxt63 = ((uint32_t)__builtin_amdgcn_readlane((int)wn, 0) & 0xFFu) == 10u;
     if (edge) {
       const int rel_lo = lo - row0 - 16 * lane;
       const int rel_hi = hi - row0 - 16 * lane;
@@ -714,7 +719,7 @@ __device__ __forceinline__ void fasta_row(const v4u& xr, uint32_t wn, int r, int
   }
 }
 // one buffer: rows half*8 .. half*8 + 7 of the wave range
-template <class Store>
+template <bool INTERIOR, class Store>
 __device__ __forceinline__ void fasta_rows(const v4u (&x)[kRows], uint32_t la, int half, int lo, int hi, int lane,
                                            FState& st, Store&& store) {
 #ifdef DP_NOROWS
@@ -723,17 +728,17 @@ __device__ __forceinline__ void fasta_rows(const v4u (&x)[kRows], uint32_t la, i
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const int R = half * kRows + r;
-    if (R * kRowBytes >= hi) break;
-    fasta_row(x[r], (r + 1 < kRows) ? x[(r + 1) & (kRows - 1)][0] : la, R, lo, hi, lane, st, store);
+    if (!INTERIOR && R * kRowBytes >= hi) break;
+    fasta_row<INTERIOR>(x[r], (r + 1 < kRows) ? x[(r + 1) & (kRows - 1)][0] : la, R, lo, hi, lane, st, store);
   }
 }
 
 // Delimiter rows of one wave range: events = delimiter bytes.  nev counts them.
-template <class Store>
+template <bool INTERIOR, class Store>
 __device__ __forceinline__ void delim_row(const v4u& xr, int r, int lo, int hi, uint32_t key, int lane, uint32_t& nev,
                                           Store&& store) {
   const int row0 = r * kRowBytes;
-  const bool edge = row0 < lo || row0 + kRowBytes >= hi;
+  const bool edge = !INTERIOR && (row0 < lo || row0 + kRowBytes >= hi);
   const uint32_t p0 = match4(xr[0], key), p1 = match4(xr[1], key);
   const uint32_t p2 = match4(xr[2], key), p3 = match4(xr[3], key);
   if (!edge && __ballot((p0 & p1 & p2 & p3) != 0xFFFFFFFFu) == 0ull) return;
@@ -744,7 +749,7 @@ __device__ __forceinline__ void delim_row(const v4u& xr, int r, int lo, int hi, 
     nev += emit_row(M, nev, [&](uint32_t rk, uint32_t b) { store(rk, pos0 + b); });
   }
 }
-template <class Store>
+template <bool INTERIOR, class Store>
 __device__ __forceinline__ void delim_rows(const v4u (&x)[kRows], int half, int lo, int hi, uint32_t key, int lane,
                                            uint32_t& nev, Store&& store) {
 #ifdef DP_NOROWS
@@ -753,8 +758,8 @@ __device__ __forceinline__ void delim_rows(const v4u (&x)[kRows], int half, int 
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const int R = half * kRows + r;
-    if (R * kRowBytes >= hi) break;
-    delim_row(x[r], R, lo, hi, key, lane, nev, store);
+    if (!INTERIOR && R * kRowBytes >= hi) break;
+    delim_row<INTERIOR>(x[r], R, lo, hi, key, lane, nev, store);
   }
 }
 
@@ -766,7 +771,7 @@ struct PhaseA {
   uint64_t wbase;
   int lo, hi;
 };
-template <int MODE>
+template <int MODE, int OUT64>
 __device__ __forceinline__ void phase_a_half(const ScanArgs& A, PhaseA& pa, Buf& b, int half, int wave, int lane,
                                              Shared& sh, uint32_t ev_head PROF_ARG) {
   v4u x[kRows];
@@ -782,10 +787,15 @@ __device__ __forceinline__ void phase_a_half(const ScanArgs& A, PhaseA& pa, Buf&
     if (rk < kDenseMax) evw[(ev_head + rk) & kEvMask] = (uint16_t)pos;
 #endif
   };
+  const bool interior = DP_INTERIOR && pa.lo == 0 && pa.hi > kWaveBytes;   // wave-uniform
+  (void)interior;
   if constexpr (MODE == kFasta) {
-    fasta_rows(x, b.la, half, pa.lo, pa.hi, lane, pa.st, keep);
+    if (interior) fasta_rows<true>(x, b.la, half, pa.lo, pa.hi, lane, pa.st, keep);
+    else fasta_rows<false>(x, b.la, half, pa.lo, pa.hi, lane, pa.st, keep);
   } else {
-    delim_rows(x, half, pa.lo, pa.hi, A.delim ^ kSel12, lane, pa.st.nev, keep);
+    // DELIM: no specialized copy (measured ±1% with uint64 output; with uint32 output the copy pushes
+    // the kernel past 128 VGPRs and spills an in-flight load destination, which tools/isa_guard.py flags)
+    delim_rows<false>(x, half, pa.lo, pa.hi, A.delim ^ kSel12, lane, pa.st.nev, keep);
   }
   PROF_MARK(1);
 }
@@ -844,7 +854,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
     for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) {
       const int an = (r + 1) * kRowBytes;
       const uint32_t wn = an + 4 <= hi16 ? *reinterpret_cast<const uint32_t*>(src + an) : 0u;
-      fasta_row(row_in(r), wn, r, lo, hi, lane, st, out);
+      fasta_row<false>(row_in(r), wn, r, lo, hi, lane, st, out);
     }
   } else {
     const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
@@ -865,7 +875,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
     };
     const uint32_t key = A.delim ^ kSel12;
 #pragma unroll 1
-    for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) delim_row(row_in(r), r, lo, hi, key, lane, n, out);
+    for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) delim_row<false>(row_in(r), r, lo, hi, key, lane, n, out);
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
@@ -1173,7 +1183,7 @@ struct DataWave {
         wait_buf(b[h]);                               // this buffer landed; the others stay in flight
         PROF_MARK(0);
       }
-      phase_a_half<MODE>(A, pa, b[h], h, wave, lane, sh, ev_head PROF_PASS);
+      phase_a_half<MODE, OUT64>(A, pa, b[h], h, wave, lane, sh, ev_head PROF_PASS);
       if (h + 1 < kBufs) load_buf(b[h], A, gn, wave, lane, h);
     }
     WaveRec rec;
@@ -1201,7 +1211,7 @@ struct DataWave {
     return un < (uint32_t)A.nunits;
   }
 
-  __device__ void run() {
+  __device__ __forceinline__ void run() {
     PROF_DECL;
     Cursor cur{0, 0, 0, 0, 0, 0};
     Geo g = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0, cur);
