@@ -98,6 +98,13 @@ def main():
                                    ctx.delim_result()))
     run("delim_rare", lambda: (ctx.delim_index_async(d.ptr, size, 0, 0, size, ord("#"), 1, 0, out.ptr, False, size // 16),
                                ctx.delim_result()))
+    csv = synth.tiled_host(synth.csv(64 * (1 << 20) - 333, 9), size)
+    nl = int(np.count_nonzero(csv == 10))
+    ctx.h2d(d.ptr, csv)
+    del csv
+    out_nl = ctx.workspace("out_nl", 8 * nl + 1024)
+    run("csv_newline_u64", lambda: (ctx.delim_index_async(d.ptr, size, 0, 0, size, 10, 1, 0, out_nl.ptr, True, nl + 64),
+                                    ctx.delim_result()))
     line = np.frombuffer(b"ACGT" * 15 + b"\n", np.uint8)
     ctx.h2d(d.ptr, np.resize(line, size))
     run("fasta_no_gt", lambda: (ctx.fasta_index_async(d.ptr, size, 0, size, chunks, out.ptr, False, size // 256),
