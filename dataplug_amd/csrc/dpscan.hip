@@ -58,7 +58,7 @@ constexpr int kWaveBytes = kRowBytes * kRangeRows;   // 16 KiB wave range per un
 constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 240 KiB look-back unit
 static_assert(kRows * kBufs == kRangeRows && kRows >= 2 && kRows <= 8, "buffers of 2, 4 or 8 rows");
 #ifndef DP_RING
-#define DP_RING 32
+#define DP_RING 16
 #endif
 #ifndef DP_EVCAP
 #define DP_EVCAP 4096
