@@ -42,15 +42,23 @@
 namespace {
 
 constexpr int kWave = 64;
-constexpr int kDataWaves = 15;                     // + 1 coordinator wave
+#ifndef DP_DWAVES
+#define DP_DWAVES 15
+#endif
+constexpr int kDataWaves = DP_DWAVES;              // + 1 coordinator wave
+static_assert(kDataWaves >= 2 && kDataWaves <= 15, "data waves: one DPP row of summaries");
 constexpr int kCoord = kDataWaves;
 constexpr int kWaves = kDataWaves + 1;
-constexpr int kThreads = kWave * kWaves;           // 1024
+constexpr int kThreads = kWave * kWaves;           // 1024 (default)
 constexpr int kRowBytes = kWave * 16;              // one dwordx4 per lane
 #ifndef DP_NBUF
 #define DP_NBUF 2
 #endif
-constexpr int kRangeRows = 16;                     // rows per wave range
+#ifndef DP_RROWS
+#define DP_RROWS 16
+#endif
+constexpr int kRangeRows = DP_RROWS;               // rows per wave range
+static_assert(kRangeRows * 1024 + 64 < 65536, "event positions are 16-bit offsets into a range");
 constexpr int kBufs = DP_NBUF;                     // input buffers per wave range: one scanned, the rest in flight
 constexpr int kRows = kRangeRows / kBufs;          // rows per buffer (one load batch)
 constexpr int kBufBytes = kRowBytes * kRows;
@@ -89,6 +97,12 @@ constexpr uint32_t kErrOverflow = 2u;
 constexpr uint64_t kStatAgg = 1ull << 62;
 constexpr uint64_t kStatPrefix = 2ull << 62;
 constexpr uint64_t kStatMask = 3ull << 62;
+// Launch epoch in bits 50..61 of every stored descriptor (AGG uses bits 0..49, PREFIX 0..48): a descriptor
+// left by an earlier launch carries another epoch and reads as "not published".  The host zeroes the
+// array only when it is (re)allocated and once every kEpochMax launches.
+constexpr int kEpochShift = 50;
+constexpr uint64_t kEpochMask = 0xFFFull << kEpochShift;
+constexpr uint32_t kEpochMax = 0xFFFu;
 constexpr uint32_t kSpinLimit = 1u << 22;          // polls (with s_sleep) before giving up
 
 enum Mode { kFasta = 0, kDelim = 1 };
@@ -131,7 +145,8 @@ struct ScanArgs {
   uint64_t obj_base;           // object offset of buffer byte 0
   uint64_t nchunks;
   uint64_t nunits;
-  unsigned long long* desc;    // [nunits] look-back descriptors (zeroed per launch)
+  unsigned long long* desc;    // [nunits] look-back descriptors, tagged with the launch epoch (no per-launch reset)
+  uint64_t epoch;              // this launch's tag, already at kEpochShift
   void* out;
   uint64_t cap;                // entries (FASTA: pairs)
   int out_u64;
@@ -376,7 +391,12 @@ __device__ __forceinline__ void lb_load(const ScanArgs& A, uint32_t u, uint32_t 
 #pragma unroll
   for (int j = 0; j < kLbPer; ++j) {
     const uint32_t k = kLbPer * rl + j;
-    d[j] = k < W ? ld_desc(&A.desc[u - 1 - k]) : kIdentDesc;
+    if (k < W) {
+      const uint64_t v = ld_desc(&A.desc[u - 1 - k]);
+      d[j] = (v & kEpochMask) == A.epoch ? v : 0ull;   // an earlier launch's descriptor: not published yet
+    } else {
+      d[j] = kIdentDesc;
+    }
   }
 }
 
@@ -1027,7 +1047,7 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
       const Func f = compose_unit(sh, s, lane);
       const uint32_t up = unit_of(pub);
       if (lane == 0) {
-        if (up > 0) st_desc(&A.desc[up], pack_agg(f));
+        if (up > 0) st_desc(&A.desc[up], pack_agg(f) | A.epoch);
         TL_STAMP(pub, 0);
         sh.done[s] = 0;                               // slot's counter free for unit pub + kRing
       }
@@ -1089,7 +1109,7 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
           sh.S[s][lane] = st0 ? (es >> 1) & 1u : es & 1u;
         }
         if (lane == 0) {
-          st_desc(&A.desc[u], pack_prefix(P_incl, S_out));
+          st_desc(&A.desc[u], pack_prefix(P_incl, S_out) | A.epoch);
           if (u + 1 == A.nunits) A.total[0] = P_incl;
           if (g.fl & kGeoLast) {
             A.chunk_end[g.c] = P_incl;
@@ -1393,6 +1413,7 @@ struct dp_ctx {
   // device workspace
   unsigned long long* d_desc = nullptr;
   uint64_t desc_cap = 0;
+  uint32_t desc_epoch = 0;            // last launch's descriptor epoch (0: the array needs zeroing first)
   uint64_t* d_tab = nullptr;          // chunk_lo | chunk_hi | chunk_u0 | pending | ctrl
   uint64_t tab_cap = 0;               // in u64 words
   uint64_t* h_tab = nullptr;          // pinned mirror
@@ -1422,7 +1443,7 @@ int ensure_tab(dp_ctx* c, uint64_t words) {
     uint64_t cap = words + words / 2 + 64;
     HIPCHK(hipMalloc(&c->d_tab, cap * 8));
     c->tab_cap = cap;
-    c->last_tab.clear();
+    c->last_tab.clear();   // forces a full upload (table + control words) before the next scan
   }
   if (words > c->h_cap) {
     if (c->h_tab) HIPCHK(hipHostFree(c->h_tab));
@@ -1438,6 +1459,7 @@ int ensure_desc(dp_ctx* c, uint64_t n) {
     uint64_t cap = ((n + n / 4 + 1023) / 1024) * 1024;
     HIPCHK(hipMalloc(&c->d_desc, cap * 8));
     c->desc_cap = cap;
+    c->desc_epoch = 0;
   }
   return DP_OK;
 }
@@ -1472,8 +1494,11 @@ int harvest_events(dp_ctx* c) {
   return DP_OK;
 }
 
-// Lay out the chunk table in aligned coordinates and enqueue its upload + the control-block reset.
+// Lay out the chunk table in aligned coordinates and enqueue its upload when it changed.
 // Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[4] (err | total | spare x2).
+// No per-launch reset: every launch rewrites pending / chunk_end of each non-empty chunk and total (when it
+// has units), so only the upload sets their defaults (-1, ~0, 0) and err = 0.  A launch that sets an err
+// bit drops last_tab, so the next one re-uploads (results of a failed launch are discarded anyway).
 int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, const uint64_t* chunks,
                  uint64_t n, uint64_t* nunits_out) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
@@ -1500,11 +1525,11 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     // the pinned mirror may still feed an earlier async copy: wait for the stream before rewriting it
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(c->h_tab, tab.data(), tab.size() * 8);
-    HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, tab.size() * 8, hipMemcpyHostToDevice, c->stream));
+    memset(c->h_tab + c->pend_off, 0xFF, 2 * n * 8);
+    memset(c->h_tab + c->ctrl_off, 0, 4 * 8);
+    HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, words * 8, hipMemcpyHostToDevice, c->stream));
     c->last_tab.swap(tab);
   }
-  HIPCHK(hipMemsetAsync(c->d_tab + c->pend_off, 0xFF, 2 * n * 8, c->stream));
-  HIPCHK(hipMemsetAsync(c->d_tab + c->ctrl_off, 0, 4 * 8, c->stream));
   *nunits_out = units;
   return DP_OK;
 }
@@ -1519,6 +1544,7 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.nchunks = n;
   a.nunits = units;
   a.desc = c->d_desc;
+  a.epoch = 0;
   if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
     d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
     cap = 1;
@@ -1537,7 +1563,11 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   int rc = ensure_desc(c, units);
   if (rc) return rc;
   a.desc = c->d_desc;
-  HIPCHK(hipMemsetAsync(c->d_desc, 0, ((units * 8 + 15) / 16) * 16, c->stream));
+  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {   // fresh array, or the epochs wrapped
+    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
+    c->desc_epoch = 0;
+  }
+  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
   const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
   hipEvent_t e0;
   rc = ev_begin(c, &e0);
@@ -1767,6 +1797,7 @@ int dp_fasta_result(dp_ctx* c, uint64_t* n_pairs, int64_t* pending, uint64_t* ch
   rc = collect_ctrl(c, 0);
   if (rc) return rc;
   const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
+  if (err) c->last_tab.clear();                         // the next launch re-uploads err = 0
   const uint64_t total = c->nchunks ? c->h_tab[c->ctrl_off + 1] : 0;
   if (n_pairs) *n_pairs = total;
   if (pending) memcpy(pending, c->h_tab + c->pend_off, c->nchunks * 8);
@@ -1828,6 +1859,7 @@ int dp_delim_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims) {
   rc = collect_ctrl(c, 0);
   if (rc) return rc;
   const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
+  if (err) c->last_tab.clear();                         // the next launch re-uploads err = 0
   const uint64_t nd = c->h_tab[c->ctrl_off + 1];
   const uint64_t nout = k ? nd / k : 0;
   if (n_delims) *n_delims = nd;
@@ -1878,6 +1910,7 @@ int dp_stream_read(dp_ctx* c, const void* d_buf, uint64_t bytes, int blocks_per_
   rc = ensure_tab(c, 8);
   if (rc) return rc;
   const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  c->last_tab.clear();   // the table area is the (practically never written) sink
   hipEvent_t e0;
   rc = ev_begin(c, &e0);
   if (rc) return rc;

@@ -183,3 +183,71 @@ def test_two_contexts_ordered_by_ctx_wait():
     assert n == len(exp)
     for c in ctxs:
         c.close()
+
+
+def _check_plan(ctx, d, a, plan, u64=False):
+    pairs, pending, cend = ctx.fasta_index(d.ptr, len(a), 0, len(a), plan, u64=u64)
+    exp = dpref.fasta_pairs(a, plan)
+    assert (pending == -1).all()
+    np.testing.assert_array_equal(pairs.astype(np.uint64), exp)
+    k = 0
+    for i, (c0, c1) in enumerate(plan):
+        k += len(dpref.fasta_pairs(a, [(c0, c1)]))
+        assert int(cend[i]) == k, (i, plan)
+
+
+def test_state_carried_between_launches():
+    # no per-launch reset of the look-back descriptors or control words: changing plans (with empty
+    # chunks, an all-empty plan), a delimiter scan, an overflow error and repeated plans on one context
+    from dataplug_amd.scan import ScanContext
+    ctx = ScanContext(0)
+    try:
+        a = synth.fasta((6 << 20) + 4321, 21)
+        d = ctx.workspace("in", len(a) + 64)
+        ctx.h2d(d.ptr, a)
+        n = len(a)
+        p1 = cpu_ref.chunk_plan(n, math.ceil(n / 5))
+        p2 = [(0, 1 << 20), (1 << 20, 1 << 20), ((1 << 20), 3 << 20), (3 << 20, 3 << 20), (3 << 20, n)]
+        p3 = [(100, 100), (2000, 2000)]
+        for plan in (p1, p2, p1, p3, p2, p2, p1):
+            _check_plan(ctx, d, a, plan)
+        got, nd = ctx.delim_index(d.ptr, n, 0, 0, n, 10, 1, 0, u64=True)
+        exp, end_nd = dpref.delim(a, 0, n, 10, 1, 0)
+        assert nd == end_nd and np.array_equal(got, exp)
+        _check_plan(ctx, d, a, p2)
+        base = (1 << 32) - (1 << 21)                      # an overflowing launch (err bit set), then clean ones
+        with pytest.raises(OverflowError):
+            ctx.fasta_index(d.ptr, n, base, base + n, [(base, base + n)], u64=False)
+        _check_plan(ctx, d, a, p2)
+        _check_plan(ctx, d, a, p1, u64=True)
+    finally:
+        ctx.close()
+
+
+def test_descriptor_epochs_wrap():
+    # more launches than descriptor epochs (4095) on one context, alternating two objects of one size and
+    # plan (same units, different descriptors): a stale descriptor read as current would change the counts
+    from dataplug_amd.scan import ScanContext
+    ctx = ScanContext(0)
+    try:
+        objs = [synth.fasta((1 << 20) + 17, s) for s in (31, 32)]
+        objs.append(_adversarial("dense", (1 << 20) + 17, 33))
+        plan = cpu_ref.chunk_plan(len(objs[0]), math.ceil(len(objs[0]) / 3))
+        exps = [dpref.fasta_pairs(o, plan) for o in objs]
+        assert len({len(e) for e in exps}) == 3
+        bufs = [ctx.workspace(f"in{i}", len(o) + 64) for i, o in enumerate(objs)]
+        for b, o in zip(bufs, objs):
+            ctx.h2d(b.ptr, o)
+        chunks = np.ascontiguousarray(np.asarray(plan, np.uint64).reshape(-1))
+        cap = max(len(e) for e in exps) + 16
+        out = ctx.workspace("out", 8 * cap)
+        for i in range(4200):
+            j = i % 3
+            ctx.fasta_index_async(bufs[j].ptr, len(objs[j]), 0, len(objs[j]), chunks, out.ptr, False, cap)
+            cnt, pending, _ = ctx.fasta_result(len(plan))
+            assert cnt == len(exps[j]) and (pending == -1).all(), i
+            if i % 700 == 0 or 4090 <= i <= 4100:
+                got = ctx.d2h(np.empty((cnt, 2), np.uint32), out.ptr)
+                np.testing.assert_array_equal(got.astype(np.uint64), exps[j])
+    finally:
+        ctx.close()

@@ -6,7 +6,7 @@ this checks the generated gfx950 assembly: on every control-flow path from a `bu
 returning `buffer_atomic_* … sc0`) into register(s) R until a wait that the load is certain to have completed by (vmcnt(N) with fewer than N
 vector-memory operations issued after it), no instruction may read or write R (dataflow over the
 kernel's basic blocks, tracking the ordered queue of outstanding vector-memory operations).  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
-(without an argument it compiles the kernel with -save-temps into a temp dir).
+(without an argument it compiles the kernel with -save-temps into a temp dir; DP_DEFINES=A=1,B adds -D's).
 """
 from __future__ import annotations
 
@@ -24,7 +24,8 @@ KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_111scan_kernelILi[01]ELi[01]EE\w*):",
 def compile_asm() -> str:
     d = tempfile.mkdtemp(prefix="dpscan_isa_")
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                    "-Wno-unused-function", "-save-temps", "-o", os.path.join(d, "x.so"), SRC], cwd=d, check=True,
+                    "-Wno-unused-function", "-save-temps", "-o", os.path.join(d, "x.so"), SRC]
+                   + ["-D" + x for x in os.environ.get("DP_DEFINES", "").split(",") if x], cwd=d, check=True,
                    stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
     return os.path.join(d, "dpscan-hip-amdgcn-amd-amdhsa-gfx950.s")
 
