@@ -2,6 +2,7 @@
 """Benchmark: device-resident FASTA header-index scan (BASELINE.json configs[1]) on 1..N MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--no-cpu-baseline]
+    python bench.py --workload csv|vcf ...    (BASELINE configs[2] / configs[3]: newline index)
 
 One step = one whole co.preprocess(chunk_size=size/4) equivalent over one synthetic 4 GiB FASTA object
 that is already resident in HBM: chunk-plan upload, the single-pass scan kernel, the split-header
@@ -46,15 +47,19 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--size", type=int, default=4 << 30)
+    p.add_argument("--workload", choices=["fasta", "csv", "vcf"], default="fasta",
+                   help="fasta: configs[1] (default, the headline line); csv: configs[2], a 32 GiB CSV per GPU; "
+                        "vcf: configs[3], one 64 GiB VCF whose body is cut into one part per GPU")
+    p.add_argument("--size", type=int, default=None,
+                   help="object bytes (default 4 GiB fasta, 32 GiB csv, 64 GiB vcf)")
     p.add_argument("--chunks", type=int, default=4, help="chunk_size = ceil(size / chunks) (fasta_example.py)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--traffic-bytes", type=float, default=None,
                    help="HBM bytes per scan launch from a rocprofv3 --pmc pass (overrides --traffic-from)")
-    p.add_argument("--traffic-from", default=os.path.join(REPO, "profiles", "latest_pmc_summary.json"),
+    p.add_argument("--traffic-from", default=None,
                    help="pmc_summary.json (tools/pmc_summary.py) of this same command: FETCH_SIZE x2 (gfx950) "
-                        "+ WRITE_SIZE per scan_kernel<FASTA> launch")
+                        "+ WRITE_SIZE per scan-kernel launch (default profiles/latest_pmc_summary[_<workload>].json)")
     return p.parse_args()
 
 
@@ -132,9 +137,210 @@ def cpu_baseline(host: np.ndarray, chunk_size: int):
             "value_1core": round(len(one) / t_one / GiB, 3)}
 
 
+def load_traffic(args, size):
+    """(HBM bytes per scan launch, source) from --traffic-bytes or a committed rocprofv3 PMC summary of the
+    same workload (tools/pmc_summary.py), else (None, None)."""
+    if args.traffic_bytes:
+        return args.traffic_bytes, "--traffic-bytes"
+    suffix = "" if args.workload == "fasta" else "_" + args.workload
+    path = args.traffic_from or os.path.join(REPO, "profiles", f"latest_pmc_summary{suffix}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pmc = json.load(f)
+    kernel = "scan_kernel<0" if args.workload == "fasta" else "scan_kernel<1"
+    if pmc.get("object_bytes", size) != size or "hbm_traffic_bytes" not in pmc \
+            or not pmc.get("kernel", kernel).startswith(kernel):
+        return None, None
+    return pmc["hbm_traffic_bytes"], os.path.relpath(os.path.realpath(path), REPO)
+
+
+def _delim_chunk(args):
+    """cpu_baseline worker for csv/vcf: the newline offsets of one chunk (oracle/cpu_ref.delim_index)."""
+    from oracle import cpu_ref
+    c0, c1 = args
+    return len(cpu_ref.delim_index(_CPU_OBJ, c0, c1))
+
+
+def cpu_baseline_delim(host: np.ndarray):
+    """The CPU newline index (numpy restatement of the '\\n' search CSVSlice.get / VCFSlice.get do per slice,
+    csv.py:60-98, vcf.py:98-140) on the host cores, bounded sample."""
+    import multiprocessing as mp
+    global _CPU_OBJ
+    _CPU_OBJ = host[: min(len(host), 1 << 30)]
+    cs = max(1, len(_CPU_OBJ) // 64)
+    plan = [(i * cs, (i + 1) * cs) for i in range(len(_CPU_OBJ) // cs)]
+    cores = min(16, os.cpu_count() or 1)
+    t0 = time.perf_counter()
+    with mp.get_context("fork").Pool(cores) as pool:
+        pool.map(_delim_chunk, plan, chunksize=1)
+    t_pool = time.perf_counter() - t0
+    from oracle import cpu_ref
+    one = _CPU_OBJ[: 256 << 20]
+    t0 = time.perf_counter()
+    cpu_ref.delim_index(one)
+    t_one = time.perf_counter() - t0
+    scanned = len(plan) * cs
+    return {"value": round(scanned / t_pool / GiB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
+            "sample": f"first {scanned / GiB:.2f} GiB of the scanned range, {len(plan)} chunks of {cs} B, "
+                      f"numpy flatnonzero(== '\\n') per chunk over a fork pool",
+            "value_1core": round(len(one) / t_one / GiB, 3)}
+
+
+def main_delim(args, world, rank, local, dist):
+    """BASELINE configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3]
+    (vcf: ONE 64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong
+    scaling): the uint64 newline index (dp_delim_index), device-resident, timed like the FASTA line."""
+    from dataplug_amd import synth
+    from dataplug_amd.scan import ScanContext
+
+    def log(msg):
+        print(f"[bench r{rank}] {msg}", file=sys.stderr, flush=True)
+
+    csv_mode = args.workload == "csv"
+    size = args.size or ((32 << 30) if csv_mode else (64 << 30))
+    t0 = time.perf_counter()
+    obj = synth.tiled_csv(size, seed=9 + rank) if csv_mode else synth.tiled_vcf(size, seed=9)
+    if csv_mode:
+        begin, end = 0, size
+    else:
+        bo = len(obj.head)                                   # body_offset (vcf.py:19-67)
+        cs = math.ceil((size - bo) / world)
+        begin, end = min(size, bo + rank * cs), min(size, bo + (rank + 1) * cs)
+    nbytes = end - begin
+    n_exp = obj.count_range(begin, end)
+    ctx = ScanContext(local)
+    ctx2 = ScanContext(local)
+    d_in = ctx.workspace("bench_in", nbytes + 64)
+    step = 4 << 30                                           # materialize + upload 4 GiB at a time
+    stage = np.empty(min(step, nbytes), np.uint8)
+    for p in range(begin, end, step):
+        q = min(end, p + step)
+        ctx.h2d(d_in.ptr + (p - begin), obj.bytes_range(p, q, out=stage))
+        log(f"uploaded {q - begin} / {nbytes} B")
+    del stage
+    gen_s = time.perf_counter() - t0
+    cap = n_exp + 1024
+    ctxs = (ctx, ctx2)
+    d_outs = (ctx.workspace("bench_out", 8 * cap), ctx2.workspace("bench_out", 8 * cap))
+
+    def launch(i):
+        ctxs[i % 2].delim_index_async(d_in.ptr, nbytes, begin, begin, end, 10, 1, 0, d_outs[i % 2].ptr, True, cap)
+
+    def collect(i):
+        return ctxs[i % 2].delim_result()
+
+    for i in range(max(2, args.warmup)):
+        launch(i)
+        collect(i)
+
+    def run_steps(serialize: bool):
+        barrier(dist, local)
+        ctx.sync()
+        ctx2.sync()
+        t0 = time.perf_counter()
+        launch(0)
+        for i in range(1, args.steps):
+            if serialize:
+                ctxs[i % 2].wait_for(ctxs[(i - 1) % 2])
+            launch(i)
+            collect(i - 1)
+        res = collect(args.steps - 1)
+        ctx.sync()
+        ctx2.sync()
+        barrier(dist, local)
+        return time.perf_counter() - t0, res
+
+    for c in ctxs:
+        c.timing(True)
+        c.timing_read()
+    dt_ser, _ = run_steps(serialize=True)
+    kern_ms, launches = 0.0, 0
+    for c in ctxs:
+        ms, n = c.timing_read()
+        c.timing(False)
+        kern_ms += ms
+        launches += n
+    dt, (n_out, _) = run_steps(serialize=False)
+    d_out = d_outs[(args.steps - 1) % 2]
+    log(f"timed {args.steps} steps: {dt:.3f} s, {n_out} offsets")
+
+    dt_max = max_over_ranks(dist, local, dt)
+    dt_ser_max = max_over_ranks(dist, local, dt_ser)
+    total_bytes = sum_over_ranks(dist, local, float(nbytes) * args.steps)
+    total_offsets = sum_over_ranks(dist, local, float(n_out) * args.steps)
+    kern_avg_max = max_over_ranks(dist, local, kern_ms / 1e3 / max(1, launches))
+
+    verified = None
+    if not args.no_verify:
+        # every offset, against the object's analytic newline positions (synth.TiledText)
+        got = ctx.d2h(np.empty(n_out, np.uint64), d_out.ptr)
+        ok, i = n_out == n_exp, 0
+        for piece in obj.delims_range(begin, end):
+            if not ok:
+                break
+            ok = np.array_equal(got[i:i + len(piece)], piece)
+            i += len(piece)
+        verified = bool(ok and i == n_out)
+        del got
+        verified = bool(sum_over_ranks(dist, local, float(verified)) == world)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline_delim(obj.bytes_range(begin, min(end, begin + (1 << 30))))
+
+    traffic, traffic_src = load_traffic(args, nbytes)
+    if rank == 0:
+        alg_bytes = nbytes + 8.0 * n_out                # N input bytes read once + one uint64 per newline
+        achieved = alg_bytes / kern_avg_max
+        name = "CSV" if csv_mode else "VCF"
+        cfg = ("'\\n' index (uint64), 32 GiB cities.csv-shaped object per GPU (BASELINE configs[2])" if csv_mode else
+               f"'\\n' index (uint64) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
+               f"(BASELINE configs[3])")
+        if args.size and csv_mode:
+            cfg = cfg.replace("32 GiB", f"{size / GiB:g} GiB")
+        out = {
+            "metric": f"GiB/s scanned (device-resident) + offsets/s, {name} newline index",
+            "value": round(total_bytes / dt_max / GiB, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak" if csv_mode else "strong",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {"workload": cfg, "object_bytes": size, "scanned_bytes_per_gpu": nbytes,
+                       "offsets_per_gpu": int(n_out),
+                       "parallelism": f"independent {'objects' if csv_mode else 'body parts'} x{world}, "
+                                      f"no collective"},
+            "offsets_per_s": round(total_offsets / dt_max, 1),
+            "serialized": {"value": round(total_bytes / dt_ser_max / GiB, 3), "unit": "GiB/s",
+                           "ms_per_step": round(dt_ser_max / args.steps * 1e3, 4),
+                           "note": "same K steps, each scan waiting on the device for the previous one"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+                         "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
+                         "kernel": "scan_kernel<DELIM>", "kernel_avg_us": round(kern_avg_max * 1e6, 2),
+                         "alg_bytes_per_launch": int(alg_bytes)},
+            "cpu_baseline": cpu,
+            "verified_bit_exact": verified,
+            "gen_s": round(gen_s, 2),
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local, dist = init_dist(args)
+    if args.workload != "fasta":
+        return main_delim(args, world, rank, local, dist)
+    if args.size is None:
+        args.size = 4 << 30
     from dataplug_amd import synth
     from dataplug_amd.scan import ScanContext
 
@@ -222,13 +428,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(host, chunk_size)
 
-    traffic, traffic_src = args.traffic_bytes, "--traffic-bytes" if args.traffic_bytes else None
-    if traffic is None and args.traffic_from and os.path.exists(args.traffic_from):
-        with open(args.traffic_from) as f:
-            pmc = json.load(f)
-        if pmc.get("object_bytes", size) == size and "hbm_traffic_bytes" in pmc:
-            traffic = pmc["hbm_traffic_bytes"]
-            traffic_src = os.path.relpath(os.path.realpath(args.traffic_from), REPO)
+    traffic, traffic_src = load_traffic(args, size)
 
     if rank == 0:
         alg_bytes = size + 8.0 * n_pairs            # N input bytes read once + 8 B per (start, end) pair

@@ -186,3 +186,67 @@ def tiled_host(base: np.ndarray, size: int) -> np.ndarray:
     for off, n in tile_plan(len(base), size):
         out[off:off + n] = base[:n]
     return out
+
+
+class TiledText:
+    """A large line-oriented object: ``head`` once, then ``body`` repeated to exactly ``size`` bytes.
+
+    Used for the BASELINE configs[2]/[3] shapes (32 GiB CSV, 64 GiB VCF): a rank materializes only the
+    byte range it scans (:meth:`bytes_range`), and the expected newline offsets of any range follow from
+    the body's own newlines (:meth:`delims_range`), so a multi-GiB index is checked without a second scan.
+    """
+
+    def __init__(self, head: np.ndarray, body: np.ndarray, size: int, delim: int = 10):
+        self.head = np.ascontiguousarray(head, np.uint8)
+        self.body = np.ascontiguousarray(body, np.uint8)
+        self.size = int(size)
+        self.delim = delim
+        self.head_pos = np.flatnonzero(self.head == delim).astype(np.uint64)
+        self.body_pos = np.flatnonzero(self.body == delim).astype(np.uint64)
+
+    def _tiles(self, start: int, end: int):
+        """(object offset, body offset, length) pieces of the body covering [start, end)."""
+        h, bl = len(self.head), len(self.body)
+        p = max(start, h)
+        while p < end:
+            q = (p - h) % bl
+            n = min(bl - q, end - p)
+            yield p, q, n
+            p += n
+
+    def bytes_range(self, start: int, end: int, out: np.ndarray | None = None) -> np.ndarray:
+        out = np.empty(end - start, np.uint8) if out is None else out[: end - start]
+        h = len(self.head)
+        if start < h:
+            out[: min(h, end) - start] = self.head[start:min(h, end)]
+        for p, q, n in self._tiles(start, end):
+            out[p - start:p - start + n] = self.body[q:q + n]
+        return out
+
+    def delims_range(self, start: int, end: int):
+        """Yields sorted uint64 arrays: the delimiter offsets in [start, end), piece by piece."""
+        h = len(self.head)
+        if start < h:
+            hp = self.head_pos
+            yield hp[(hp >= start) & (hp < min(h, end))]
+        bp = self.body_pos
+        for p, q, n in self._tiles(start, end):
+            lo, hi = np.searchsorted(bp, q), np.searchsorted(bp, q + n)
+            yield bp[lo:hi] + np.uint64(p - q)
+
+    def count_range(self, start: int, end: int) -> int:
+        return int(sum(len(x) for x in self.delims_range(start, end)))
+
+
+def tiled_csv(size: int, seed: int = 0, block: int = 64 * 2**20 - 333) -> TiledText:
+    """cities.csv-shaped CSV of ``size`` bytes: one header line, then a seeded row block repeated."""
+    base = csv(block, seed)
+    h = len(CSV_HEADER)
+    return TiledText(base[:h], base[h:], size)
+
+
+def tiled_vcf(size: int, seed: int = 0, block: int = 64 * 2**20 - 333) -> TiledText:
+    """VCF of ``size`` bytes: the header once, then a seeded row block repeated."""
+    base = vcf(block, seed)
+    h = len(VCF_HEADER)
+    return TiledText(base[:h], base[h:], size)
