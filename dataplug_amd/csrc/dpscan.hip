@@ -174,6 +174,10 @@ __device__ __forceinline__ uint32_t match4(uint32_t w, uint32_t key) {
 #ifndef DP_PACK_IND
 #define DP_PACK_IND 1
 #endif
+#ifndef DP_PAIRSTORE   // DELIM phase B: 16-byte stores of offset pairs (uint64 output, every_k = 1)
+#define DP_PAIRSTORE 1
+#endif
+typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
 #ifndef DP_RANKCLAMP
 #define DP_RANKCLAMP 1
 #endif
@@ -944,6 +948,30 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
     const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - P % k);
     const uint64_t q0 = (P + r0) / k;
     const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
+#if DP_PAIRSTORE
+    if constexpr (OUT64 != 0) {
+      // Every delimiter, uint64 output, the whole list in bounds (wave-uniform): two offsets per lane and
+      // one 16-byte store, which halves the store instructions that queue behind the input loads.  An odd
+      // q0 puts its first entry in a single store so that the pairs are 16-byte aligned.
+      if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
+        uint64_t* o = reinterpret_cast<uint64_t*>(A.out) + q0;
+        const uint32_t h = nq ? (uint32_t)(q0 & 1u) : 0u;
+        if (h && lane == 0) o[0] = add + evw[ev0 & kEvMask];
+        const uint32_t m = nq - h;
+        for (uint32_t t = 2u * (uint32_t)lane; t < m; t += 2u * kWave) {
+          const uint32_t i = h + t;
+          const uint64_t v0 = add + evw[(ev0 + i) & kEvMask];
+          if (t + 1u < m) {
+            const uint64_t v1 = add + evw[(ev0 + i + 1u) & kEvMask];
+            *reinterpret_cast<v2u64*>(o + i) = v2u64{v0, v1};
+          } else {
+            o[i] = v0;
+          }
+        }
+        return;
+      }
+    }
+#endif
     for (uint32_t t = (uint32_t)lane; t < nq; t += kWave) {
       const uint64_t q = q0 + t;
       const uint64_t val = add + evw[(ev0 + r0 + t * k) & kEvMask];
