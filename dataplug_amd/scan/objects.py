@@ -63,6 +63,36 @@ def read_range_into(storage, bucket: str, key: str, lo: int, hi: int, out: memor
         list(ex.map(one, starts))
 
 
+def fetch_to_device(ctx: ScanContext, storage, bucket: str, key: str, lo: int, hi: int, d_ptr: int,
+                    part: int = _GET_PART, threads: int = _GET_THREADS):
+    """Object bytes [lo, hi) into device memory at ``d_ptr``: parallel ranged GETs into the context's pinned
+    staging buffer, each part's H2D copy issued on the context stream as soon as that part has landed, so
+    the PCIe copy overlaps the remaining GETs (storage -> pinned -> HBM pipeline).
+    Returns the pinned buffer (valid until the context's next fetch).  The copies are asynchronous: work
+    enqueued afterwards on the same stream (the scan) sees the bytes."""
+    n = hi - lo
+    host = ctx.pinned("object", max(n, 1))
+    if n <= 0:
+        return host
+    view = host.view(n)
+    starts = list(range(0, n, part))
+    if len(starts) == 1:
+        read_range_into(storage, bucket, key, lo, hi, view, part=part, threads=threads)
+        ctx.h2d_async(d_ptr, host.ptr, n)
+        return host
+
+    def one(a: int) -> int:
+        read_range_into(storage, bucket, key, lo + a, lo + min(n, a + part), view[a:], part=part, threads=1)
+        return a
+
+    with cf.ThreadPoolExecutor(min(threads, len(starts))) as ex:
+        futs = [ex.submit(one, a) for a in starts]
+        for f in cf.as_completed(futs):       # H2D issued from this (the context's) thread only
+            a = f.result()
+            ctx.h2d_async(d_ptr + a, host.ptr + a, min(n, a + part) - a)
+    return host
+
+
 def resolve_line_end(ctx: ScanContext, storage, bucket: str, key: str, size: int, pos: int) -> int:
     """1 + the first '\\n' at or after object offset ``pos``, or ``size`` (what the reference's
     seek(start) + readline() + tell() gives for a header cut by its chunk end, fasta.py:45-56).
@@ -89,10 +119,8 @@ def _fasta_group(dev: int, co, plan: Sequence[Tuple[int, int]], u64: bool) -> np
     lo = min(c0 for c0, _ in plan)
     hi = max(c1 for _, c1 in plan)
     n = hi - lo
-    host = ctx.pinned("object", n)
-    read_range_into(co.storage, co.path.bucket, co.path.key, lo, hi, host.view(n))
     d = ctx.workspace("input", n + 64)
-    ctx.h2d_async(d.ptr, host.ptr, n)
+    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, d.ptr)
     pairs, pending, _ = ctx.fasta_index(d.ptr, n, lo, size, plan, u64=u64)
     for p in pending[pending >= 0]:
         start = int(pairs[p, 0])
@@ -138,10 +166,8 @@ def fasta_index_chunk(co, data, chunk_offset: int, job: int = 0, u64: bool = Fal
 def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int):
     ctx = get_context(dev)
     n = hi - lo
-    host = ctx.pinned("object", n)
-    read_range_into(co.storage, co.path.bucket, co.path.key, lo, hi, host.view(n))
     d = ctx.workspace("input", n + 64)
-    ctx.h2d_async(d.ptr, host.ptr, n)
+    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, d.ptr)
     return ctx.delim_index(d.ptr, n, lo, lo, hi, delim=delim, every_k=every_k, emit_add=emit_add, u64=True)
 
 

@@ -21,6 +21,8 @@ import xml.etree.ElementTree as ET
 from email.utils import formatdate
 from typing import Dict, Optional
 
+import numpy as np
+
 from .errors import ClientError
 from .memory import MemoryStore, parse_range
 
@@ -48,7 +50,9 @@ class StreamingBody(io.RawIOBase):
         if n <= 0:
             return 0
         if isinstance(self._src, memoryview):
-            memoryview(b).cast("B")[:n] = self._src[self._pos:self._pos + n]
+            # numpy copies without holding the GIL, so parallel ranged GETs copy in parallel
+            np.copyto(np.frombuffer(memoryview(b).cast("B")[:n], np.uint8),
+                      np.frombuffer(self._src[self._pos:self._pos + n], np.uint8))
         else:
             n = self._src.readinto(memoryview(b).cast("B")[:n])
             if n == 0:

@@ -69,6 +69,11 @@ def main():
     ctx.h2d_async(d.ptr, pin.ptr, size)
     ctx.sync()
     t_h2d = time.perf_counter() - t0
+    ctx.sync()
+    t0 = time.perf_counter()
+    so.fetch_to_device(ctx, co.storage, "genomics", "x.fasta", 0, size, d.ptr)
+    ctx.sync()
+    t_pipe = time.perf_counter() - t0
     plan = [(i * cs, min(size, (i + 1) * cs)) for i in range(size // cs)]
     ctx.fasta_index(d.ptr, size, 0, size, plan)
     t0 = time.perf_counter()
@@ -76,6 +81,7 @@ def main():
     t_scan = time.perf_counter() - t0
     res.update({"stage_get_into_pinned_GiB_per_s": round(size / t_get / GiB, 2),
                 "stage_h2d_GiB_per_s": round(size / t_h2d / GiB, 2),
+                "stage_get_h2d_pipelined_GiB_per_s": round(size / t_pipe / GiB, 2),
                 "stage_scan_plus_d2h_s": round(t_scan, 4), "index_bytes": int(pairs.nbytes)})
     srv.stop()
     print(json.dumps(res), flush=True)
