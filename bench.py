@@ -204,9 +204,8 @@ def main_delim(args, world, rank, local, dist):
     if csv_mode:
         begin, end = 0, size
     else:
-        bo = len(obj.head)                                   # body_offset (vcf.py:19-67)
-        cs = math.ceil((size - bo) / world)
-        begin, end = min(size, bo + rank * cs), min(size, bo + (rank + 1) * cs)
+        from dataplug_amd.dist import rank_byte_range
+        begin, end = rank_byte_range(len(obj.head), size, rank, world)   # body [body_offset, size), vcf.py:19-67
     nbytes = end - begin
     n_exp = obj.count_range(begin, end)
     ctx = ScanContext(local)

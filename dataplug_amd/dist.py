@@ -31,6 +31,14 @@ def rank_chunks(nchunks: int, rank: int, world: int) -> Tuple[int, int]:
     return groups[rank] if rank < len(groups) else (nchunks, nchunks)
 
 
+def rank_byte_range(begin: int, end: int, rank: int, world: int) -> Tuple[int, int]:
+    """Raw byte range of ``rank`` when one object's [begin, end) is cut into ``world`` parts for a newline
+    index (bench.py --workload vcf): ceil-sized parts, so the parts' offset lists concatenate, in rank
+    order, to the whole range's index (no boundary adjustment is needed for a delimiter index)."""
+    step = -(-(end - begin) // world) if end > begin else 0
+    return min(end, begin + rank * step), min(end, begin + (rank + 1) * step)
+
+
 @dataclass
 class Dist:
     world: int = 1

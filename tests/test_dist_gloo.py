@@ -9,7 +9,7 @@ import textwrap
 
 import numpy as np
 
-from dataplug_amd.dist import rank_chunks, split_groups
+from dataplug_amd.dist import rank_byte_range, rank_chunks, split_groups
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -25,6 +25,23 @@ def test_split_groups_cover_and_disjoint():
     assert rank_chunks(2, 3, 4) == (2, 2)
 
 
+def test_rank_byte_ranges_concatenate_to_whole_index():
+    """bench.py --workload vcf: the per-rank newline indexes of the body parts concatenate to the whole."""
+    from dataplug_amd import synth
+    from oracle import cpu_ref
+    t = synth.tiled_vcf(2_000_003, seed=4, block=300_007)
+    a = t.bytes_range(0, t.size)
+    bo = len(t.head)
+    whole = cpu_ref.delim_index(a, bo, t.size)
+    for world in (1, 2, 3, 8, 13):
+        parts = [rank_byte_range(bo, t.size, r, world) for r in range(world)]
+        assert parts[0][0] == bo and parts[-1][1] == t.size
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(world - 1))
+        got = np.concatenate([cpu_ref.delim_index(a, lo, hi) for lo, hi in parts])
+        assert np.array_equal(got, whole)
+    assert rank_byte_range(5, 5, 0, 4) == (5, 5)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -37,7 +54,7 @@ WORKER = textwrap.dedent("""
     import json, os, sys
     import numpy as np
     sys.path.insert(0, {repo!r})
-    from dataplug_amd.dist import Dist, rank_chunks
+    from dataplug_amd.dist import Dist, rank_byte_range, rank_chunks
     from dataplug_amd import synth
     from oracle import cpu_ref
     d = Dist.from_env(backend="gloo")
@@ -46,9 +63,12 @@ WORKER = textwrap.dedent("""
     i0, i1 = rank_chunks(len(plan), d.rank, d.world)
     mine = [cpu_ref.fasta_chunk_pairs(data, c0, c1) for c0, c1 in plan[i0:i1]]
     d.barrier()
+    tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
+    lo, hi = rank_byte_range(len(tv.head), tv.size, d.rank, d.world)
+    nl = np.concatenate(list(tv.delims_range(lo, hi))).tolist()
     mx = d.max(float(d.rank + 1))
     sm = d.sum(float(sum(len(m) for m in mine)))
-    out = {{"rank": d.rank, "range": [i0, i1], "pairs": [p for m in mine for p in m], "max": mx, "sum": sm}}
+    out = {{"rank": d.rank, "range": [i0, i1], "pairs": [p for m in mine for p in m], "max": mx, "sum": sm, "nl": nl}}
     with open(os.path.join({tmp!r}, f"r{{d.rank}}.json"), "w") as f:
         json.dump(out, f)
     d.close()
@@ -77,3 +97,6 @@ def test_two_rank_gloo(tmp_path):
     assert res[0]["pairs"] + res[1]["pairs"] == whole
     assert res[0]["max"] == res[1]["max"] == 2.0
     assert res[0]["sum"] == res[1]["sum"] == float(n)
+    tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
+    body_nl = cpu_ref.delim_index(tv.bytes_range(0, tv.size), len(tv.head), tv.size).tolist()
+    assert res[0]["nl"] + res[1]["nl"] == body_nl
