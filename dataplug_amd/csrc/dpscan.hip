@@ -174,6 +174,11 @@ __device__ __forceinline__ uint32_t match4(uint32_t w, uint32_t key) {
 #ifndef DP_PACK_IND
 #define DP_PACK_IND 1
 #endif
+// DELIM output stores with the non-temporal hint (the index is not re-read by the kernel).  Same-box A/B:
+// CSV/VCF +2%; on FASTA's sparse 4-byte stores the hint measured -1 to -2%, so FASTA keeps plain stores.
+#ifndef DP_NTSTORE
+#define DP_NTSTORE 1
+#endif
 #ifndef DP_PAIRSTORE   // DELIM phase B: 16-byte stores of offset pairs (uint64 output, every_k = 1)
 #define DP_PAIRSTORE 1
 #endif
@@ -290,9 +295,10 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
 #endif
 }
 
-template <typename T>
+template <typename T, bool NT = false>
 __device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
-  reinterpret_cast<T*>(out)[i] = (T)v;
+  if constexpr (NT) __builtin_nontemporal_store((T)v, reinterpret_cast<T*>(out) + i);
+  else reinterpret_cast<T*>(out)[i] = (T)v;
 }
 
 // Summary of a byte range as a function of the incoming line state S (does the current line already
@@ -895,7 +901,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
       const uint64_t q = q0 + t;
       const uint64_t val = add + pos;
       if (near4g) ovf |= val > 0xFFFFFFFFull;
-      put<OutT>(A.out, q < last ? q : last, val);
+      put<OutT, DP_NTSTORE != 0>(A.out, q < last ? q : last, val);
     };
     const uint32_t key = A.delim ^ kSel12;
 #pragma unroll 1
@@ -963,10 +969,17 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
           const uint64_t v0 = add + evw[(ev0 + i) & kEvMask];
           if (t + 1u < m) {
             const uint64_t v1 = add + evw[(ev0 + i + 1u) & kEvMask];
+#if DP_NTSTORE
+            __builtin_nontemporal_store(v2u64{v0, v1}, reinterpret_cast<v2u64*>(o + i));
+          } else {
+            __builtin_nontemporal_store((uint64_t)v0, o + i);
+          }
+#else
             *reinterpret_cast<v2u64*>(o + i) = v2u64{v0, v1};
           } else {
             o[i] = v0;
           }
+#endif
         }
         return;
       }
@@ -976,7 +989,7 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
       const uint64_t q = q0 + t;
       const uint64_t val = add + evw[(ev0 + r0 + t * k) & kEvMask];
       if (near4g) ovf |= val > 0xFFFFFFFFull;
-      put<OutT>(A.out, q < last ? q : last, val);
+      put<OutT, DP_NTSTORE != 0>(A.out, q < last ? q : last, val);
     }
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
