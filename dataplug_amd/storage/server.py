@@ -197,8 +197,11 @@ def main(argv=None):
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=9000)
     ap.add_argument("--put", action="append", default=[], metavar="BUCKET/KEY=PATH")
+    ap.add_argument("--bucket", action="append", default=[], help="create this (empty) bucket")
     args = ap.parse_args(argv)
     srv = LoopbackS3Server(host=args.host, port=args.port)
+    for b in args.bucket:
+        srv.store.create_bucket(b)
     for spec in args.put:
         dst, _, path = spec.partition("=")
         bucket, _, key = dst.partition("/")

@@ -2,9 +2,10 @@
 
     python tools/e2e_rate.py [--size BYTES] [--reps N]
 
-co.preprocess(chunk_size=size/4) on a synthetic FASTA held by (a) an in-process store (memory://) and
-(b) the loopback HTTP S3 server: ranged GETs into pinned host memory -> H2D -> scan -> D2H of the index
--> PUT of index + attrs.  Also times the stages separately on the same object.
+co.preprocess(chunk_size=size/4) on a synthetic FASTA held by (a) an in-process store (memory://), (b) the
+loopback HTTP S3 server in its own process, and (c) the same server as a thread of this process: ranged
+GETs into pinned host memory -> H2D -> scan -> D2H of the index -> PUT of index + attrs.  Also times the
+stages separately on the same object.
 """
 from __future__ import annotations
 
@@ -12,12 +13,15 @@ import argparse
 import json
 import math
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
 
 from dataplug_amd import synth  # noqa: E402
 from dataplug_amd.cloudobject import CloudObject  # noqa: E402
@@ -33,6 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4 << 30)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--port", type=int, default=19001)
     args = ap.parse_args()
     size = args.size
     host = synth.tiled_fasta_host(size, seed=1)
@@ -44,7 +49,22 @@ def main():
     cs = math.ceil(size / 4)
     res = {"object_bytes": size, "chunk_size": cs}
     srv = LoopbackS3Server(store).start()
-    for name, cfg in (("memory", {"endpoint_url": "memory://e2e"}), ("loopback_http", srv.storage_config)):
+    # the loopback server in its own process, as MinIO serves the reference's examples (an in-process server
+    # shares the GIL with the client's GET threads: tools/http_probe.py)
+    with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp"), delete=False) as f:
+        f.write(memoryview(store.get("genomics", "x.fasta").data))
+        path = f.name
+    port = args.port
+    proc = subprocess.Popen([sys.executable, "-m", "dataplug_amd.storage.server", "--port", str(port),
+                             "--put", f"genomics/x.fasta={path}", "--bucket", "genomics.meta"],
+                            cwd=REPO, stdout=subprocess.PIPE, text=True)
+    line = proc.stdout.readline()
+    assert line.startswith("serving"), line
+    os.unlink(path)
+    configs = (("memory", {"endpoint_url": "memory://e2e"}),
+               ("loopback_http", {"endpoint_url": f"http://127.0.0.1:{port}"}),
+               ("loopback_http_in_process", srv.storage_config))
+    for name, cfg in configs:
         co = CloudObject.from_s3(FASTA, "s3://genomics/x.fasta", s3_config=cfg)
         co.preprocess(chunk_size=cs, force=True)          # warm: context, pinned + device buffers
         ts = []
@@ -84,6 +104,8 @@ def main():
                 "stage_get_h2d_pipelined_GiB_per_s": round(size / t_pipe / GiB, 2),
                 "stage_scan_plus_d2h_s": round(t_scan, 4), "index_bytes": int(pairs.nbytes)})
     srv.stop()
+    proc.terminate()
+    proc.wait(timeout=30)
     print(json.dumps(res), flush=True)
 
 
