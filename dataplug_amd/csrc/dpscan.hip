@@ -77,6 +77,9 @@ static_assert(kRows * kBufs == kRangeRows && kRows >= 2 && kRows <= 8, "buffers 
 #ifndef DP_LBFAST
 #define DP_LBFAST 1
 #endif
+#ifndef DP_LAGSHIFT    // DP_PRIO 2: issue priority = min(lag << DP_LAGSHIFT, 3)
+#define DP_LAGSHIFT 0
+#endif
 #ifndef DP_PRIO_LEVELS
 #define DP_PRIO_LEVELS 4u
 #endif
@@ -1223,7 +1226,8 @@ struct DataWave {
       uint32_t front = 0;
       if (lane == 0) front = __hip_atomic_fetch_max(&sh.front, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       front = rfl(front);
-      set_prio(front > k ? (front - k < 3u ? front - k : 3u) : 0u);
+      const uint32_t lag = front > k ? (front - k) << DP_LAGSHIFT : 0u;
+      set_prio(lag < 3u ? lag : 3u);
     }
 #else
     set_prio(((uint32_t)(wave >> 2) + k) % DP_PRIO_LEVELS);   // the 4 data waves of a SIMD take turns
