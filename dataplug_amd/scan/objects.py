@@ -64,13 +64,14 @@ def read_range_into(storage, bucket: str, key: str, lo: int, hi: int, out: memor
 
 
 def fetch_to_device(ctx: ScanContext, storage, bucket: str, key: str, lo: int, hi: int, d_ptr: int,
-                    part: int = _GET_PART, threads: int = _GET_THREADS):
+                    part: Optional[int] = None, threads: int = _GET_THREADS):
     """Object bytes [lo, hi) into device memory at ``d_ptr``: parallel ranged GETs into the context's pinned
     staging buffer, each part's H2D copy issued on the context stream as soon as that part has landed, so
     the PCIe copy overlaps the remaining GETs (storage -> pinned -> HBM pipeline).
     Returns the pinned buffer (valid until the context's next fetch).  The copies are asynchronous: work
     enqueued afterwards on the same stream (the scan) sees the bytes."""
     n = hi - lo
+    part = part or _GET_PART
     host = ctx.pinned("object", max(n, 1))
     if n <= 0:
         return host

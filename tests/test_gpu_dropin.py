@@ -94,6 +94,27 @@ def test_fasta_synthetic_groups(monkeypatch, devices, div):
     assert np.array_equal(_index(co), exp.reshape(-1).astype(np.uint32))
 
 
+@pytest.mark.parametrize("part", [None, (1 << 20) + 13])
+@pytest.mark.parametrize("where", ["memory", "loopback"])
+def test_fasta_pipelined_fetch_many_parts(server, monkeypatch, part, where):
+    """storage -> pinned -> HBM pipeline (objects.fetch_to_device): many ranged-GET parts (ragged last part)
+    whose H2D copies are issued as they land, out of order; the index equals the oracle's."""
+    from oracle import cpu_ref, dpref
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    from dataplug_amd.scan import objects
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0")
+    if part:
+        monkeypatch.setattr(objects, "_GET_PART", part)
+    n = (100 << 20) + 4099 if part is None else (16 << 20) + 777
+    data = synth.fasta(n, 31)
+    cfg = _mem(f"gpu_pipe_{part}") if where == "memory" else server.storage_config
+    co = _co(FASTA, data.tobytes(), f"pipe_{part}_{where}", cfg)
+    cs = -(-n // 4)
+    co.preprocess(chunk_size=cs, force=True)
+    exp = dpref.fasta_pairs(data, cpu_ref.chunk_plan(n, cs))
+    assert np.array_equal(_index(co), exp.reshape(-1).astype(np.uint32))
+
+
 def test_fasta_header_crossing_group_boundary(monkeypatch):
     """A header line opened near the end of group 0's last chunk whose '\\n' lies far inside group 1's
     region: group 0's buffer has no newline after it -> pending -> dp_find_delim on later bytes."""
