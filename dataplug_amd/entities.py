@@ -74,6 +74,18 @@ class CloudObjectSlice:
         raise NotImplementedError()
 
 
+def get_slices(slices, threads: int = 16) -> list:
+    """``[s.get() for s in slices]`` with the slices fetched concurrently: each ``get()``
+    is ranged GETs plus copies that release the GIL, so a thread pool materializes many slices at storage
+    speed.  The results, and any exception, are those of the sequential loop."""
+    slices = list(slices)
+    if threads <= 1 or len(slices) <= 1:
+        return [s.get() for s in slices]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(min(threads, len(slices))) as ex:
+        return list(ex.map(lambda s: s.get(), slices))
+
+
 class PartitioningStrategy:
     """Decorator for partitioning strategies (entities.py:74-87)."""
 

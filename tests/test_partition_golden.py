@@ -15,6 +15,7 @@ import pytest
 
 from dataplug_amd import synth
 from dataplug_amd.cloudobject import CloudObject
+from dataplug_amd.entities import get_slices
 from dataplug_amd.formats._lines import SliceError, store_line_index
 from dataplug_amd.preprocessing.handler import upload_metadata
 from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
@@ -85,6 +86,8 @@ def test_csv_partitions_match_reference():
                 else:
                     assert s.get() == e[2], (rec["object"], kw, s.chunk_id)
                 checked += 1
+            if not any(isinstance(e[2], dict) for e in expected):
+                assert get_slices(slices, threads=4) == [e[2] for e in expected]
     assert checked > 100
 
 
@@ -142,6 +145,7 @@ def test_fasta_partitions_match_reference():
         assert got == rec["slices"], (rec["object"], rec["num_chunks"])
         if "get" in rec:
             assert [base64.b64encode(s.get()).decode() for s in slices] == rec["get"]
+        assert get_slices(slices, threads=4) == [s.get() for s in slices]
         n_checked += 1
     assert n_checked >= 5
 
