@@ -68,7 +68,8 @@ def init_dist(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
-    if world > 1:
+    # any launch by torch.distributed.run (even one rank) takes the RCCL path the N > 1 runs take
+    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
         import torch
         import torch.distributed as dist_mod
         torch.cuda.set_device(local)
