@@ -4,25 +4,30 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--no-cpu-baseline]
     python bench.py --workload csv|vcf ...    (BASELINE configs[2] / configs[3]: newline index)
 
-One step = one whole co.preprocess(chunk_size=size/4) equivalent over one synthetic 4 GiB FASTA object
-that is already resident in HBM: chunk-plan upload, the single-pass scan kernel, the split-header
-resolve kernel and the read-back of the pair count / per-chunk state (the index itself stays in HBM;
-the H2D/D2H-inclusive end-to-end rate is reported separately).
+The workload is ONE synthetic FASTA object of N x 4 GiB (N = --gpus) with the reference's chunk plan at
+chunk_size = 1 GiB (size / 4N: 4 chunks per GPU, the configs[1] plan at N = 1), split over the N GPUs by
+the product's multi-GPU split (``scan.objects.fasta_groups``: contiguous chunk groups, one per GPU, no
+collective; the reference runs the chunks as independent map jobs, preprocess.py:39-51).  Each GPU holds
+its group's bytes (+ a 64 KiB look-ahead halo) in HBM before the timed region.
 
-Steps are issued the way a caller indexing a stream of objects would: two scan contexts (streams)
-alternate, and step k + 1 is enqueued before step k's result is collected, so one step's host round trip
-hides behind the next step's scan.  Every step does the whole pass and reads back its result.  `value`
-comes from K such steps whose scans may overlap on the GPU (the next object's scan starts on the CUs the
-previous one's last workgroups leave idle); `serialized` repeats the K steps with each scan waiting on the
-device for the previous one.
+One step = on every GPU, one dp_fasta_index over its chunk group: the chunk-table check, the single-pass
+scan kernel, the split-header resolve kernel and the read-back of pair count / per-chunk state (the index
+stays in HBM; the H2D/D2H-inclusive end-to-end rate is in DESIGN.md §6).  Steps alternate between two
+scan contexts (streams) and step k + 1 is enqueued before step k's result is collected, so the host round
+trip hides behind the next scan; each scan waits on the device for the previous one, so one scan runs at a
+time and ``ms_per_step`` >= the scan kernel's own duration.
 
-Multi-GPU (``torch.distributed.run --nproc-per-node N``): one process per GPU, each indexing its own
-object (independent objects/chunks, no collective on the data path; weak scaling).  Barrier + device
-sync bracket the K timed steps; the max time over ranks is reported.
+Launch modes (the same worker code in both):
+  * ``python bench.py --gpus N``: one process, one host thread per GPU (how ``co.preprocess`` runs a
+    multi-GPU object, scan/objects.py); exits non-zero if fewer than N devices are visible
+    (``--devices 0,0,0,0`` maps workers to devices explicitly, e.g. to rehearse the split on one GPU).
+  * ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``: one rank per GPU; barriers and
+    the max/sum reductions go over a gloo CPU group, so RCCL is never initialised (nothing is exchanged).
 
-Also measured inside this run: the scan kernel's average duration from HIP events on its own stream
-over the K serialized launches (-> roofline), and, on rank 0 at N = 1, the reference algorithm on the
-host cores (cpu_baseline).
+Also measured in this run: every GPU's scan-kernel average duration from HIP events on its own stream
+(-> roofline, with a read-only stream kernel's rate on the same buffer as the measured peak), the fixed-
+total ("strong") curve point — the configs[1] 4 GiB object split over the same N GPUs — and, at N = 1, the
+reference algorithm on the host cores (cpu_baseline).
 """
 from __future__ import annotations
 
@@ -31,6 +36,7 @@ import json
 import math
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -51,8 +57,11 @@ def parse():
                    help="fasta: configs[1] (default, the headline line); csv: configs[2], a 32 GiB CSV per GPU; "
                         "vcf: configs[3], one 64 GiB VCF whose body is cut into one part per GPU")
     p.add_argument("--size", type=int, default=None,
-                   help="object bytes (default 4 GiB fasta, 32 GiB csv, 64 GiB vcf)")
-    p.add_argument("--chunks", type=int, default=4, help="chunk_size = ceil(size / chunks) (fasta_example.py)")
+                   help="bytes per GPU (default 4 GiB fasta, 32 GiB csv) / object bytes (vcf, default 64 GiB)")
+    p.add_argument("--chunks", type=int, default=4, help="FASTA map chunks per GPU (chunk_size = size / (chunks*N))")
+    p.add_argument("--devices", default=None,
+                   help="thread mode: comma-separated device of each worker (default 0..N-1)")
+    p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) point")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--traffic-bytes", type=float, default=None,
@@ -63,44 +72,147 @@ def parse():
     return p.parse_args()
 
 
-def init_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # any launch by torch.distributed.run (even one rank) takes the RCCL path the N > 1 runs take
-    if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ:
-        import torch
-        import torch.distributed as dist_mod
-        torch.cuda.set_device(local)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
-        dist = dist_mod
-    return world, rank, local, dist
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def barrier(dist, local):
-    if dist is not None:
-        import torch
-        dist.barrier()
-        torch.cuda.synchronize(local)
+# ------------------------------------------------------------------------------------------ team of workers
+class Team:
+    """The workers of one run: host threads of this process (one per GPU), or this process as one rank of
+    a torch.distributed.run launch (gloo CPU group: barriers and the final gather only, never RCCL)."""
+
+    def __init__(self, n_local: int, pg=None):
+        self._tb = threading.Barrier(n_local)
+        self.pg = pg
+
+    def barrier(self):
+        self._tb.wait()
+        if self.pg is not None:
+            self.pg.barrier()
+
+    def gather(self, results):
+        """rank 0: every rank's list of worker results, concatenated; other ranks: None."""
+        if self.pg is None:
+            return results
+        out = [None] * self.pg.get_world_size()
+        self.pg.all_gather_object(out, results)
+        return [r for rs in out for r in rs] if self.pg.get_rank() == 0 else None
 
 
-def max_over_ranks(dist, local, x: float) -> float:
-    if dist is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def launch_mode(args):
+    """(world, rank, [devices of this process's workers], process group or None)."""
+    from dataplug_amd.scan import device_count
+    if "TORCHELASTIC_RUN_ID" in os.environ or int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch.distributed as dist
+        world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        if args.gpus not in (1, world):
+            log(f"--gpus {args.gpus} != WORLD_SIZE {world}: one rank per GPU, using {world}")
+        if local >= device_count():
+            log(f"rank {rank}: local rank {local} but only {device_count()} device(s) visible")
+            sys.exit(2)
+        dist.init_process_group("gloo")
+        return world, rank, [local], dist
+    n = args.gpus
+    devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
+    if len(devs) != n:
+        log(f"--devices names {len(devs)} device(s) for --gpus {n}")
+        sys.exit(2)
+    visible = device_count()
+    if max(devs) >= visible:
+        log(f"--gpus {n} needs devices {sorted(set(devs))}, but only {visible} visible")
+        sys.exit(2)
+    return n, 0, devs, None
 
 
-def sum_over_ranks(dist, local, x: float) -> float:
-    if dist is None:
-        return x
-    import torch
-    t = torch.tensor([x], dtype=torch.float64, device=f"cuda:{local}")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+def run_workers(fn, devs, rank0_index, team):
+    """fn(worker index, device) on one thread per device (inline when there is one); the results in order."""
+    if len(devs) == 1:
+        return [fn(rank0_index, devs[0])]
+    res, errs = [None] * len(devs), []
+
+    def body(i):
+        try:
+            res[i] = fn(rank0_index + i, devs[i])
+        except BaseException as e:      # a failed worker must not leave the others waiting in a barrier
+            errs.append(e)
+            team._tb.abort()
+
+    th = [threading.Thread(target=body, args=(i,)) for i in range(len(devs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return res
+
+
+class Steps:
+    """K steps of one scan workload alternating between two contexts of one GPU (see the module doc)."""
+
+    def __init__(self, team, ctxs, launch, collect):
+        self.team, self.ctxs, self.launch, self.collect = team, ctxs, launch, collect
+
+    def warm(self, n):
+        for i in range(max(2, n)):                    # both contexts (workspaces, code objects)
+            self.launch(i)
+            self.collect(i)
+
+    def timed(self, steps, serialize=True, timing=False):
+        """Wall seconds of ``steps`` steps between barrier + device sync on both sides; with ``timing``
+        also (kernel ms total, launches) from HIP events around every scan launch; and the last result."""
+        c0, c1 = self.ctxs
+        if timing:
+            for c in self.ctxs:
+                c.timing(True)
+                c.timing_read()
+        c0.sync()
+        c1.sync()
+        self.team.barrier()
+        t0 = time.perf_counter()
+        self.launch(0)
+        for i in range(1, steps):
+            if serialize:
+                self.ctxs[i % 2].wait_for(self.ctxs[(i - 1) % 2])
+            self.launch(i)
+            self.collect(i - 1)
+        res = self.collect(steps - 1)
+        c0.sync()
+        c1.sync()
+        self.team.barrier()
+        dt = time.perf_counter() - t0
+        kern = (0.0, 0)
+        if timing:
+            ms, n = 0.0, 0
+            for c in self.ctxs:
+                a, b = c.timing_read()
+                c.timing(False)
+                ms += a
+                n += b
+            kern = (ms, n)
+        return dt, kern, res
+
+
+def stream_peak(ctx, d_ptr, nbytes, reps=5):
+    """Best read rate (B/s) of the plain read-only stream kernel over this buffer (measured roofline)."""
+    best = 0.0
+    n16 = nbytes // 16 * 16
+    for bpc in (4, 8):
+        ctx.stream_read(d_ptr, n16, bpc)
+        ctx.sync()
+        ctx.timing(True)
+        ctx.timing_read()
+        for _ in range(reps):
+            ctx.stream_read(d_ptr, n16, bpc)
+        ms, n = ctx.timing_read()
+        ctx.timing(False)
+        best = max(best, n16 / (ms / 1e3 / max(1, n)))
+    return best
+
+
+# ------------------------------------------------------------------------------------------ CPU baseline
+_CPU_OBJ = b""
 
 
 def _regex_chunk(args):
@@ -110,50 +222,71 @@ def _regex_chunk(args):
     return len(cpu_ref.fasta_chunk_pairs(_CPU_OBJ, c0, c1))
 
 
-_CPU_OBJ = b""
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+
+
+def pool_workers():
+    """Fork-pool size: every CPU this process may use, capped by the box's CPU share (OMP_NUM_THREADS=16
+    on the GPU box, where os.cpu_count() reports the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, cap) if cap > 0 else n)
 
 
 def cpu_baseline(host: np.ndarray, chunk_size: int):
-    """The reference algorithm (re.finditer per chunk + fix-up) on the host cores, bounded sample."""
+    """The reference algorithm (re.finditer per chunk + split-header fix-up, fasta.py:24-63) on the host:
+    (1) a fork pool over every usable core, 64 chunks of the object's first GiB; (2) one core, the same GiB;
+    (3) the reference's default shape, parallel_config={} (sequential): the configs[1] chunk plan over the
+    WHOLE object, each chunk copied out first (the ranged GET's bytes, handler.py:39-42)."""
     import multiprocessing as mp
     global _CPU_OBJ
-    sample = min(len(host), 1 << 30)                 # bounded sample: the object's first GiB
+    from oracle import cpu_ref
+    sample = min(len(host), 1 << 30)
     _CPU_OBJ = host[:sample].tobytes()
-    cs = max(1, min(chunk_size, sample // 64))       # fan chunks out over a fork pool (BASELINE.md §3)
+    cs = max(1, sample // 64)
     plan = [(i * cs, (i + 1) * cs) for i in range(sample // cs)]
-    cores = min(16, os.cpu_count() or 1)
+    workers = pool_workers()
     t0 = time.perf_counter()
-    with mp.get_context("fork").Pool(cores) as pool:
+    with mp.get_context("fork").Pool(workers) as pool:
         pool.map(_regex_chunk, plan, chunksize=1)
     t_pool = time.perf_counter() - t0
-    one = _CPU_OBJ[: 256 << 20]
     t0 = time.perf_counter()
-    from oracle import cpu_ref
-    cpu_ref.fasta_chunk_pairs(one, 0, len(one))
+    for c0, c1 in plan:
+        cpu_ref.fasta_chunk_pairs(_CPU_OBJ, c0, c1)
     t_one = time.perf_counter() - t0
+    _CPU_OBJ = b""
+    seq_plan = cpu_ref.chunk_plan(len(host), chunk_size)
+    t0 = time.perf_counter()
+    for c0, c1 in seq_plan:
+        data = host[c0:c1].tobytes()              # the chunk's GET body
+        pairs = [(c0 + m.start(), c0 + m.end()) for m in cpu_ref._HEADER_RE.finditer(data)]
+        np.array(pairs, dtype=np.uint64)
+        del data
+    t_seq = time.perf_counter() - t0
     scanned = len(plan) * cs
-    return {"value": round(scanned / t_pool / GiB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
+    seq_bytes = sum(c1 - c0 for c0, c1 in seq_plan)
+    return {"value": round(scanned / t_pool / GiB, 3), "unit": "GiB/s", "cores": workers, "kind": "port",
             "sample": f"first {scanned / GiB:.2f} GiB of the object, {len(plan)} chunks of {cs} B, "
-                      f"re.finditer(rb'>.+(\\n)?') + fix-up per chunk (fasta.py:36-56) over a fork pool",
-            "value_1core": round(len(one) / t_one / GiB, 3)}
-
-
-def load_traffic(args, size):
-    """(HBM bytes per scan launch, source) from --traffic-bytes or a committed rocprofv3 PMC summary of the
-    same workload (tools/pmc_summary.py), else (None, None)."""
-    if args.traffic_bytes:
-        return args.traffic_bytes, "--traffic-bytes"
-    suffix = "" if args.workload == "fasta" else "_" + args.workload
-    path = args.traffic_from or os.path.join(REPO, "profiles", f"latest_pmc_summary{suffix}.json")
-    if not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        pmc = json.load(f)
-    kernel = "scan_kernel<0" if args.workload == "fasta" else "scan_kernel<1"
-    if pmc.get("object_bytes", size) != size or "hbm_traffic_bytes" not in pmc \
-            or not pmc.get("kernel", kernel).startswith(kernel):
-        return None, None
-    return pmc["hbm_traffic_bytes"], os.path.relpath(os.path.realpath(path), REPO)
+                      f"re.finditer(rb'>.+(\\n)?') + fix-up per chunk (fasta.py:36-56) over a {workers}-process "
+                      f"fork pool",
+            "value_1core": round(scanned / t_one / GiB, 3),
+            "sequential_default": {"value": round(seq_bytes / t_seq / GiB, 3), "unit": "GiB/s", "cores": 1,
+                                   "sample": f"the whole {len(host) / GiB:g} GiB object, {len(seq_plan)} chunks "
+                                             f"of {chunk_size} B in order (parallel_config={{}}): chunk copy + "
+                                             f"regex + uint32 packing"},
+            "host": host_info()}
 
 
 def _delim_chunk(args):
@@ -168,61 +301,242 @@ def cpu_baseline_delim(host: np.ndarray):
     csv.py:60-98, vcf.py:98-140) on the host cores, bounded sample."""
     import multiprocessing as mp
     global _CPU_OBJ
+    from oracle import cpu_ref
     _CPU_OBJ = host[: min(len(host), 1 << 30)]
     cs = max(1, len(_CPU_OBJ) // 64)
     plan = [(i * cs, (i + 1) * cs) for i in range(len(_CPU_OBJ) // cs)]
-    cores = min(16, os.cpu_count() or 1)
+    workers = pool_workers()
     t0 = time.perf_counter()
-    with mp.get_context("fork").Pool(cores) as pool:
+    with mp.get_context("fork").Pool(workers) as pool:
         pool.map(_delim_chunk, plan, chunksize=1)
     t_pool = time.perf_counter() - t0
-    from oracle import cpu_ref
-    one = _CPU_OBJ[: 256 << 20]
     t0 = time.perf_counter()
-    cpu_ref.delim_index(one)
+    for c0, c1 in plan:
+        cpu_ref.delim_index(_CPU_OBJ, c0, c1)
     t_one = time.perf_counter() - t0
     scanned = len(plan) * cs
-    return {"value": round(scanned / t_pool / GiB, 3), "unit": "GiB/s", "cores": cores, "kind": "port",
+    _CPU_OBJ = b""
+    return {"value": round(scanned / t_pool / GiB, 3), "unit": "GiB/s", "cores": workers, "kind": "port",
             "sample": f"first {scanned / GiB:.2f} GiB of the scanned range, {len(plan)} chunks of {cs} B, "
-                      f"numpy flatnonzero(== '\\n') per chunk over a fork pool",
-            "value_1core": round(len(one) / t_one / GiB, 3)}
+                      f"numpy flatnonzero(== '\\n') per chunk over a {workers}-process fork pool",
+            "value_1core": round(scanned / t_one / GiB, 3), "host": host_info()}
 
 
-def main_delim(args, world, rank, local, dist):
-    """BASELINE configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3]
-    (vcf: ONE 64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong
-    scaling): the uint64 newline index (dp_delim_index), device-resident, timed like the FASTA line."""
-    from dataplug_amd import synth
+def load_traffic(args, size, kernel):
+    """(HBM bytes per scan launch, source) from --traffic-bytes or a committed rocprofv3 PMC summary of the
+    same workload and per-GPU size (tools/pmc_summary.py), else (None, None)."""
+    if args.traffic_bytes:
+        return args.traffic_bytes, "--traffic-bytes"
+    suffix = "" if args.workload == "fasta" else "_" + args.workload
+    path = args.traffic_from or os.path.join(REPO, "profiles", f"latest_pmc_summary{suffix}.json")
+    if not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        pmc = json.load(f)
+    if pmc.get("object_bytes", size) != size or "hbm_traffic_bytes" not in pmc \
+            or not pmc.get("kernel", kernel).startswith(kernel):
+        return None, None
+    return pmc["hbm_traffic_bytes"], os.path.relpath(os.path.realpath(path), REPO)
+
+
+# ------------------------------------------------------------------------------------------ FASTA
+class FastaSpec:
+    """One FASTA object and its chunk plan, split over n workers (scan.objects.fasta_groups)."""
+
+    def __init__(self, size: int, chunks_total: int, n_workers: int, seed: int = 1):
+        from dataplug_amd import synth
+        from dataplug_amd.scan.objects import fasta_groups
+        self.size = size
+        self.chunk_size = math.ceil(size / chunks_total)
+        n = size // self.chunk_size
+        self.plan = [(i * self.chunk_size, size if self.chunk_size == n - 1 else (i + 1) * self.chunk_size)
+                     for i in range(n)]
+        self.groups = fasta_groups(self.plan, n_workers, size)
+        self.obj = synth.TiledFasta(size, seed=seed)
+        # the reference's uint32 index holds every offset < 2^32 (ends <= size; the synthetic object never
+        # ends inside a header line); larger objects need the opt-in uint64 index (index_dtype="uint64")
+        self.u64 = size > (1 << 32)
+
+
+def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, dev: int, keep_host: bool):
     from dataplug_amd.scan import ScanContext
+    out = {"worker": k, "device": dev}
+    ctxs = (ScanContext(dev), ScanContext(dev))
 
-    def log(msg):
-        print(f"[bench r{rank}] {msg}", file=sys.stderr, flush=True)
+    def prepare(sp: FastaSpec, tag: str):
+        if k >= len(sp.groups):
+            return None
+        g = sp.groups[k]
+        host = sp.obj.bytes_range(g.lo, g.buf_hi)
+        d_in = ctxs[0].workspace(f"in_{tag}", len(host) + 64)
+        ctxs[0].h2d(d_in.ptr, host)
+        chunks = np.ascontiguousarray(np.asarray(g.chunks(sp.plan), np.uint64).reshape(-1))
+        nch = len(chunks) // 2
+        cap = (g.hi - g.lo) // 256 + 1024
+        osz = 2 * cap * (8 if sp.u64 else 4)
+        d_outs = (ctxs[0].workspace(f"out_{tag}", osz), ctxs[1].workspace(f"out_{tag}", osz))
 
+        def launch(i):
+            ctxs[i % 2].fasta_index_async(d_in.ptr, len(host), g.lo, sp.size, chunks, d_outs[i % 2].ptr,
+                                           sp.u64, cap)
+
+        def collect(i):
+            return ctxs[i % 2].fasta_result(nch)
+
+        scanned = sum(c1 - c0 for c0, c1 in g.chunks(sp.plan))
+        return {"g": g, "host": host, "d_in": d_in, "d_outs": d_outs, "steps": Steps(team, ctxs, launch, collect),
+                "scanned": scanned, "chunks": chunks}
+
+    def verify(sp: FastaSpec, st, res, i_last):
+        n_pairs, pending, _ = res
+        if args.no_verify:
+            return None
+        from oracle import dpref          # the checker (test infrastructure), outside every timed region
+        g = st["g"]
+        rel = [(c0 - g.lo, c1 - g.lo) for c0, c1 in g.chunks(sp.plan)]
+        exp = dpref.fasta_pairs(st["host"], rel)
+        got = np.empty((n_pairs, 2), np.uint64 if sp.u64 else np.uint32)
+        ctxs[0].d2h(got, st["d_outs"][i_last % 2].ptr)
+        return bool((pending == -1).all() and np.array_equal(got.astype(np.uint64) - np.uint64(g.lo), exp))
+
+    t0 = time.perf_counter()
+    st = prepare(spec, "main")
+    ss = prepare(strong, "strong") if strong is not None else None
+    out["gen_s"] = time.perf_counter() - t0
+    S = st["steps"]
+    S.warm(args.warmup)
+    # (1) HIP events on each context's own stream around every scan launch: the kernel's own duration
+    dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
+    # (2) the K timed steps of `value` (no events)
+    dt, _, res = S.timed(args.steps)
+    # (3) the same steps without the device-side wait between consecutive scans (secondary)
+    dt_ov, _, _ = S.timed(args.steps, serialize=False)
+    out.update(dt=dt, dt_overlap=dt_ov, kern_s=kms / 1e3 / max(1, kn), scanned=st["scanned"], pairs=res[0],
+               alg_bytes=st["scanned"] + (16 if spec.u64 else 8) * res[0],
+               stream_peak=stream_peak(ctxs[0], st["d_in"].ptr, st["g"].hi - st["g"].lo))
+    out["verified"] = verify(spec, st, res, args.steps - 1)
+    if ss is not None:
+        ss["steps"].warm(args.warmup)
+        dts, (sms, sn), sres = ss["steps"].timed(args.steps, timing=True)
+        out["strong"] = {"dt": dts, "scanned": ss["scanned"], "pairs": sres[0], "kern_s": sms / 1e3 / max(1, sn),
+                         "verified": verify(strong, ss, sres, args.steps - 1)}
+    elif strong is not None:
+        team.barrier()                 # no group for this worker in the strong split: keep the barriers paired
+        team.barrier()
+    if keep_host:
+        out["host"] = st["host"]
+    for c in ctxs:
+        c.close()
+    return out
+
+
+def main_fasta(args, world, rank, devs, team):
+    per_gpu = args.size or (4 << 30)
+    size = per_gpu * world
+    spec = FastaSpec(size, args.chunks * world, world)
+    strong = None
+    if world > 1 and not args.no_strong:
+        strong = FastaSpec(per_gpu, args.chunks * world, world)
+    log(f"{world} GPU(s): one {size / GiB:g} GiB FASTA, {len(spec.plan)} chunks of {spec.chunk_size} B, "
+        f"{'uint64' if spec.u64 else 'uint32'} index, devices {devs} (rank {rank})")
+    keep = world == 1 and not args.no_cpu_baseline
+    res = run_workers(lambda k, d: fasta_worker(args, team, spec, strong, k, d, keep), devs, rank * len(devs), team)
+    host = res[0].pop("host", None) if keep else None
+    allres = team.gather(res)
+    if allres is None:
+        return
+    K = args.steps
+    dt = max(r["dt"] for r in allres)
+    dt_ov = max(r["dt_overlap"] for r in allres)
+    scanned = sum(r["scanned"] for r in allres)
+    pairs = sum(r["pairs"] for r in allres)
+    kern = max(r["kern_s"] for r in allres)
+    ach = min(r["alg_bytes"] / r["kern_s"] for r in allres)
+    peak_meas = min(r["stream_peak"] for r in allres)
+    verified = None if args.no_verify else all(r["verified"] for r in allres)
+    cpu = cpu_baseline(host, spec.chunk_size) if host is not None else None
+    traffic, traffic_src = load_traffic(args, per_gpu, "scan_kernel<0") if world == 1 else (None, None)
+    strong_out = None
+    if strong is not None:
+        sr = [r["strong"] for r in allres if "strong" in r]
+        sdt = max(r["dt"] for r in sr)
+        strong_out = {"value": round(sum(r["scanned"] for r in sr) * K / sdt / GiB, 3), "unit": "GiB/s",
+                      "ms_per_step": round(sdt / K * 1e3, 4), "object_bytes": strong.size,
+                      "chunks": len(strong.plan), "gpus_used": len(sr),
+                      "kernel_avg_us_max": round(max(r["kern_s"] for r in sr) * 1e6, 2),
+                      "verified_bit_exact": None if args.no_verify else all(r["verified"] for r in sr),
+                      "note": "fixed total: the configs[1] 4 GiB object, chunk plan size/(4N), split over the "
+                              "same N GPUs (strong scaling point of SURVEY.md §8(e))"}
+    r0 = allres[0]
+    out = {
+        "metric": "GiB/s scanned (device-resident) + offsets/s, FASTA index at 1/2/4/8 MI355X",
+        "value": round(scanned * K / dt / GiB, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": f"FASTA '>' header index of ONE {size / GiB:g} GiB synthetic object "
+                               f"({per_gpu / GiB:g} GiB per GPU), chunk_size={spec.chunk_size} "
+                               f"(= size/{len(spec.plan)}; BASELINE configs[1] at N=1)",
+                   "object_bytes": size, "chunks": len(spec.plan), "pairs": int(pairs),
+                   "index_dtype": "uint64" if spec.u64 else "uint32",
+                   "parallelism": f"contiguous chunk groups x{world} (scan.objects.fasta_groups), "
+                                  f"{'one rank per GPU (gloo for barriers)' if team.pg is not None else 'one host thread per GPU'}, "
+                                  f"no collective"},
+        "offsets_per_s": round(2.0 * pairs * K / dt, 1),
+        "overlapped": {"value": round(scanned * K / dt_ov / GiB, 3), "unit": "GiB/s",
+                       "ms_per_step": round(dt_ov / K * 1e3, 4),
+                       "note": "same K steps without the device-side wait between consecutive scans (the library "
+                               "still runs one scan grid at a time per GPU)"},
+        "strong": strong_out,
+        "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
+                     "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
+                     "kernel": "scan_kernel<FASTA>", "kernel_avg_us": round(kern * 1e6, 2),
+                     "alg_bytes_per_launch": int(r0["alg_bytes"]),
+                     "measured_peak": round(peak_meas / 1e9, 1),
+                     "frac_of_measured_peak": round(ach / peak_meas, 4),
+                     "note": "per GPU (the slowest GPU's algorithmic bytes / its average scan launch); "
+                             "measured_peak = read-only stream kernel over the same buffer, same run"},
+        "cpu_baseline": cpu,
+        "verified_bit_exact": verified,
+        "gen_s": round(max(r["gen_s"] for r in allres), 2),
+    }
+    print(json.dumps(out), flush=True)
+
+
+# ------------------------------------------------------------------------------------------ CSV / VCF
+def delim_worker(args, team, k, world, dev, keep_host):
+    """configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3] (vcf: ONE
+    64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong scaling): the
+    uint64 newline index (dp_delim_index), device-resident, timed like the FASTA line."""
+    from dataplug_amd import synth
+    from dataplug_amd.dist import rank_byte_range
+    from dataplug_amd.scan import ScanContext
     csv_mode = args.workload == "csv"
     size = args.size or ((32 << 30) if csv_mode else (64 << 30))
     t0 = time.perf_counter()
-    obj = synth.tiled_csv(size, seed=9 + rank) if csv_mode else synth.tiled_vcf(size, seed=9)
-    if csv_mode:
-        begin, end = 0, size
-    else:
-        from dataplug_amd.dist import rank_byte_range
-        begin, end = rank_byte_range(len(obj.head), size, rank, world)   # body [body_offset, size), vcf.py:19-67
+    obj = synth.tiled_csv(size, seed=9 + k) if csv_mode else synth.tiled_vcf(size, seed=9)
+    begin, end = (0, size) if csv_mode else rank_byte_range(len(obj.head), size, k, world)
     nbytes = end - begin
     n_exp = obj.count_range(begin, end)
-    ctx = ScanContext(local)
-    ctx2 = ScanContext(local)
-    d_in = ctx.workspace("bench_in", nbytes + 64)
+    ctxs = (ScanContext(dev), ScanContext(dev))
+    d_in = ctxs[0].workspace("bench_in", nbytes + 64)
     step = 4 << 30                                           # materialize + upload 4 GiB at a time
     stage = np.empty(min(step, nbytes), np.uint8)
     for p in range(begin, end, step):
         q = min(end, p + step)
-        ctx.h2d(d_in.ptr + (p - begin), obj.bytes_range(p, q, out=stage))
-        log(f"uploaded {q - begin} / {nbytes} B")
+        ctxs[0].h2d(d_in.ptr + (p - begin), obj.bytes_range(p, q, out=stage))
     del stage
     gen_s = time.perf_counter() - t0
     cap = n_exp + 1024
-    ctxs = (ctx, ctx2)
-    d_outs = (ctx.workspace("bench_out", 8 * cap), ctx2.workspace("bench_out", 8 * cap))
+    d_outs = (ctxs[0].workspace("bench_out", 8 * cap), ctxs[1].workspace("bench_out", 8 * cap))
 
     def launch(i):
         ctxs[i % 2].delim_index_async(d_in.ptr, nbytes, begin, begin, end, 10, 1, 0, d_outs[i % 2].ptr, True, cap)
@@ -230,51 +544,15 @@ def main_delim(args, world, rank, local, dist):
     def collect(i):
         return ctxs[i % 2].delim_result()
 
-    for i in range(max(2, args.warmup)):
-        launch(i)
-        collect(i)
-
-    def run_steps(serialize: bool):
-        barrier(dist, local)
-        ctx.sync()
-        ctx2.sync()
-        t0 = time.perf_counter()
-        launch(0)
-        for i in range(1, args.steps):
-            if serialize:
-                ctxs[i % 2].wait_for(ctxs[(i - 1) % 2])
-            launch(i)
-            collect(i - 1)
-        res = collect(args.steps - 1)
-        ctx.sync()
-        ctx2.sync()
-        barrier(dist, local)
-        return time.perf_counter() - t0, res
-
-    for c in ctxs:
-        c.timing(True)
-        c.timing_read()
-    dt_ser, _ = run_steps(serialize=True)
-    kern_ms, launches = 0.0, 0
-    for c in ctxs:
-        ms, n = c.timing_read()
-        c.timing(False)
-        kern_ms += ms
-        launches += n
-    dt, (n_out, _) = run_steps(serialize=False)
-    d_out = d_outs[(args.steps - 1) % 2]
-    log(f"timed {args.steps} steps: {dt:.3f} s, {n_out} offsets")
-
-    dt_max = max_over_ranks(dist, local, dt)
-    dt_ser_max = max_over_ranks(dist, local, dt_ser)
-    total_bytes = sum_over_ranks(dist, local, float(nbytes) * args.steps)
-    total_offsets = sum_over_ranks(dist, local, float(n_out) * args.steps)
-    kern_avg_max = max_over_ranks(dist, local, kern_ms / 1e3 / max(1, launches))
-
+    S = Steps(team, ctxs, launch, collect)
+    S.warm(args.warmup)
+    dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
+    dt, _, (n_out, _) = S.timed(args.steps)
+    dt_ov, _, _ = S.timed(args.steps, serialize=False)
     verified = None
     if not args.no_verify:
         # every offset, against the object's analytic newline positions (synth.TiledText)
-        got = ctx.d2h(np.empty(n_out, np.uint64), d_out.ptr)
+        got = ctxs[0].d2h(np.empty(n_out, np.uint64), d_outs[(args.steps - 1) % 2].ptr)
         ok, i = n_out == n_exp, 0
         for piece in obj.delims_range(begin, end):
             if not ok:
@@ -283,191 +561,85 @@ def main_delim(args, world, rank, local, dist):
             i += len(piece)
         verified = bool(ok and i == n_out)
         del got
-        verified = bool(sum_over_ranks(dist, local, float(verified)) == world)
+    out = {"dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn), "scanned": nbytes, "offsets": n_out,
+           "alg_bytes": nbytes + 8 * n_out, "verified": verified, "gen_s": gen_s, "size": size,
+           "stream_peak": stream_peak(ctxs[0], d_in.ptr, nbytes)}
+    if keep_host:
+        out["host"] = obj.bytes_range(begin, min(end, begin + (1 << 30)))
+    for c in ctxs:
+        c.close()
+    return out
 
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_delim(obj.bytes_range(begin, min(end, begin + (1 << 30))))
 
-    traffic, traffic_src = load_traffic(args, nbytes)
-    if rank == 0:
-        alg_bytes = nbytes + 8.0 * n_out                # N input bytes read once + one uint64 per newline
-        achieved = alg_bytes / kern_avg_max
-        name = "CSV" if csv_mode else "VCF"
-        cfg = ("'\\n' index (uint64), 32 GiB cities.csv-shaped object per GPU (BASELINE configs[2])" if csv_mode else
-               f"'\\n' index (uint64) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
-               f"(BASELINE configs[3])")
-        if args.size and csv_mode:
-            cfg = cfg.replace("32 GiB", f"{size / GiB:g} GiB")
-        out = {
-            "metric": f"GiB/s scanned (device-resident) + offsets/s, {name} newline index",
-            "value": round(total_bytes / dt_max / GiB, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak" if csv_mode else "strong",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {"workload": cfg, "object_bytes": size, "scanned_bytes_per_gpu": nbytes,
-                       "offsets_per_gpu": int(n_out),
-                       "parallelism": f"independent {'objects' if csv_mode else 'body parts'} x{world}, "
-                                      f"no collective"},
-            "offsets_per_s": round(total_offsets / dt_max, 1),
-            "serialized": {"value": round(total_bytes / dt_ser_max / GiB, 3), "unit": "GiB/s",
-                           "ms_per_step": round(dt_ser_max / args.steps * 1e3, 4),
-                           "note": "same K steps, each scan waiting on the device for the previous one"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
-                         "kernel": "scan_kernel<DELIM>", "kernel_avg_us": round(kern_avg_max * 1e6, 2),
-                         "alg_bytes_per_launch": int(alg_bytes)},
-            "cpu_baseline": cpu,
-            "verified_bit_exact": verified,
-            "gen_s": round(gen_s, 2),
-        }
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+def main_delim(args, world, rank, devs, team):
+    keep = world == 1 and not args.no_cpu_baseline
+    res = run_workers(lambda k, d: delim_worker(args, team, k, world, d, keep), devs, rank * len(devs), team)
+    host = res[0].pop("host", None) if keep else None
+    allres = team.gather(res)
+    if allres is None:
+        return
+    csv_mode = args.workload == "csv"
+    K = args.steps
+    size = allres[0]["size"]
+    dt = max(r["dt"] for r in allres)
+    dt_ov = max(r["dt_overlap"] for r in allres)
+    scanned = sum(r["scanned"] for r in allres)
+    offs = sum(r["offsets"] for r in allres)
+    kern = max(r["kern_s"] for r in allres)
+    ach = min(r["alg_bytes"] / r["kern_s"] for r in allres)
+    peak_meas = min(r["stream_peak"] for r in allres)
+    cpu = cpu_baseline_delim(host) if host is not None else None
+    traffic, traffic_src = load_traffic(args, allres[0]["scanned"], "scan_kernel<1") if world == 1 else (None, None)
+    name = "CSV" if csv_mode else "VCF"
+    cfg = (f"'\\n' index (uint64), {size / GiB:g} GiB cities.csv-shaped object per GPU (BASELINE configs[2])"
+           if csv_mode else
+           f"'\\n' index (uint64) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
+           f"(BASELINE configs[3])")
+    out = {
+        "metric": f"GiB/s scanned (device-resident) + offsets/s, {name} newline index",
+        "value": round(scanned * K / dt / GiB, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / K * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak" if csv_mode else "strong",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": cfg, "object_bytes": size, "scanned_bytes_per_gpu": allres[0]["scanned"],
+                   "offsets_per_gpu": int(allres[0]["offsets"]),
+                   "parallelism": f"independent {'objects' if csv_mode else 'body parts'} x{world}, no collective"},
+        "offsets_per_s": round(offs * K / dt, 1),
+        "overlapped": {"value": round(scanned * K / dt_ov / GiB, 3), "unit": "GiB/s",
+                       "ms_per_step": round(dt_ov / K * 1e3, 4)},
+        "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
+                     "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
+                     "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
+                     "kernel": "scan_kernel<DELIM>", "kernel_avg_us": round(kern * 1e6, 2),
+                     "alg_bytes_per_launch": int(allres[0]["alg_bytes"]),
+                     "measured_peak": round(peak_meas / 1e9, 1),
+                     "frac_of_measured_peak": round(ach / peak_meas, 4)},
+        "cpu_baseline": cpu,
+        "verified_bit_exact": None if args.no_verify else all(r["verified"] for r in allres),
+        "gen_s": round(max(r["gen_s"] for r in allres), 2),
+    }
+    print(json.dumps(out), flush=True)
 
 
 def main():
     args = parse()
-    world, rank, local, dist = init_dist(args)
-    if args.workload != "fasta":
-        return main_delim(args, world, rank, local, dist)
-    if args.size is None:
-        args.size = 4 << 30
-    from dataplug_amd import synth
-    from dataplug_amd.scan import ScanContext
-
-    ctx = ScanContext(local)
-    ctx2 = ScanContext(local)       # second stream + workspace: step k+1 is queued while step k's result is read
-    size = args.size
-    chunk_size = math.ceil(size / args.chunks)
-    plan = [(i * chunk_size, size if chunk_size == size // chunk_size - 1 else (i + 1) * chunk_size)
-            for i in range(size // chunk_size)]
-    chunks = np.ascontiguousarray(np.asarray(plan, np.uint64).reshape(-1))
-
-    # synthetic object for this rank (seeded; repeated non-power-of-two base block), resident in HBM
-    t0 = time.perf_counter()
-    host = synth.tiled_fasta_host(size, seed=1 + rank)
-    gen_s = time.perf_counter() - t0
-    d_in = ctx.workspace("bench_in", size + 64)
-    ctx.h2d(d_in.ptr, host)
-    cap = size // 256 + 1024
-    ctxs = (ctx, ctx2)
-    d_outs = (ctx.workspace("bench_out", 8 * cap), ctx2.workspace("bench_out", 8 * cap))
-
-    def launch(i):
-        ctxs[i % 2].fasta_index_async(d_in.ptr, size, 0, size, chunks, d_outs[i % 2].ptr, False, cap)
-
-    def collect(i):
-        return ctxs[i % 2].fasta_result(len(plan))
-
-    for i in range(max(2, args.warmup)):            # warms both contexts (workspaces, code objects)
-        launch(i)
-        collect(i)
-
-    def run_steps(serialize: bool):
-        """K steps; returns (wall seconds, last result).  Step k + 1 is enqueued on the other context's
-        stream before step k's result is collected, so the host round trip of one step hides behind the
-        next step's scan.  serialize: step k + 1 waits on the device for step k (no kernel overlap)."""
-        barrier(dist, local)
-        ctx.sync()
-        ctx2.sync()
-        t0 = time.perf_counter()
-        launch(0)
-        for i in range(1, args.steps):
-            if serialize:
-                ctxs[i % 2].wait_for(ctxs[(i - 1) % 2])
-            launch(i)
-            collect(i - 1)
-        res = collect(args.steps - 1)
-        ctx.sync()
-        ctx2.sync()
-        barrier(dist, local)
-        return time.perf_counter() - t0, res
-
-    # (1) serialized steps, HIP events on each context's own stream around every scan launch: the scan
-    #     kernel's own duration (roofline.achieved), and the throughput without any kernel overlap
-    for c in ctxs:
-        c.timing(True)
-        c.timing_read()
-    dt_ser, _ = run_steps(serialize=True)
-    kern_ms, launches = 0.0, 0
-    for c in ctxs:
-        ms, n = c.timing_read()
-        c.timing(False)
-        kern_ms += ms
-        launches += n
-    # (2) the K timed steps of `value`: consecutive objects' scans may overlap on the GPU (the next one
-    #     starts on the CUs the previous one's last workgroups leave idle)
-    dt, (n_pairs, pending, cend) = run_steps(serialize=False)
-    d_out = d_outs[(args.steps - 1) % 2]
-
-    dt_max = max_over_ranks(dist, local, dt)
-    dt_ser_max = max_over_ranks(dist, local, dt_ser)
-    total_bytes = sum_over_ranks(dist, local, float(size) * args.steps)
-    total_offsets = sum_over_ranks(dist, local, 2.0 * n_pairs * args.steps)
-    kern_avg_s = kern_ms / 1e3 / max(1, launches)
-    kern_avg_max = max_over_ranks(dist, local, kern_avg_s)
-
-    verified = None
-    if not args.no_verify and rank == 0:
-        from oracle import dpref
-        exp = dpref.fasta_pairs(host, plan)
-        got = np.empty((n_pairs, 2), np.uint32)
-        ctx.d2h(got, d_out.ptr)
-        verified = bool(np.array_equal(got.astype(np.uint64), exp))
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(host, chunk_size)
-
-    traffic, traffic_src = load_traffic(args, size)
-
-    if rank == 0:
-        alg_bytes = size + 8.0 * n_pairs            # N input bytes read once + 8 B per (start, end) pair
-        achieved = alg_bytes / kern_avg_max
-        value = total_bytes / dt_max / GiB
-        out = {
-            "metric": "GiB/s scanned (device-resident) + offsets/s, FASTA index at 1/2/4/8 MI355X",
-            "value": round(value, 3),
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt_max / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic",
-            "config": {"workload": f"FASTA '>' header index, {size / GiB:g} GiB synthetic object per GPU, "
-                                   f"chunk_size=size/{args.chunks} (BASELINE configs[1])",
-                       "object_bytes": size, "chunks": len(plan), "pairs": int(n_pairs),
-                       "parallelism": f"independent objects x{world}, no collective"},
-            "offsets_per_s": round(total_offsets / dt_max, 1),
-            "serialized": {"value": round(total_bytes / dt_ser_max / GiB, 3), "unit": "GiB/s",
-                           "ms_per_step": round(dt_ser_max / args.steps * 1e3, 4),
-                           "note": "same K steps, each scan waiting on the device for the previous one"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                         "traffic": None if traffic is None else int(traffic),
-                         "traffic_source": traffic_src,
-                         "kernel": "scan_kernel<FASTA>", "kernel_avg_us": round(kern_avg_max * 1e6, 2),
-                         "alg_bytes_per_launch": int(alg_bytes)},
-            "cpu_baseline": cpu,
-            "verified_bit_exact": verified,
-            "gen_s": round(gen_s, 2),
-        }
-        print(json.dumps(out), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    world, rank, devs, pg = launch_mode(args)
+    team = Team(len(devs), pg)
+    try:
+        if args.workload == "fasta":
+            main_fasta(args, world, rank, devs, team)
+        else:
+            main_delim(args, world, rank, devs, team)
+    finally:
+        if pg is not None:
+            pg.destroy_process_group()
 
 
 if __name__ == "__main__":

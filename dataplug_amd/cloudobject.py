@@ -16,6 +16,7 @@ from typing import Any, Dict, List, Optional
 
 from .entities import CloudDataFormat, CloudObjectSlice
 from .preprocessing.preprocess import mapreduce_preprocessing, monolithic_preprocessing, use_batch_path
+from .scan.objects import DEVICES_ATTR, parse_devices
 from .storage.client import PickleableS3ClientProxy
 from .storage.errors import ClientError
 from .storage.reader import open_object
@@ -186,15 +187,23 @@ class CloudObject:
             self.storage.create_bucket(Bucket=self.meta_path.bucket)
 
         fmt = self._format_cls
-        if chunk_size is None:
-            monolithic_preprocessing(self, parallel_config, fmt.preprocessing_function, extra_args)
-        else:
-            assert chunk_size != 0 and chunk_size <= self.size, \
-                "Chunk size must be greater than 0 and less or equal to object size"
-            assert fmt.finalizer_function is not None, "Finalizer function must be defined for mapreduce"
-            batch = fmt.batch_function if use_batch_path(fmt, parallel_config) else None
-            mapreduce_preprocessing(self, parallel_config, chunk_size, fmt.preprocessing_function,
-                                    fmt.finalizer_function, extra_args, batch_function=batch)
+        # GPU selection: parallel_config["dataplug_devices"] (or the same key in
+        # extra_args) ahead of DATAPLUG_AMD_DEVICES; it travels with the object to joblib workers
+        devs = parse_devices(parallel_config.get("dataplug_devices", extra_args.get("dataplug_devices")))
+        prev = getattr(self, DEVICES_ATTR, None)
+        setattr(self, DEVICES_ATTR, devs)
+        try:
+            if chunk_size is None:
+                monolithic_preprocessing(self, parallel_config, fmt.preprocessing_function, extra_args)
+            else:
+                assert chunk_size != 0 and chunk_size <= self.size, \
+                    "Chunk size must be greater than 0 and less or equal to object size"
+                assert fmt.finalizer_function is not None, "Finalizer function must be defined for mapreduce"
+                batch = fmt.batch_function if use_batch_path(fmt, parallel_config) else None
+                mapreduce_preprocessing(self, parallel_config, chunk_size, fmt.preprocessing_function,
+                                        fmt.finalizer_function, extra_args, batch_function=batch)
+        finally:
+            setattr(self, DEVICES_ATTR, prev)
         self._meta_headers = None
         self.fetch()
 

@@ -33,6 +33,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1450,6 +1451,19 @@ int fail(int code, const std::string& msg) {
 
 }  // namespace
 
+// One persistent scan grid at a time per device.  The look-back assumes every workgroup of a grid is
+// resident; two grids launched at the same moment from different streams (one process indexing several
+// objects or chunk groups on one GPU, e.g. DATAPLUG_AMD_DEVICES=0,0,0) could split the CUs between them and
+// wait on each other's unscheduled workgroups.  So a scan launch on a ctx stream first waits (on the device,
+// no host sync) for the last scan launched on that device from any other stream.
+struct DeviceSerial {
+  std::mutex m;
+  hipEvent_t last = nullptr;          // completion of the device's last scan (owned by that ctx)
+  hipStream_t last_stream = nullptr;
+};
+constexpr int kMaxDevices = 64;
+DeviceSerial g_serial[kMaxDevices];
+
 struct dp_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
@@ -1475,6 +1489,7 @@ struct dp_ctx {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_order = nullptr;      // dp_ctx_wait: device-scope ordering event on this ctx's stream
+  hipEvent_t ev_scan = nullptr;       // end of this ctx's last scan launch (DeviceSerial)
   size_t ev_used = 0;
   double ms_acc = 0.0;
   uint64_t launches = 0;
@@ -1614,6 +1629,10 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   }
   a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
   const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
+  DeviceSerial& ds = g_serial[c->device];
+  std::lock_guard<std::mutex> lock(ds.m);
+  if (ds.last && ds.last_stream != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, ds.last, 0));
+  if (!c->ev_scan) HIPCHK(hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming | hipEventReleaseToDevice));
   hipEvent_t e0;
   rc = ev_begin(c, &e0);
   if (rc) return rc;
@@ -1629,7 +1648,12 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   else
     hipLaunchKernelGGL((scan_kernel<kDelim, 1>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   HIPCHK(hipGetLastError());
-  return ev_end(c);
+  rc = ev_end(c);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(c->ev_scan, c->stream));
+  ds.last = c->ev_scan;
+  ds.last_stream = c->stream;
+  return DP_OK;
 }
 
 int check_ctx(dp_ctx* c) {
@@ -1667,7 +1691,8 @@ int dp_ctx_create(int device, dp_ctx** out) {
   if (!out) return fail(DP_ERR_INVALID, "null out");
   int n = 0;
   HIPCHK(hipGetDeviceCount(&n));
-  if (device < 0 || device >= n) return fail(DP_ERR_INVALID, "device " + std::to_string(device) + " out of range");
+  if (device < 0 || device >= n || device >= kMaxDevices)
+    return fail(DP_ERR_INVALID, "device " + std::to_string(device) + " out of range");
   HIPCHK(hipSetDevice(device));
   dp_ctx* c = new dp_ctx();
   c->device = device;
@@ -1709,6 +1734,14 @@ int dp_ctx_destroy(dp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+  if (c->ev_scan) {
+    std::lock_guard<std::mutex> lock(g_serial[c->device].m);
+    if (g_serial[c->device].last == c->ev_scan) {
+      g_serial[c->device].last = nullptr;
+      g_serial[c->device].last_stream = nullptr;
+    }
+    (void)hipEventDestroy(c->ev_scan);
+  }
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->h_tab) (void)hipHostFree(c->h_tab);

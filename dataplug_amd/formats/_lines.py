@@ -100,8 +100,10 @@ class LineIndex:
         return i < self.count and self.value(i) == x
 
 
-class SliceError(Exception):
-    """The reference's ``get()`` fails for this slice (kept as an error, not papered over)."""
+class SliceError(ValueError):
+    """The reference's ``get()`` fails for this slice (kept as an error, not papered over).  A ``ValueError``:
+    what the reference raises there (the negative ``seek`` of csv.py:75; its VCF range expansion past the end
+    of the object fails inside the storage client instead)."""
 
 
 def csv_body(lines: LineIndex, size: int, r0: int, r1: int, chunk_id: int, num_chunks: int,

@@ -55,8 +55,10 @@ def mapreduce_preprocessing(cloud_object, parallel_config, chunk_size, preproces
         raise Exception("Preprocessing function must have (chunk_data, chunk_id, chunk_size, num_chunks) as parameters")
     num_chunks = cloud_object.size // chunk_size
     extras = {}
-    for a in sig:
+    for a, prm in sig.items():
         if a not in ("cloud_object", "chunk_id", "chunk_size", "num_chunks", "chunk_data"):
+            if a not in extra_args and prm.default is not inspect.Parameter.empty:
+                continue                     # optional plugin keyword (e.g. FASTA index_dtype): its default
             extras[a] = extra_args[a]        # KeyError like the reference when an extra arg is missing
 
     if batch_function is not None:

@@ -9,22 +9,49 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
 from ._lib import DPScanUnavailable
 from ..dist import split_groups
+from ..storage.ranges import GET_PART as _GET_PART, GET_THREADS as _GET_THREADS, read_range_into
 from .device import ScanContext, device_count, get_context
 
-_GET_PART = 32 << 20          # ranged-GET part size for parallel fetches
-_GET_THREADS = 16
 _HALO0 = 64 << 10             # first look-ahead window when a header line crosses the fetched bytes
 
 
-def devices(max_devices: Optional[int] = None) -> List[int]:
+DEVICES_ATTR = "_dataplug_devices"
+
+
+def parse_devices(spec) -> Optional[List[int]]:
+    """A device list from ``parallel_config["dataplug_devices"]`` / ``extra_args["dataplug_devices"]``
+    (an int count, a list of ordinals, or a "0,1,..." string); None if unset.  Repeating an ordinal runs
+    several groups on one GPU (how the multi-GPU split is rehearsed on a 1-GPU box)."""
+    if spec is None:
+        return None
+    if isinstance(spec, str):
+        devs = [int(x) for x in spec.split(",") if x.strip()]
+    elif isinstance(spec, int) and not isinstance(spec, bool):
+        if spec <= 0:
+            raise ValueError(f"dataplug_devices={spec}: need at least one GPU")
+        devs = list(range(spec))
+    else:
+        devs = [int(x) for x in spec]
+    if not devs or any(d < 0 for d in devs):
+        raise ValueError(f"dataplug_devices={spec!r}: expected a non-empty list of GPU ordinals")
+    return devs
+
+
+def devices(max_devices: Optional[int] = None, co=None) -> List[int]:
+    """GPUs an index build runs on: the object's ``dataplug_devices`` (set by ``co.preprocess`` from its
+    ``parallel_config`` / ``extra_args``), else ``DATAPLUG_AMD_DEVICES``, else every visible GPU."""
     env = os.environ.get("DATAPLUG_AMD_DEVICES")
-    if env:
+    own = getattr(co, DEVICES_ATTR, None) if co is not None else None
+    if own:
+        devs = list(own)
+    elif env:
         devs = [int(x) for x in env.split(",") if x.strip()]
     else:
         n = device_count()
@@ -35,34 +62,6 @@ def devices(max_devices: Optional[int] = None) -> List[int]:
 
 
 # ------------------------------------------------------------------------------------------ storage → host
-def read_range_into(storage, bucket: str, key: str, lo: int, hi: int, out: memoryview,
-                    part: int = _GET_PART, threads: int = _GET_THREADS) -> None:
-    """Object bytes [lo, hi) into ``out`` (len >= hi - lo) with parallel ranged GETs (inclusive Range)."""
-    n = hi - lo
-    if n <= 0:
-        return
-    out = out.cast("B") if out.format != "B" else out
-
-    def one(a: int) -> None:
-        b = min(n, a + part)
-        res = storage.get_object(Bucket=bucket, Key=key, Range=f"bytes={lo + a}-{lo + b - 1}")
-        body = res["Body"]
-        got = a
-        with body:
-            while got < b:
-                r = body.readinto(out[got:b])
-                if not r:
-                    raise IOError(f"short read of {bucket}/{key} at {lo + got}")
-                got += r
-
-    starts = list(range(0, n, part))
-    if len(starts) == 1:
-        one(0)
-        return
-    with cf.ThreadPoolExecutor(min(threads, len(starts))) as ex:
-        list(ex.map(one, starts))
-
-
 def fetch_to_device(ctx: ScanContext, storage, bucket: str, key: str, lo: int, hi: int, d_ptr: int,
                     part: Optional[int] = None, threads: int = _GET_THREADS):
     """Object bytes [lo, hi) into device memory at ``d_ptr``: parallel ranged GETs into the context's pinned
@@ -114,18 +113,46 @@ def resolve_line_end(ctx: ScanContext, storage, bucket: str, key: str, size: int
 
 
 # ------------------------------------------------------------------------------------------ FASTA
-def _fasta_group(dev: int, co, plan: Sequence[Tuple[int, int]], u64: bool) -> np.ndarray:
+@dataclass(frozen=True)
+class FastaGroup:
+    """One GPU's share of a FASTA chunk plan: chunks [i0, i1) of the plan (contiguous, so the outputs
+    concatenate in chunk order like merge_fasta_metadata, fasta.py:66-74), the bytes they scan [lo, hi),
+    and the bytes fetched into HBM [lo, buf_hi): ``hi`` plus a look-ahead halo, so a header line cut by the
+    group's last chunk usually ends inside the same launch (resolve kernel) instead of a later GET."""
+    i0: int
+    i1: int
+    lo: int
+    hi: int
+    buf_hi: int
+
+    def chunks(self, plan: Sequence[Tuple[int, int]]) -> List[Tuple[int, int]]:
+        return list(plan[self.i0:self.i1])
+
+
+def fasta_groups(plan: Sequence[Tuple[int, int]], n_groups: int, size: int, halo: int = _HALO0) -> List[FastaGroup]:
+    """The multi-GPU split of one object's chunk plan (the reference runs the chunks as
+    independent map jobs, preprocess.py:39-51): ``split_groups`` of the chunk list over ``n_groups`` GPUs.
+    Used by ``fasta_index_object`` and by bench.py's multi-GPU line (one thread or rank per group)."""
+    out = []
+    for i0, i1 in split_groups(len(plan), n_groups):
+        if i1 <= i0:
+            continue
+        lo = min(c0 for c0, _ in plan[i0:i1])
+        hi = max(c1 for _, c1 in plan[i0:i1])
+        out.append(FastaGroup(i0, i1, lo, hi, min(size, hi + halo)))
+    return out
+
+
+def _fasta_group(dev: int, co, plan: Sequence[Tuple[int, int]], g: FastaGroup, u64: bool) -> np.ndarray:
     ctx = get_context(dev)
     size = co.size
-    lo = min(c0 for c0, _ in plan)
-    hi = max(c1 for _, c1 in plan)
-    n = hi - lo
+    n = g.buf_hi - g.lo
     d = ctx.workspace("input", n + 64)
-    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, d.ptr)
-    pairs, pending, _ = ctx.fasta_index(d.ptr, n, lo, size, plan, u64=u64)
+    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, g.lo, g.buf_hi, d.ptr)
+    pairs, pending, _ = ctx.fasta_index(d.ptr, n, g.lo, size, g.chunks(plan), u64=u64)
     for p in pending[pending >= 0]:
         start = int(pairs[p, 0])
-        end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, size, hi)
+        end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, size, g.buf_hi)
         if not u64 and end > 0xFFFFFFFF:
             raise OverflowError(f"FASTA offset {end} does not fit the uint32 index (header at {start})")
         pairs[p, 1] = end
@@ -138,12 +165,12 @@ def fasta_index_object(co, plan: Sequence[Tuple[int, int]], u64: bool = False,
     ``merge_fasta_metadata`` (fasta.py:66-74) assembles from the per-chunk map outputs."""
     if not plan:
         return np.zeros((0, 2), np.uint64 if u64 else np.uint32)
-    devs = devices(max_devices)
-    groups = split_groups(len(plan), len(devs))
+    devs = devices(max_devices, co)
+    groups = fasta_groups(plan, len(devs), co.size)
     if len(groups) == 1:
-        return _fasta_group(devs[0], co, plan, u64)
+        return _fasta_group(devs[0], co, plan, groups[0], u64)
     with cf.ThreadPoolExecutor(len(groups)) as ex:
-        futs = [ex.submit(_fasta_group, devs[k], co, plan[i0:i1], u64) for k, (i0, i1) in enumerate(groups)]
+        futs = [ex.submit(_fasta_group, devs[k], co, plan, g, u64) for k, g in enumerate(groups)]
         parts = [f.result() for f in futs]
     return np.concatenate(parts)
 
@@ -151,7 +178,7 @@ def fasta_index_object(co, plan: Sequence[Tuple[int, int]], u64: bool = False,
 def fasta_index_chunk(co, data, chunk_offset: int, job: int = 0, u64: bool = False) -> np.ndarray:
     """Pairs of one map chunk whose bytes ``data`` the caller already holds (the per-chunk plugin call),
     scanned on GPU ``job % n_gpus``."""
-    devs = devices()
+    devs = devices(co=co)
     ctx = get_context(devs[job % len(devs)])
     n = len(data)
     pairs, pending, _ = ctx.fasta_index_host(data, chunk_offset, co.size, [(chunk_offset, chunk_offset + n)], u64=u64)
@@ -181,7 +208,7 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
     end = co.size if end is None else end
     if end <= begin:
         return np.zeros(0, np.uint64)
-    devs = devices(max_devices)
+    devs = devices(max_devices, co)
     nparts = max(len(devs), -(-(end - begin) // part_bytes))
     step = -(-(end - begin) // nparts)
     bounds = [(begin + i * step, min(end, begin + (i + 1) * step)) for i in range(nparts)]

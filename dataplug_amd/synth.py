@@ -180,6 +180,41 @@ def tiled_fasta_host(size: int, seed: int = 0, block: int = 64 * 2**20 - 4099) -
     return out
 
 
+class TiledFasta:
+    """``tiled_fasta_host(size, seed)`` without materializing it: any byte range on demand.
+
+    The multi-GPU benchmark indexes ONE object of N x 4 GiB whose chunk groups live on different GPUs; each
+    worker builds only the bytes of its own group (plus the look-ahead halo).  ``bytes_range(0, size)``
+    equals ``tiled_fasta_host(size, seed)`` byte for byte (tests/test_synth_tiled.py)."""
+
+    def __init__(self, size: int, seed: int = 0, block: int = 64 * 2**20 - 4099):
+        self.size = int(size)
+        self.base = fasta(min(block, self.size), seed)
+        # the object-level tail fix of _fix_fasta_tail: bytes after the object's last '\n'
+        t0 = max(0, self.size - (1 << 20))
+        tail = self._raw(t0, self.size)
+        nls = np.flatnonzero(tail == 10)
+        self.tail0 = t0 + int(nls[-1]) + 1 if len(nls) else 0
+        self.tail_fix = self.tail0 < self.size and bool((tail[self.tail0 - t0:] == ord(">")).any())
+
+    def _raw(self, start: int, end: int, out: np.ndarray | None = None) -> np.ndarray:
+        out = np.empty(end - start, np.uint8) if out is None else out[: end - start]
+        bl = len(self.base)
+        p = start
+        while p < end:
+            q = p % bl
+            n = min(bl - q, end - p)
+            out[p - start:p - start + n] = self.base[q:q + n]
+            p += n
+        return out
+
+    def bytes_range(self, start: int, end: int, out: np.ndarray | None = None) -> np.ndarray:
+        out = self._raw(start, end, out)
+        if self.tail_fix and end > self.tail0:
+            out[max(self.tail0, start) - start:] = ord("N")
+        return out
+
+
 def tiled_host(base: np.ndarray, size: int) -> np.ndarray:
     """``size`` bytes made of repeated copies of ``base`` (the last copy truncated)."""
     out = np.empty(size, np.uint8)

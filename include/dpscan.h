@@ -6,7 +6,9 @@
  * the message of the last failure on the calling thread is available from dp_last_error().  No C++
  * exception crosses this boundary.  A dp_ctx is bound to one device and owns one stream plus the
  * scan workspace; use one ctx per host thread (calls on distinct ctx are thread-safe, and ctypes
- * releases the GIL around them).
+ * releases the GIL around them).  Scan kernels of different ctx on one device run one after another
+ * (each launch waits on the device for the previous one): the persistent scan grid needs every one
+ * of its workgroups resident.
  *
  * Reference interfaces each entry point replaces (CLOUDLAB-URV/dataplug @ 2025-07-11):
  *   dp_fasta_index  <- dataplug/formats/genomics/fasta.py:24-63 (preprocess_fasta: the per-chunk

@@ -1,6 +1,6 @@
-"""N>1 path on CPU: two ranks over gloo (127.0.0.1).  Ranks get disjoint contiguous chunk groups that
-cover the plan, the per-rank outputs concatenated in rank order equal the single-process index, and the
-bench's barrier / max / sum reductions behave."""
+"""N>1 path on CPU: two ranks over gloo (127.0.0.1), driven through bench.py's own Team / FastaSpec.  Ranks
+get disjoint contiguous chunk groups of one object from the product split (scan.objects.fasta_groups), the
+per-rank outputs gathered in rank order equal the single-process index."""
 import os
 import socket
 import subprocess
@@ -9,7 +9,7 @@ import textwrap
 
 import numpy as np
 
-from dataplug_amd.dist import rank_byte_range, rank_chunks, split_groups
+from dataplug_amd.dist import rank_byte_range, split_groups
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -22,7 +22,7 @@ def test_split_groups_cover_and_disjoint():
             assert flat == list(range(n))
             sizes = [b - a for a, b in gr]
             assert max(sizes) - min(sizes) <= 1
-    assert rank_chunks(2, 3, 4) == (2, 2)
+    assert split_groups(2, 4) == [(0, 1), (1, 2)]
 
 
 def test_rank_byte_ranges_concatenate_to_whole_index():
@@ -54,33 +54,44 @@ WORKER = textwrap.dedent("""
     import json, os, sys
     import numpy as np
     sys.path.insert(0, {repo!r})
-    from dataplug_amd.dist import Dist, rank_byte_range, rank_chunks
+    import torch.distributed as dist
+    import bench
+    from oracle import dpref
+    from dataplug_amd.dist import rank_byte_range
     from dataplug_amd import synth
-    from oracle import cpu_ref
-    d = Dist.from_env(backend="gloo")
-    data = bytes(synth.fasta(1 << 20, 3))
-    plan = cpu_ref.chunk_plan(len(data), (1 << 20) // 7)
-    i0, i1 = rank_chunks(len(plan), d.rank, d.world)
-    mine = [cpu_ref.fasta_chunk_pairs(data, c0, c1) for c0, c1 in plan[i0:i1]]
-    d.barrier()
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    team = bench.Team(1, dist)                      # what bench.py builds under torch.distributed.run
+    # bench.py's FASTA workload: one object, chunk plan size/(4N), the product's group split
+    # (scan.objects.fasta_groups); this rank materializes only its group + halo, as a bench rank does
+    spec = bench.FastaSpec({size}, 4 * world, world, seed=3)
+    g = spec.groups[rank]
+    host = spec.obj.bytes_range(g.lo, g.buf_hi)
+    rel = [(c0 - g.lo, c1 - g.lo) for c0, c1 in g.chunks(spec.plan)]
+    # the GPU scan of the group stands in as the oracle over the same bytes (no GPU here)
+    mine = (dpref.fasta_pairs(host, rel) + np.uint64(g.lo)).tolist()
+    team.barrier()
     tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
-    lo, hi = rank_byte_range(len(tv.head), tv.size, d.rank, d.world)
+    lo, hi = rank_byte_range(len(tv.head), tv.size, rank, world)
     nl = np.concatenate(list(tv.delims_range(lo, hi))).tolist()
-    mx = d.max(float(d.rank + 1))
-    sm = d.sum(float(sum(len(m) for m in mine)))
-    out = {{"rank": d.rank, "range": [i0, i1], "pairs": [p for m in mine for p in m], "max": mx, "sum": sm, "nl": nl}}
-    with open(os.path.join({tmp!r}, f"r{{d.rank}}.json"), "w") as f:
-        json.dump(out, f)
-    d.close()
+    allres = team.gather([{{"rank": rank, "group": [g.i0, g.i1, g.lo, g.hi, g.buf_hi], "pairs": mine, "nl": nl}}])
+    if allres is not None:
+        with open(os.path.join({tmp!r}, "gathered.json"), "w") as f:
+            json.dump(allres, f)
+    dist.destroy_process_group()
 """)
 
 
 def test_two_rank_gloo(tmp_path):
+    """Two ranks over gloo, as bench.py runs under torch.distributed.run: each takes its chunk group of ONE
+    object from the product's split, the gather reaches rank 0 in rank order, and the groups' pairs
+    concatenate to the whole object's index."""
     import json
-    from oracle import cpu_ref
+    from oracle import cpu_ref, dpref
     from dataplug_amd import synth
+    size = (3 << 20) + 12345
     script = tmp_path / "w.py"
-    script.write_text(WORKER.format(repo=REPO, tmp=str(tmp_path)))
+    script.write_text(WORKER.format(repo=REPO, tmp=str(tmp_path), size=size))
     port = _free_port()
     procs = []
     for r in range(2):
@@ -89,14 +100,14 @@ def test_two_rank_gloo(tmp_path):
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, cwd=REPO))
     for p in procs:
         assert p.wait(timeout=240) == 0
-    res = [json.load(open(tmp_path / f"r{r}.json")) for r in range(2)]
-    data = bytes(synth.fasta(1 << 20, 3))
-    idx, n = cpu_ref.fasta_index(data, (1 << 20) // 7)
-    whole = np.frombuffer(idx, np.uint32).reshape(-1, 2).tolist()
-    assert res[0]["range"][1] == res[1]["range"][0] and res[1]["range"][1] == 7
+    res = json.load(open(tmp_path / "gathered.json"))
+    assert [r["rank"] for r in res] == [0, 1]
+    g0, g1 = res[0]["group"], res[1]["group"]
+    obj = synth.TiledFasta(size, seed=3).bytes_range(0, size)
+    plan = cpu_ref.chunk_plan(size, -(-size // 8))         # 7 chunks: the tail past 7 * cs is never scanned
+    assert g0[0] == 0 and g0[1] == g1[0] and g1[1] == len(plan) and g0[3] == g1[2]
+    whole = dpref.fasta_pairs(obj, plan).tolist()
     assert res[0]["pairs"] + res[1]["pairs"] == whole
-    assert res[0]["max"] == res[1]["max"] == 2.0
-    assert res[0]["sum"] == res[1]["sum"] == float(n)
     tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
     body_nl = cpu_ref.delim_index(tv.bytes_range(0, tv.size), len(tv.head), tv.size).tolist()
     assert res[0]["nl"] + res[1]["nl"] == body_nl

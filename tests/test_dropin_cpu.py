@@ -137,3 +137,135 @@ def test_open_split_header_readline(server, sample):
         f.seek(236)
         line = f.readline()
         assert line.startswith(b">") and f.tell() == 296
+
+
+# ------------------------------------------------------------------------------------------ device selection
+@pytest.mark.parametrize("where", ["parallel_config", "extra_args"])
+def test_device_keyword_ahead_of_env(server, sample, monkeypatch, where):
+    """co.preprocess(parallel_config={"dataplug_devices": [...]}) (or the same key in extra_args) picks the
+    GPUs ahead of DATAPLUG_AMD_DEVICES, for this call only."""
+    data, exp = sample
+    seen = []
+
+    def fasta_index_object(co, plan, u64=False, max_devices=None):
+        seen.append(scan_objects.devices(max_devices, co))
+        return exp
+
+    monkeypatch.setattr(scan_objects, "fasta_index_object", fasta_index_object)
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "5,6")
+    co = _upload(server, data, f"dev_{where}.fasta")
+    kw = {where: {"dataplug_devices": [0, 0, 1]}}
+    co.preprocess(chunk_size=534, **kw)
+    co.preprocess(chunk_size=534, force=True, **{where: {"dataplug_devices": "2"}})
+    co.preprocess(chunk_size=534, force=True, **{where: {"dataplug_devices": 3}})
+    co.preprocess(chunk_size=534, force=True)
+    assert seen == [[0, 0, 1], [2], [0, 1, 2], [5, 6]]
+    assert getattr(co, scan_objects.DEVICES_ATTR) is None
+    with pytest.raises(ValueError):
+        co.preprocess(chunk_size=534, force=True, **{where: {"dataplug_devices": []}})
+
+
+def test_device_keyword_reaches_joblib_map_jobs(server, sample, monkeypatch):
+    data, exp = sample
+    seen = []
+
+    def fasta_index_chunk(co, data, chunk_offset, job=0, u64=False):
+        seen.append(tuple(scan_objects.devices(co=co)))
+        return exp[(exp[:, 0] >= chunk_offset) & (exp[:, 0] < chunk_offset + len(data))]
+
+    monkeypatch.setattr(scan_objects, "fasta_index_chunk", fasta_index_chunk)
+    co = _upload(server, data, "dev_joblib.fasta")
+    co.preprocess(chunk_size=534, parallel_config={"backend": "threading", "n_jobs": 2, "dataplug_devices": [1, 0]})
+    assert seen and set(seen) == {(1, 0)}
+    idx = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read(),
+                        np.uint32)
+    assert np.array_equal(idx, exp.reshape(-1))
+
+
+# ------------------------------------------------------------------------------------------ uint64 index
+@pytest.mark.parametrize("parallel_config", [{}, {"backend": "threading", "n_jobs": 2}])
+def test_uint64_index_opt_in(server, sample, stub_scan, parallel_config):
+    """extra_args={"index_dtype": "uint64"}: same pairs as 8-byte words, attributes say so, and
+    partition_chunks_strategy reads it back into the same slices as the uint32 index."""
+    data, exp = sample
+    co32 = _upload(server, data, "u32.fasta")
+    co32.preprocess(chunk_size=534, parallel_config=parallel_config)
+    co64 = _upload(server, data, "u64.fasta")
+    co64.preprocess(chunk_size=534, parallel_config=parallel_config, extra_args={"index_dtype": "uint64"})
+    assert co64.attributes.index_dtype == "uint64" and co64.attributes.num_sequences == 9
+    assert not hasattr(co32.attributes, "index_dtype")          # the reference's attributes, unchanged
+    raw = co64.storage.get_object(Bucket=co64.meta_path.bucket, Key=co64.meta_path.key)["Body"].read()
+    assert np.array_equal(np.frombuffer(raw, "<u8").reshape(-1, 2), exp)
+    for n in (1, 3, 8):
+        s32 = co32.partition(ffa.partition_chunks_strategy, num_chunks=n)
+        s64 = co64.partition(ffa.partition_chunks_strategy, num_chunks=n)
+        assert [(s.offset, s.header, s.range_0, s.range_1) for s in s32] == \
+            [(s.offset, s.header, s.range_0, s.range_1) for s in s64]
+    with pytest.raises(ValueError):
+        co64.preprocess(chunk_size=534, force=True, extra_args={"index_dtype": "int8"})
+
+
+# ------------------------------------------------------------------------------------------ bulk slice gets
+def _counting(storage):
+    calls = []
+    orig = storage.get_object
+
+    def get_object(**kw):
+        calls.append(kw.get("Range"))
+        return orig(**kw)
+
+    storage.get_object = get_object
+    return calls
+
+
+def test_fasta_get_slices_batched_over_http(server, fasta_cases):
+    """get_slices on FASTA slices over the loopback HTTP server: the reference's get() outputs (golden,
+    made by running the reference) from a few coalesced ranged GETs instead of 1-2 per slice."""
+    import base64
+    import json
+    from dataplug_amd.entities import get_slices
+    from dataplug_amd.preprocessing.handler import upload_metadata
+    from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
+    from dataplug_amd import synth
+    from oracle import cpu_ref
+    recs = json.load(open(os.path.join(GOLDEN, "fasta_slices.json")))
+    z = fasta_cases
+    i = list(z["kind"]).index("sample")
+    objs = {"sample": bytes(z["data"][z["data_off"][i]:z["data_off"][i + 1]]),
+            "synth1": bytes(synth.fasta(1 << 18, 11))}
+    checked = 0
+    for rec in recs:
+        data = objs[rec["object"]]
+        co = _upload(server, data, f"slices_{rec['object']}.fasta")
+        idx, nseq = cpu_ref.fasta_index(data, rec["chunk_size"])
+        upload_metadata(co, PreprocessingMetadata(metadata=idx, attributes={"num_sequences": nseq}))
+        co.fetch()
+        slices = co.partition(ffa.partition_chunks_strategy, num_chunks=rec["num_chunks"])
+        calls = _counting(co.storage)
+        got = get_slices(slices, threads=4)
+        n_batched = len(calls)
+        if "get" in rec:
+            assert [base64.b64encode(g).decode() for g in got] == rec["get"]
+        calls.clear()
+        assert [s.get() for s in slices] == got
+        assert n_batched <= 2 and len(calls) >= len(slices)
+        checked += 1
+    assert checked == len(recs)
+
+
+def test_get_slices_first_error_in_slice_order():
+    from dataplug_amd.entities import CloudObjectSlice, get_slices
+
+    class S(CloudObjectSlice):
+        def __init__(self, i):
+            super().__init__(i, i + 1)
+            self.i = i
+
+        def get(self):
+            if self.i in (3, 7):
+                raise ValueError(f"slice {self.i}")
+            return self.i
+
+    assert get_slices([S(i) for i in (0, 1, 2)], threads=4) == [0, 1, 2]
+    with pytest.raises(ValueError, match="slice 3"):
+        get_slices([S(i) for i in range(10)], threads=4)

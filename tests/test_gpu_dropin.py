@@ -5,7 +5,9 @@ sizes (oracle), the per-chunk joblib route, multi-group splits (DATAPLUG_AMD_DEV
 multi-GPU grouping on one GPU), and a header line crossing a group boundary (pending-end resolution).
 CSV/VCF: the GPU newline index equals the bytes' '\\n' positions and the partitions equal the reference's
 get() outputs.  FASTQ.gz: total_lines and per-read ends on the inflated stream, read batches' lines."""
+import base64
 import gzip
+import builtins
 import json
 import os
 
@@ -14,6 +16,7 @@ import pytest
 
 from dataplug_amd import synth
 from dataplug_amd.cloudobject import CloudObject
+from dataplug_amd.entities import get_slices
 from dataplug_amd.storage import LoopbackS3Server, MemoryStore
 
 pytestmark = pytest.mark.gpu
@@ -63,6 +66,8 @@ def test_fasta_sample_over_loopback(server, fasta_cases, parallel_config):
         sl = co.partition(partition_chunks_strategy, num_chunks=rec["num_chunks"])
         assert [[s.offset, None if s.header is None else list(s.header), s.range_0, s.range_1] for s in sl] == \
             rec["slices"]
+        if "get" in rec:          # the reference's get() outputs, materialized by the batched get_slices
+            assert [base64.b64encode(b).decode() for b in get_slices(sl)] == rec["get"]
 
 
 def test_fasta_golden_cases_batch_and_per_chunk(fasta_cases):
@@ -168,8 +173,9 @@ def test_csv_line_index_and_partitions(monkeypatch, devices):
         for n, expected in rec["num_chunks"].items():
             for s, e in zip(co.partition(fcsv.partition_num_chunks, num_chunks=int(n)), expected):
                 if isinstance(e[2], dict):
-                    with pytest.raises(SliceError):
+                    with pytest.raises(getattr(builtins, e[2]["error"])) as ei:   # the reference's class
                         s.get()
+                    assert isinstance(ei.value, SliceError)
                 else:
                     assert s.get() == e[2]
 
@@ -221,3 +227,54 @@ def test_fastq_gz_reads():
     batches = co.partition(partition_reads_batches, num_batches=7)
     got = [ln for b in batches for ln in b.get()]
     assert got == [x.decode() for x in lines]
+
+
+# ------------------------------------------------------------------------------------------ multi-GPU split
+def test_bench_thread_mode_split_on_one_gpu(tmp_path):
+    """bench.py --gpus 4 --devices 0,0,0,0: the multi-GPU line's own code (one host thread per GPU, the
+    product's chunk-group split of ONE object, per-group halo) rehearsed on one GPU; every group's index is
+    bit-exact against the oracle (verified_bit_exact) and the strong-scaling point too."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--devices", "0,0,0,0",
+           "--size", str((48 << 20) + 4099), "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 4 and line["verified_bit_exact"] is True
+    assert line["config"]["chunks"] == 16 and line["config"]["index_dtype"] == "uint32"
+    assert line["strong"]["verified_bit_exact"] is True and line["strong"]["gpus_used"] == 4
+    assert line["ms_per_step"] * 1e3 >= line["roofline"]["kernel_avg_us"]
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    import subprocess
+    import sys
+    from dataplug_amd.scan import device_count
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n = device_count() + 1
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(n), "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, cwd=repo)
+    assert r.returncode != 0 and "visible" in r.stderr
+
+
+@pytest.mark.parametrize("u64", [False, True])
+def test_device_keyword_and_uint64_index(u64):
+    """parallel_config={"dataplug_devices": [0, 0, 0]} runs the three-group split on the GPU box; with
+    extra_args={"index_dtype": "uint64"} the stored index is the same pairs as 8-byte words."""
+    from oracle import cpu_ref, dpref
+    from dataplug_amd.formats.genomics.fasta import FASTA, partition_chunks_strategy
+    from dataplug_amd.entities import get_slices
+    data = synth.fasta((20 << 20) + 123, 55)
+    co = _co(FASTA, data.tobytes(), f"devkw{u64}", _mem(f"gpu_devkw_{u64}"))
+    cs = -(-len(data) // 9)
+    co.preprocess(chunk_size=cs, parallel_config={"dataplug_devices": [0, 0, 0]},
+                  extra_args={"index_dtype": "uint64"} if u64 else None)
+    exp = dpref.fasta_pairs(data, cpu_ref.chunk_plan(len(data), cs))
+    raw = co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read()
+    got = np.frombuffer(raw, "<u8" if u64 else "<u4").reshape(-1, 2)
+    assert np.array_equal(got.astype(np.uint64), exp)
+    assert getattr(co.attributes, "index_dtype", "uint32") == ("uint64" if u64 else "uint32")
+    slices = co.partition(partition_chunks_strategy, num_chunks=7)
+    assert get_slices(slices) == [s.get() for s in slices]

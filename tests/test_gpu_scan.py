@@ -251,3 +251,79 @@ def test_descriptor_epochs_wrap():
                 np.testing.assert_array_equal(got.astype(np.uint64), exps[j])
     finally:
         ctx.close()
+
+
+def test_two_contexts_unserialized_every_step_exact():
+    """bench.py's issue pattern WITHOUT dp_ctx_wait: two contexts on one GPU, step k + 1 enqueued before step
+    k is collected, two different objects (and a FASTA / newline mix) so a stale or mixed-up output shows.
+    Every step's index is checked.  The library runs one persistent scan grid at a time per device (the
+    look-back needs every workgroup of a grid resident), so no launch may time out (DP_ERR_TIMEOUT)."""
+    from dataplug_amd.scan import ScanContext
+    objs = [synth.fasta((24 << 20) + 99, 12), synth.fasta((20 << 20) + 4097, 13)]
+    plans = [cpu_ref.chunk_plan(len(o), math.ceil(len(o) / 4)) for o in objs]
+    exps = [dpref.fasta_pairs(o, p) for o, p in zip(objs, plans)]
+    nl_exp = [dpref.delim(o, 0, len(o))[0] for o in objs]
+    ctxs = (ScanContext(0), ScanContext(0))
+    try:
+        ds = []
+        for c, o in zip(ctxs, objs):
+            d = c.workspace("in", len(o) + 64)
+            c.h2d(d.ptr, o)
+            ds.append(d)
+        chunks = [np.ascontiguousarray(np.asarray(p, np.uint64).reshape(-1)) for p in plans]
+        caps = [len(o) // 8 for o in objs]
+        outs = [c.workspace("out", 8 * cap) for c, cap in zip(ctxs, caps)]
+
+        def launch(i):
+            j = i % 2
+            if i % 3 == 2:
+                ctxs[j].delim_index_async(ds[j].ptr, len(objs[j]), 0, 0, len(objs[j]), 10, 1, 0, outs[j].ptr, True,
+                                          caps[j])
+            else:
+                ctxs[j].fasta_index_async(ds[j].ptr, len(objs[j]), 0, len(objs[j]), chunks[j], outs[j].ptr, False,
+                                          caps[j])
+
+        def check(i):
+            j = i % 2
+            if i % 3 == 2:
+                n, nd = ctxs[j].delim_result()
+                got = ctxs[j].d2h(np.empty(n, np.uint64), outs[j].ptr)
+                assert np.array_equal(got, nl_exp[j]), i
+            else:
+                n, pending, _ = ctxs[j].fasta_result(len(plans[j]))
+                got = ctxs[j].d2h(np.empty((n, 2), np.uint32), outs[j].ptr)
+                assert (pending == -1).all() and np.array_equal(got.astype(np.uint64), exps[j]), i
+
+        launch(0)
+        for i in range(1, 24):
+            launch(i)
+            check(i - 1)
+        check(23)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_concurrent_threads_one_device():
+    """Several host threads launching scans on ONE GPU at the same moment (what DATAPLUG_AMD_DEVICES=0,0,0,0
+    and bench.py --devices 0,0,0,0 do): every result exact, no look-back timeout."""
+    import concurrent.futures as cf
+    from dataplug_amd.scan import ScanContext
+    objs = [synth.fasta((12 << 20) + 31 * i, 40 + i) for i in range(4)]
+    plans = [cpu_ref.chunk_plan(len(o), math.ceil(len(o) / 3)) for o in objs]
+    exps = [dpref.fasta_pairs(o, p) for o, p in zip(objs, plans)]
+
+    def worker(i):
+        ctx = ScanContext(0)
+        try:
+            d = ctx.workspace("in", len(objs[i]) + 64)
+            ctx.h2d(d.ptr, objs[i])
+            for _ in range(6):
+                pairs, pending, _ = ctx.fasta_index(d.ptr, len(objs[i]), 0, len(objs[i]), plans[i])
+                assert (pending == -1).all() and np.array_equal(pairs.astype(np.uint64), exps[i])
+        finally:
+            ctx.close()
+        return True
+
+    with cf.ThreadPoolExecutor(4) as ex:
+        assert all(ex.map(worker, range(4)))

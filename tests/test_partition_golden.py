@@ -7,6 +7,7 @@ Objects: the reference's sample files are rebuilt from the golden single-slice g
 the recorded sha256; synthetic objects are regenerated from their seeds (dataplug_amd.synth).
 """
 import base64
+import builtins
 import json
 import os
 
@@ -81,8 +82,9 @@ def test_csv_partitions_match_reference():
             assert [[s.range_0, s.range_1] for s in slices] == [e[:2] for e in expected], (rec["object"], kw)
             for s, e in zip(slices, expected):
                 if isinstance(e[2], dict):
-                    with pytest.raises(SliceError):
+                    with pytest.raises(getattr(builtins, e[2]["error"])) as ei:   # the reference's class
                         s.get()
+                    assert isinstance(ei.value, SliceError)
                 else:
                     assert s.get() == e[2], (rec["object"], kw, s.chunk_id)
                 checked += 1
@@ -102,8 +104,9 @@ def test_vcf_partitions_match_reference():
             assert [[s.range_0, s.range_1] for s in slices] == [e[:2] for e in expected]
             for s, e in zip(slices, expected):
                 if isinstance(e[2], dict):
-                    with pytest.raises(SliceError):
+                    with pytest.raises(getattr(builtins, e[2]["error"])) as ei:   # the reference's class
                         s.get()
+                    assert isinstance(ei.value, SliceError)
                 else:
                     assert s.get() == e[2], (rec["object"], n, s.chunk_id)
 
