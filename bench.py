@@ -403,6 +403,7 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
     st = prepare(spec, "main")
     ss = prepare(strong, "strong") if strong is not None else None
     out["gen_s"] = time.perf_counter() - t0
+    team.barrier()                    # every worker's uploads are done before any scan (shared-GPU rehearsals)
     S = st["steps"]
     S.warm(args.warmup)
     # (1) HIP events on each context's own stream around every scan launch: the kernel's own duration
@@ -508,6 +509,10 @@ def main_fasta(args, world, rank, devs, team):
         "verified_bit_exact": verified,
         "gen_s": round(max(r["gen_s"] for r in allres), 2),
     }
+    if world > 1:
+        out["per_gpu"] = [{"worker": r["worker"], "device": r["device"], "bytes": r["scanned"],
+                           "ms_per_step": round(r["dt"] / K * 1e3, 4), "kernel_avg_us": round(r["kern_s"] * 1e6, 2),
+                           "verified": r["verified"]} for r in allres]
     print(json.dumps(out), flush=True)
 
 
@@ -545,6 +550,7 @@ def delim_worker(args, team, k, world, dev, keep_host):
         return ctxs[i % 2].delim_result()
 
     S = Steps(team, ctxs, launch, collect)
+    team.barrier()
     S.warm(args.warmup)
     dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
     dt, _, (n_out, _) = S.timed(args.steps)

@@ -107,7 +107,21 @@ constexpr uint64_t kStatMask = 3ull << 62;
 constexpr int kEpochShift = 50;
 constexpr uint64_t kEpochMask = 0xFFFull << kEpochShift;
 constexpr uint32_t kEpochMax = 0xFFFu;
-constexpr uint32_t kSpinLimit = 1u << 22;          // polls (with s_sleep) before giving up
+// Every inter-wave / inter-workgroup wait is bounded in TIME (the 100 MHz realtime counter, read every 256
+// polls), not in polls: a scan may share the device with other work (a blit kernel of another thread's
+// pageable copy, another process's kernels) that delays part of the grid by far more than any poll count
+// would allow, while a grid that really cannot become resident must still end.
+constexpr uint64_t kWaitTicks = 100000000ull * 20;   // 20 s
+constexpr uint32_t kPollCheck = 255u;                // check the clock every 256 polls
+__device__ __forceinline__ bool wait_expired(uint32_t spins, uint64_t& t0) {
+  if ((spins & kPollCheck) != kPollCheck) return false;
+  const uint64_t t = __builtin_amdgcn_s_memrealtime();
+  if (t0 == 0) {
+    t0 = t;
+    return false;
+  }
+  return t - t0 > kWaitTicks;
+}
 
 enum Mode { kFasta = 0, kDelim = 1 };
 
@@ -1001,8 +1015,9 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
 
 // Bounded LDS poll for a value written by another wave of the workgroup.
 __device__ __forceinline__ bool lds_wait_eq(const uint32_t* p, uint32_t v, uint32_t* err) {
+  uint64_t t0 = 0;
   for (uint32_t spins = 0; lds_ld(p) != v; ++spins) {
-    if (spins > kSpinLimit) {
+    if (wait_expired(spins, t0)) {
       if (__lane_id() == 0) atomicOr(err, kErrTimeout);
       return false;
     }
@@ -1083,6 +1098,7 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
   uint32_t prevS = 0;
   uint32_t pub = 0, res = 0;
   uint32_t idle = 0;
+  uint64_t idle_t0 = 0;
   auto unit_of = [&](uint32_t k) { return u0 + k * G; };
   auto compose_ready = [&]() {
     bool any = false;
@@ -1173,8 +1189,9 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     }
     if (prog) {
       idle = 0;
+      idle_t0 = 0;
     } else {
-      if (++idle > kSpinLimit) {
+      if (wait_expired(++idle, idle_t0)) {
         if (lane == 0) atomicOr(A.err, kErrTimeout);
         break;
       }
@@ -1345,13 +1362,19 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   }
 }
 
+// x - pa clamped to 0..16 (the byte bound inside one 16-byte lane), without 32-bit truncation
+__device__ __forceinline__ int lane_rel(uint64_t x, uint64_t pa) {
+  return x <= pa ? 0 : (x - pa >= 16u ? 16 : (int)(x - pa));
+}
 // first position >= from (aligned coords) holding the delimiter, inside [from, end); -1 if none.  One wave.
 __device__ uint64_t wave_find(const uint8_t* base, uint64_t from, uint64_t end, uint32_t pat, int lane, bool& found) {
   const uint32_t key = pat ^ kSel12;
   for (uint64_t a = from & ~15ull; a < end; a += kRowBytes) {
     const uint64_t pa = a + (uint64_t)lane * 16;
     uint32_t m = 0;
-    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), key) & range16((int64_t)from - (int64_t)pa, (int64_t)end - (int64_t)pa);
+    // the lane's window [from, end) in its own 16 bytes, clamped in 64 bits: end - pa exceeds an int once the
+    // buffer runs more than 2 GiB past `from` (a header cut by a chunk end early in a large buffer)
+    if (pa < end) m = mask16(*reinterpret_cast<const uint4*>(base + pa), key) & range16(lane_rel(from, pa), lane_rel(end, pa));
     const uint64_t bal = __ballot(m != 0u);
     if (bal) {
       const int l = (int)__builtin_ctzll(bal);

@@ -238,7 +238,7 @@ def test_bench_thread_mode_split_on_one_gpu(tmp_path):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--devices", "0,0,0,0",
-           "--size", str((48 << 20) + 4099), "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+           "--size", str((48 << 20) + 4096), "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])

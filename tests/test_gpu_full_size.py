@@ -76,3 +76,25 @@ def test_csv_8gib_newline_index(ctx):
     del got
     got4, nd4 = ctx.delim_index(d.ptr, size, 0, 0, size, delim=10, every_k=4, emit_add=1, u64=True)
     assert nd4 == len(exp) and np.array_equal(got4, exp[3::4] + np.uint64(1))
+
+
+def test_header_cut_by_chunk_end_far_before_buffer_end(ctx):
+    """A header line cut by a chunk end more than 2 GiB before the end of the device buffer: its end comes
+    from the resolve kernel's search, whose lane window once truncated (end - pos) to 32 bits and skipped to
+    the first '\\n' 2 GiB before the buffer end (found by bench.py's 4 x 4 GiB split).  Every chunk end of
+    the plan cuts a header here, and dp_find_delim is checked from the same positions."""
+    from oracle import dpref
+    size = 2 * GiB + (96 << 20)
+    host = synth.tiled_fasta_host(size, seed=5)
+    d = ctx.workspace("full_in", size + 64)
+    ctx.h2d(d.ptr, host)
+    gts = np.flatnonzero(host[: 8 << 20] == ord(">"))
+    cuts = [int(p) + 7 for p in gts[[3, 40, 41, 900]]]          # 7 bytes into header lines
+    plan = [(0, cuts[0])] + list(zip(cuts[:-1], cuts[1:])) + [(cuts[-1], size)]
+    pairs, pending, _ = ctx.fasta_index(d.ptr, size, 0, size, plan, u64=True)
+    assert (pending < 0).all()
+    exp = dpref.fasta_pairs(host, plan)
+    assert np.array_equal(pairs, exp)
+    for c in cuts:
+        nl = int(np.flatnonzero(host[c:c + 4096] == 10)[0]) + c
+        assert ctx.find_delim(d.ptr, size, 0, c, 10) == nl
