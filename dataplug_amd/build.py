@@ -34,7 +34,7 @@ def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=S
 def build_gz() -> str:
     os.makedirs(os.path.dirname(GZ_OUT), exist_ok=True)
     cc = os.environ.get("CC", "gcc")
-    subprocess.run([cc, "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-o", GZ_OUT + ".tmp", GZ_SRC, "-lz"], check=True)
+    subprocess.run([cc, "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-o", GZ_OUT + ".tmp", GZ_SRC, "-lz", "-lpthread"], check=True)
     os.replace(GZ_OUT + ".tmp", GZ_OUT)
     return GZ_OUT
 

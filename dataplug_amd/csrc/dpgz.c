@@ -14,8 +14,13 @@
  * Resuming at a point needs the bit offset: the Python side shifts the compressed bytes so the block
  * starts at bit 0 and inflates raw with the window as dictionary (no inflatePrime needed there).
  *
+ * Streaming form (dpgz_stream_*): the same points while the object passes through in bounded pieces, each
+ * point carrying its own window.  BGZF-style members (compressed size in the header) are inflated
+ * independently on a thread pool (dpgz_bgzf_scan + dpgz_inflate_members).
+ *
  * C ABI (declared in include/dpgz.h), no exceptions, int status (0 = ok).
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -123,4 +128,238 @@ void dpgz_free(dpgz_result* r) {
   free(r);
 }
 
-int dpgz_abi_version(void) { return 1; }
+int dpgz_abi_version(void) { return 2; }
+
+/* ------------------------------------------------------------------------------------------ streaming
+ * The same access points, built while the object streams through in bounded pieces (FASTQ.gz objects far
+ * larger than host memory, like the reference's 64 KiB writes into gztool's stdin, gzipped.py:62-83):
+ * compressed bytes go in as they arrive, inflated bytes come out into the caller's (pinned) piece buffer,
+ * and each point carries its own 32 KiB window (zlib's history at that block boundary, inflateGetDictionary)
+ * and the inflated byte before it, so nothing behind the current piece has to be kept. */
+struct dpgz_stream {
+  z_stream z;
+  int active;                 /* inside a member */
+  int failed;
+  uint64_t in_total;          /* compressed offset of the next input byte */
+  uint64_t out_total;         /* inflated bytes produced so far */
+  uint64_t span, last;
+  uint64_t members;
+  int32_t prev;               /* last inflated byte, -1 before any */
+  dpgz_point_ex* pts;         /* points not yet taken */
+  uint64_t npts, pcap;
+  uint8_t* win;               /* their windows, concatenated */
+  uint64_t nwin, wcap;
+};
+
+int dpgz_stream_new(uint64_t span, dpgz_stream** out) {
+  if (!out) return DPGZ_ERR_INVALID;
+  dpgz_stream* s = (dpgz_stream*)calloc(1, sizeof(dpgz_stream));
+  if (!s) return DPGZ_ERR_MEMORY;
+  s->span = span ? span : (1u << 20);
+  s->prev = -1;
+  *out = s;
+  return DPGZ_OK;
+}
+
+void dpgz_stream_free(dpgz_stream* s) {
+  if (!s) return;
+  if (s->active) inflateEnd(&s->z);
+  free(s->pts);
+  free(s->win);
+  free(s);
+}
+
+static int stream_point(dpgz_stream* s, uint64_t in_byte, uint32_t bits, uint32_t member) {
+  if (grow((void**)&s->pts, &s->pcap, s->npts + 1, sizeof(dpgz_point_ex))) return -1;
+  dpgz_point_ex* p = &s->pts[s->npts++];
+  p->in_byte = in_byte;
+  p->out_byte = s->out_total;
+  p->bits = bits;
+  p->member_start = member;
+  p->prev_byte = s->prev;
+  p->window_len = 0;
+  if (!member) {
+    if (grow((void**)&s->win, &s->wcap, s->nwin + 32768, 1)) return -1;
+    uInt n = 0;
+    if (inflateGetDictionary(&s->z, s->win + s->nwin, &n) != Z_OK) return -1;
+    p->window_len = n;
+    s->nwin += n;
+  }
+  s->last = s->out_total;
+  return 0;
+}
+
+int dpgz_stream_inflate(dpgz_stream* s, const uint8_t* in, uint64_t in_len, int in_final, uint8_t* out,
+                        uint64_t out_cap, uint64_t* consumed, uint64_t* produced, int* at_end) {
+  if (!s || (!in && in_len) || (!out && out_cap) || !consumed || !produced || !at_end) return DPGZ_ERR_INVALID;
+  if (s->failed) return s->failed;
+  uint64_t ci = 0, po = 0;
+  int rc = DPGZ_OK, stuck = 0;
+  *at_end = 0;
+  while (po < out_cap) {
+    if (!s->active) {
+      while (ci < in_len && in[ci] == 0) ++ci;          /* zero padding after a member (like gzip -d) */
+      if (ci == in_len) {
+        if (in_final) *at_end = 1;
+        break;
+      }
+      memset(&s->z, 0, sizeof(s->z));
+      if (inflateInit2(&s->z, 31) != Z_OK) { rc = DPGZ_ERR_ZLIB; break; }
+      s->active = 1;
+      if (stream_point(s, s->in_total + ci, 0, 1)) { rc = DPGZ_ERR_MEMORY; break; }
+      ++s->members;
+    }
+    const uint64_t left = in_len - ci;
+    s->z.next_in = (Bytef*)(in + ci);
+    s->z.avail_in = (uInt)(left > 0x40000000ull ? 0x40000000ull : left);
+    const uint64_t room = out_cap - po;
+    s->z.next_out = out + po;
+    s->z.avail_out = (uInt)(room > DPGZ_CHUNK ? DPGZ_CHUNK : room);
+    const uInt ai = s->z.avail_in, ao = s->z.avail_out;
+    const int zr = inflate(&s->z, Z_BLOCK);
+    const uint64_t used = ai - s->z.avail_in, made = ao - s->z.avail_out;
+    if (made) s->prev = out[po + made - 1];
+    ci += used;
+    po += made;
+    s->out_total += made;
+    if (zr == Z_STREAM_END) {
+      inflateEnd(&s->z);
+      s->active = 0;
+      continue;
+    }
+    if (zr != Z_OK && zr != Z_BUF_ERROR) { rc = DPGZ_ERR_ZLIB; break; }
+    if (zr == Z_BUF_ERROR || (!used && !made)) {
+      if (ci == in_len) {                                  /* needs more input */
+        if (in_final) rc = DPGZ_ERR_TRUNCATED;
+        break;
+      }
+      if (po == out_cap) break;                            /* needs more room */
+      if (++stuck > 1) { rc = DPGZ_ERR_ZLIB; break; }      /* no progress with input and room: corrupt */
+    } else {
+      stuck = 0;
+    }
+    if ((s->z.data_type & 128) && !(s->z.data_type & 64) && s->out_total - s->last >= s->span) {
+      if (stream_point(s, s->in_total + ci, (uint32_t)(s->z.data_type & 7), 0)) { rc = DPGZ_ERR_MEMORY; break; }
+    }
+  }
+  s->in_total += ci;
+  *consumed = ci;
+  *produced = po;
+  if (rc != DPGZ_OK) s->failed = rc;
+  return rc;
+}
+
+int dpgz_stream_take(dpgz_stream* s, dpgz_point_ex* pts, uint64_t max_pts, uint8_t* windows, uint64_t win_cap,
+                     uint64_t* n_pts, uint64_t* n_win) {
+  if (!s || !n_pts || !n_win) return DPGZ_ERR_INVALID;
+  uint64_t n = s->npts < max_pts ? s->npts : max_pts, w = 0;
+  for (uint64_t i = 0; i < n; ++i) w += s->pts[i].window_len;
+  while (w > win_cap && n > 0) w -= s->pts[--n].window_len;
+  if (n && (!pts || (w && !windows))) return DPGZ_ERR_INVALID;
+  memcpy(pts, s->pts, n * sizeof(dpgz_point_ex));
+  memcpy(windows, s->win, w);
+  memmove(s->pts, s->pts + n, (s->npts - n) * sizeof(dpgz_point_ex));
+  memmove(s->win, s->win + w, s->nwin - w);
+  s->npts -= n;
+  s->nwin -= w;
+  *n_pts = n;
+  *n_win = w;
+  return DPGZ_OK;
+}
+
+int dpgz_stream_state(dpgz_stream* s, uint64_t* in_total, uint64_t* out_total, uint64_t* members, uint64_t* pending_pts,
+                      uint64_t* pending_win) {
+  if (!s) return DPGZ_ERR_INVALID;
+  if (in_total) *in_total = s->in_total;
+  if (out_total) *out_total = s->out_total;
+  if (members) *members = s->members;
+  if (pending_pts) *pending_pts = s->npts;
+  if (pending_win) *pending_win = s->nwin;
+  return DPGZ_OK;
+}
+
+/* ------------------------------------------------------------------------------------------ BGZF members
+ * Members whose compressed size is in their header (the BGZF "BC" extra subfield: BSIZE + 1) and whose
+ * inflated size is their ISIZE trailer can be inflated independently: one member per task on a thread pool,
+ * each straight to its place in the output. */
+int dpgz_bgzf_scan(const uint8_t* gz, uint64_t len, uint64_t* in_off, uint64_t* in_len, uint64_t* out_len,
+                   uint64_t cap, uint64_t* n, uint64_t* used) {
+  if ((!gz && len) || !n || !used) return DPGZ_ERR_INVALID;
+  uint64_t p = 0, k = 0;
+  while (k < cap) {
+    while (p < len && gz[p] == 0) ++p;
+    if (len - p < 18) break;
+    const uint8_t* h = gz + p;
+    if (h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return DPGZ_ERR_ZLIB;   /* not BGZF */
+    const uint64_t xlen = (uint64_t)h[10] | ((uint64_t)h[11] << 8);
+    if (len - p < 12 + xlen) break;
+    uint64_t bsize = 0;
+    for (uint64_t q = 12; q + 4 <= 12 + xlen;) {
+      const uint64_t slen = (uint64_t)h[q + 2] | ((uint64_t)h[q + 3] << 8);
+      if (h[q] == 'B' && h[q + 1] == 'C' && slen == 2) bsize = ((uint64_t)h[q + 4] | ((uint64_t)h[q + 5] << 8)) + 1;
+      q += 4 + slen;
+    }
+    if (!bsize) return DPGZ_ERR_ZLIB;
+    if (len - p < bsize) break;                             /* member continues past this batch */
+    const uint8_t* t = gz + p + bsize - 4;
+    in_off[k] = p;
+    in_len[k] = bsize;
+    out_len[k] = (uint64_t)t[0] | ((uint64_t)t[1] << 8) | ((uint64_t)t[2] << 16) | ((uint64_t)t[3] << 24);
+    ++k;
+    p += bsize;
+  }
+  *n = k;
+  *used = p;
+  return DPGZ_OK;
+}
+
+typedef struct {
+  const uint8_t* gz;
+  const uint64_t *in_off, *in_len, *out_off, *out_len;
+  uint8_t* out;
+  uint64_t n;
+  uint64_t next;              /* next member to take (atomic) */
+  int rc;
+} members_job;
+
+static void* members_worker(void* arg) {
+  members_job* j = (members_job*)arg;
+  for (;;) {
+    const uint64_t i = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+    if (i >= j->n || __atomic_load_n(&j->rc, __ATOMIC_RELAXED)) break;
+    z_stream z;
+    memset(&z, 0, sizeof(z));
+    int rc = DPGZ_OK;
+    if (inflateInit2(&z, 31) != Z_OK) rc = DPGZ_ERR_ZLIB;
+    if (rc == DPGZ_OK) {
+      z.next_in = (Bytef*)(j->gz + j->in_off[i]);
+      z.avail_in = (uInt)j->in_len[i];
+      z.next_out = j->out + j->out_off[i];
+      z.avail_out = (uInt)j->out_len[i];
+      const int zr = inflate(&z, Z_FINISH);
+      if (zr != Z_STREAM_END || z.total_out != j->out_len[i]) rc = zr == Z_BUF_ERROR ? DPGZ_ERR_TRUNCATED : DPGZ_ERR_ZLIB;
+      inflateEnd(&z);
+    }
+    if (rc) {
+      int zero = 0;
+      __atomic_compare_exchange_n(&j->rc, &zero, rc, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+    }
+  }
+  return NULL;
+}
+
+int dpgz_inflate_members(const uint8_t* gz, const uint64_t* in_off, const uint64_t* in_len, const uint64_t* out_off,
+                         const uint64_t* out_len, uint64_t n, uint8_t* out, int threads) {
+  if ((!gz || !in_off || !in_len || !out_off || !out_len || !out) && n) return DPGZ_ERR_INVALID;
+  members_job j = {gz, in_off, in_len, out_off, out_len, out, n, 0, DPGZ_OK};
+  int nt = threads > 0 ? threads : 1;
+  if ((uint64_t)nt > n) nt = (int)(n ? n : 1);
+  pthread_t th[256];
+  if (nt > 256) nt = 256;
+  int started = 0;
+  for (int t = 1; t < nt; ++t)
+    if (pthread_create(&th[t], NULL, members_worker, &j) == 0) ++started; else break;
+  members_worker(&j);
+  for (int t = 1; t <= started; ++t) pthread_join(th[t], NULL);
+  return j.rc;
+}

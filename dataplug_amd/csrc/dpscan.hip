@@ -168,6 +168,8 @@ struct ScanArgs {
   void* out;
   uint64_t cap;                // entries (FASTA: pairs)
   int out_u64;
+  uint32_t wrap32;             // DELIM uint32 output as low words (paged index): no overflow check
+  uint64_t carry;              // DELIM: delimiters before this launch's first byte (a streamed object's pieces)
   uint32_t delim;              // DELIM: byte replicated x4
   uint32_t every_k;
   uint32_t emit_add;
@@ -887,7 +889,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
     return a + 16 <= hi16 ? *reinterpret_cast<const v4u*>(src + a) : v4u{0u, 0u, 0u, 0u};
   };
   const uint64_t obj_off = A.obj_base - A.shift + wbase;
-  const bool near4g = !OUT64 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+  const bool near4g = !OUT64 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
   bool ovf = false;
   if constexpr (MODE == kFasta) {
     const uint64_t b0 = 2 * P - S, last = 2 * A.cap - 1;
@@ -907,9 +909,11 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
   } else {
     const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
     const uint32_t k = A.every_k;
-    // every k-th delimiter overall: rank rk is kept iff rk >= r0 and (rk - r0) % k == 0, at q0 + (rk - r0) / k
-    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - P % k);
-    const uint64_t q0 = (P + r0) / k;
+    // every k-th delimiter overall (counting from the carried ordinal): rank rk is kept iff rk >= r0 and
+    // (rk - r0) % k == 0, at q0 + (rk - r0) / k
+    const uint64_t Pc = P + A.carry;
+    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - Pc % k);
+    const uint64_t q0 = (Pc + r0) / k - A.carry / k;
     uint32_t n = 0;
     auto out = [&](uint32_t rk, uint32_t pos) {
       if (rk < r0) return;
@@ -949,7 +953,7 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
     return;
   }
   const uint64_t obj_off = A.obj_base - A.shift + wbase;
-  const bool near4g = !OUT64 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+  const bool near4g = !OUT64 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
   const uint16_t* evw = sh.ev[wave];
   bool ovf = false;
   if constexpr (MODE == kFasta) {
@@ -968,9 +972,11 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
   } else {
     const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
     const uint32_t k = A.every_k;
-    // every k-th delimiter overall (FASTQ read ends): list entries r0, r0 + k, ... go to q0, q0 + 1, ...
-    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - P % k);
-    const uint64_t q0 = (P + r0) / k;
+    // every k-th delimiter overall (FASTQ read ends), counting from the carried ordinal: list entries
+    // r0, r0 + k, ... go to q0, q0 + 1, ...
+    const uint64_t Pc = P + A.carry;
+    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - Pc % k);
+    const uint64_t q0 = (Pc + r0) / k - A.carry / k;
     const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
 #if DP_PAIRSTORE
     if constexpr (OUT64 != 0) {
@@ -1432,8 +1438,11 @@ __global__ void __launch_bounds__(kWave) find_kernel(const uint8_t* base, uint64
 }
 
 // ------------------------------------------------------------------------------------------ calibration
-// Plain read-only stream (16 B per lane, grid-stride, 4 loads in flight per lane, non-temporal like the
-// scan's input loads): the achievable HBM read rate on this device, reported next to the roofline fraction.
+// Streaming ceilings on this device, reported next to the roofline fractions (tools/ubench_rw.hip has the
+// variants these were chosen from): one 1024-thread workgroup per CU, each wave reading 16 KiB ranges as
+// 16 non-temporal 16-byte lane loads in flight, and optionally writing `wq16 / 65536` output bytes per
+// input byte as contiguous non-temporal 16-byte lane stores, range by range — the DELIM index's traffic
+// mix (CSV ~0.22, VCF ~0.10).  Read-only: the best plain read rate measured (~7.0 TB/s on MI355X).
 __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
   uint4 v;
   v.x = __builtin_nontemporal_load(&p->x);
@@ -1442,18 +1451,36 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
   v.w = __builtin_nontemporal_load(&p->w);
   return v;
 }
-__global__ void __launch_bounds__(256) stream_read_kernel(const uint4* __restrict__ p, uint64_t n16,
-                                                         unsigned* __restrict__ sink) {
+constexpr int kCalRange = 16384;
+__global__ void __launch_bounds__(1024) stream_kernel(const uint4* __restrict__ in, uint64_t n16,
+                                                     uint4* __restrict__ out, uint64_t wq16,
+                                                     unsigned* __restrict__ sink) {
+  const int lane = __lane_id();
+  const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t nranges = (n16 * 16 + kCalRange - 1) / kCalRange;
   uint32_t acc = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = ld_nt(p + i), b = ld_nt(p + i + stride), c = ld_nt(p + i + 2 * stride), d = ld_nt(p + i + 3 * stride);
-    acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
-  }
-  for (; i < n16; i += stride) {
-    const uint4 a = ld_nt(p + i);
-    acc ^= a.x ^ a.y ^ a.z ^ a.w;
+  for (uint64_t r = wave; r < nranges; r += nwaves) {
+    const uint64_t i0 = r * (kCalRange / 16) + (uint64_t)lane;
+    uint4 v[kCalRange / 1024];
+#pragma unroll
+    for (int i = 0; i < kCalRange / 1024; ++i) {
+      const uint64_t j = i0 + (uint64_t)i * 64;
+      v[i] = j < n16 ? ld_nt(in + j) : uint4{0u, 0u, 0u, 0u};
+    }
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < kCalRange / 1024; ++i) x ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+    acc ^= x;
+    if (out) {
+      const uint64_t e0 = (r * wq16) >> 6, e1 = ((r + 1) * wq16) >> 6;   // 16-byte elements of this range
+      for (uint64_t e = e0 + (uint64_t)lane; e < e1; e += 64) {
+        __builtin_nontemporal_store(x, &out[e].x);
+        __builtin_nontemporal_store((uint32_t)e, &out[e].y);
+        __builtin_nontemporal_store((uint32_t)r, &out[e].z);
+        __builtin_nontemporal_store(acc, &out[e].w);
+      }
+    }
   }
   if (acc == 0x9E3779B9u) sink[0] = acc;   // keeps the loads alive; practically never stores
 }
@@ -1507,6 +1534,7 @@ struct dp_ctx {
   uint64_t nchunks = 0, cap = 0;
   int out_u64 = 0;
   uint32_t every_k = 1;
+  uint64_t carry = 0;
   uint64_t pend_off = 0, ctrl_off = 0;
   // timing
   bool timing = false;
@@ -1618,7 +1646,8 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
 }
 
 int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t units,
-                void* d_out, int out_u64, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add) {
+                void* d_out, int out_u64, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add,
+                uint64_t carry = 0, uint32_t wrap32 = 0) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
   ScanArgs a;
   a.base = d_buf - shift;
@@ -1635,6 +1664,8 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.out = d_out;
   a.cap = cap;
   a.out_u64 = out_u64;
+  a.wrap32 = wrap32;
+  a.carry = carry;
   a.delim = delim * 0x01010101u;
   a.every_k = every_k;
   a.emit_add = emit_add;
@@ -1927,42 +1958,54 @@ int dp_fasta_index(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t b
   return dp_fasta_result(c, n_pairs, pending, chunk_end);
 }
 
-int dp_delim_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin,
-                         uint64_t end, uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out,
-                         int out_u64, uint64_t cap) {
+int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, const uint64_t* ranges,
+                          uint64_t nranges, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
+                          void* d_out, int out_mode, uint64_t cap) {
   int rc = check_ctx(c);
   if (rc) return rc;
   if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is already in flight on this ctx");
   if (every_k == 0) return fail(DP_ERR_INVALID, "every_k must be >= 1");
   if (delim > 255) return fail(DP_ERR_INVALID, "delim must be a byte");
-  if (end > begin && !d_buf) return fail(DP_ERR_INVALID, "null buffer");
+  if (out_mode < 0 || out_mode > 2) return fail(DP_ERR_INVALID, "out_mode must be 0 (uint32), 1 (uint64) or 2 (uint32 low words)");
+  if (nranges == 0 || !ranges) return fail(DP_ERR_INVALID, "no ranges");
+  for (uint64_t i = 0; i < nranges; ++i) {
+    if (ranges[2 * i + 1] > ranges[2 * i] && !d_buf) return fail(DP_ERR_INVALID, "null buffer");
+    if (i && ranges[2 * i] < ranges[2 * i - 1]) return fail(DP_ERR_INVALID, "ranges must ascend without overlap");
+  }
   if (cap && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
-  const uint64_t ch[2] = {begin, end};
   uint64_t units = 0;
-  rc = stage_chunks(c, d_buf, buf_len, buf_base, ch, 1, &units);
+  rc = stage_chunks(c, d_buf, buf_len, buf_base, ranges, nranges, &units);
   if (rc) return rc;
-  rc = launch_scan(c, kDelim, d_buf, buf_base, 1, units, d_out, out_u64, cap, delim, every_k, emit_add);
+  rc = launch_scan(c, kDelim, d_buf, buf_base, nranges, units, d_out, out_mode == 1, cap, delim, every_k, emit_add,
+                   carry, out_mode == 2);
   if (rc) return rc;
   c->inflight = kDelim;
-  c->nchunks = 1;
+  c->nchunks = nranges;
   c->cap = cap;
-  c->out_u64 = out_u64;
+  c->out_u64 = out_mode == 1;
   c->every_k = every_k;
+  c->carry = carry;
   return DP_OK;
 }
 
-int dp_delim_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims) {
+int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint64_t* range_end) {
   int rc = check_ctx(c);
   if (rc) return rc;
   if (c->inflight != kDelim) return fail(DP_ERR_INVALID, "no delimiter scan in flight on this ctx");
-  const uint64_t k = c->every_k;
+  const uint64_t k = c->every_k, carry = c->carry;
   c->inflight = -1;
   rc = collect_ctrl(c, 0);
   if (rc) return rc;
   const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
   if (err) c->last_tab.clear();                         // the next launch re-uploads err = 0
-  const uint64_t nd = c->h_tab[c->ctrl_off + 1];
-  const uint64_t nout = k ? nd / k : 0;
+  // delimiters in the launch (the total is written at the last unit; no unit: none)
+  uint64_t nd = 0;
+  for (uint64_t i = 0; i < c->nchunks; ++i) {
+    const uint64_t e = c->h_tab[c->pend_off + c->nchunks + i];
+    if (e != ~0ull) nd = e;                             // empty ranges were never visited: carry the previous
+    if (range_end) range_end[i] = nd;
+  }
+  const uint64_t nout = (carry + nd) / k - carry / k;
   if (n_delims) *n_delims = nd;
   if (n_out) *n_out = nout;
   if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out (grid not co-resident?)");
@@ -1970,6 +2013,18 @@ int dp_delim_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims) {
   if (nout > c->cap) return fail(DP_ERR_CAPACITY, "output capacity " + std::to_string(c->cap) + " < " +
                                                       std::to_string(nout) + " offsets");
   return DP_OK;
+}
+
+int dp_delim_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin,
+                         uint64_t end, uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out,
+                         int out_u64, uint64_t cap) {
+  const uint64_t r[2] = {begin, end};
+  return dp_delim_ranges_async(c, d_buf, buf_len, buf_base, r, 1, delim, every_k, emit_add, 0, d_out, out_u64 ? 1 : 0,
+                               cap);
+}
+
+int dp_delim_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims) {
+  return dp_delim_ranges_result(c, n_out, n_delims, nullptr);
 }
 
 int dp_delim_index(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t begin, uint64_t end,
@@ -2005,20 +2060,26 @@ int dp_find_delim(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t bu
   return DP_OK;
 }
 
-int dp_stream_read(dp_ctx* c, const void* d_buf, uint64_t bytes, int blocks_per_cu) {
+int dp_stream_rw(dp_ctx* c, const void* d_in, uint64_t bytes, void* d_out, uint32_t write_q16, int blocks_per_cu) {
   int rc = check_ctx(c);
   if (rc) return rc;
+  if (write_q16 && !d_out) return fail(DP_ERR_INVALID, "null output with write_q16 > 0");
   rc = ensure_tab(c, 8);
   if (rc) return rc;
-  const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 8;
+  const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 1;
   c->last_tab.clear();   // the table area is the (practically never written) sink
   hipEvent_t e0;
   rc = ev_begin(c, &e0);
   if (rc) return rc;
-  hipLaunchKernelGGL(stream_read_kernel, dim3((unsigned)(c->cus * bpc)), dim3(256), 0, c->stream,
-                     reinterpret_cast<const uint4*>(d_buf), bytes / 16, reinterpret_cast<unsigned*>(c->d_tab));
+  hipLaunchKernelGGL(stream_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, c->stream,
+                     reinterpret_cast<const uint4*>(d_in), bytes / 16, write_q16 ? reinterpret_cast<uint4*>(d_out) : nullptr,
+                     (uint64_t)write_q16, reinterpret_cast<unsigned*>(c->d_tab));
   HIPCHK(hipGetLastError());
   return ev_end(c);
+}
+
+int dp_stream_read(dp_ctx* c, const void* d_buf, uint64_t bytes, int blocks_per_cu) {
+  return dp_stream_rw(c, d_buf, bytes, nullptr, 0, blocks_per_cu);
 }
 
 int dp_timing_enable(dp_ctx* c, int enable) {

@@ -3,11 +3,13 @@
 The reference shells out to gztool 1.4.3 (gzipped.py:26-153; not vendored, not installed here) for
 ``total_lines``, a window table and a binary index that lets a slice resume inflating mid-object.  Here:
 
-* libdpgz.so (zlib, ``dataplug_amd/csrc/dpgz.c``) inflates the object once and records access points at
-  deflate block boundaries every ``span`` inflated bytes plus every gzip member start;
-* the inflated bytes are scanned on the GPU (``dp_delim_index``): every '\n' offset, from which
-  ``total_lines`` (+1 for a final unterminated line — gztool's own convention is unpinned),
-  each point's line number and the per-record (FASTQ read) end offsets follow;
+* the object streams once through ``scan.gzindex``: libdpgz.so (zlib, ``dataplug_amd/csrc/dpgz.c``) inflates
+  it in bounded pieces (one core for a plain gzip stream, a thread pool for BGZF-style members) and records
+  access points at deflate block boundaries every ``span`` inflated bytes plus gzip member starts, each
+  with its window; each piece is scanned on the GPU (``dp_delim_ranges`` with the newline ordinal carried
+  across pieces), from which ``total_lines`` (+1 for a final unterminated line — gztool's own convention is
+  unpinned, SURVEY.md §8(c)), each point's line number and the per-record (FASTQ read) end offsets follow;
+  host memory stays bounded by the piece buffers, whatever the object size;
 * the meta object is the window table as parquet with the reference's columns (window, compressed_byte,
   uncompressed_byte, line_number, window_size, window_offset) plus ``bits``, ``member_start`` and
   ``line_start``; the 32 KiB windows are stored at ``attributes.index_key`` (``<key>.idx``) and the
@@ -26,7 +28,9 @@ import numpy as np
 from ... import gz as gzidx
 from ...entities import CloudDataFormat, CloudObjectSlice, PartitioningStrategy
 from ...preprocessing.metadata import PreprocessingMetadata
+from ...scan import gzindex
 from ...scan import objects as scan_objects
+from ...scan.device import get_context
 from ...version import __version__
 
 if TYPE_CHECKING:
@@ -62,32 +66,33 @@ def window_table(inflated: np.ndarray, points: np.ndarray, newlines: np.ndarray)
     return rows, b"".join(blobs)
 
 
-def preprocess_gzip(cloud_object: "CloudObject", record_lines: int = 4, span: int = SPAN) -> PreprocessingMetadata:
+def preprocess_gzip(cloud_object: "CloudObject", record_lines: int = 4, span: int = SPAN,
+                    piece_bytes: int = gzindex.PIECE_BYTES) -> PreprocessingMetadata:
+    """gzipped.py:46-153: streams the object once (one GET, read in 1 MiB pieces like the reference's writes
+    into gztool) through the bounded inflate -> HBM -> newline-scan pipeline of ``scan.gzindex``; stores the
+    windows (``<key>.idx``), the read ends (``<key>.records``) and the window table (parquet, the meta object)."""
     import pandas as pd
 
+    ctx = get_context(scan_objects.devices(co=cloud_object)[0])
     res = cloud_object.storage.get_object(Bucket=cloud_object.path.bucket, Key=cloud_object.path.key)
     with res["Body"] as body:
-        data = body.read()
-    inflated, points = gzidx.build_index(data, span=span)
-    del data
-    newlines, n_nl = scan_objects.record_index_bytes(inflated, delim=10, every_k=1, emit_add=0)
-    total_lines = n_nl + (1 if len(inflated) and inflated[-1] != 10 else 0)
-    ends = newlines[record_lines - 1::record_lines] + np.uint64(1)
-    rows, windows = window_table(inflated, points, newlines)
+        ix = gzindex.index_stream(ctx, body.read, record_lines=record_lines, span=span, piece_bytes=piece_bytes)
     meta = cloud_object.meta_path
     idx_key, rec_key = meta.key + ".idx", meta.key + ".records"
     st = cloud_object.storage
-    st.put_object(Body=windows, Bucket=meta.bucket, Key=idx_key, Metadata={"dataplug": __version__})
-    st.put_object(Body=np.ascontiguousarray(ends, dtype="<u8").tobytes(), Bucket=meta.bucket, Key=rec_key,
-                  Metadata={"dataplug": __version__})
-    df = pd.DataFrame(rows, columns=WINDOW_COLUMNS).set_index(["window"])
+    extra = {"Metadata": {"dataplug": __version__}}
+    st.upload_fileobj(Fileobj=ix.windows, Bucket=meta.bucket, Key=idx_key, ExtraArgs=extra)
+    st.upload_fileobj(Fileobj=ix.ends, Bucket=meta.bucket, Key=rec_key, ExtraArgs=extra)
+    ix.windows.close()
+    ix.ends.close()
+    df = pd.DataFrame(ix.rows, columns=WINDOW_COLUMNS).set_index(["window"])
     out = io.BytesIO()
     df.to_parquet(out, engine="pyarrow")
     out.seek(0)
     return PreprocessingMetadata(metadata=out, attributes={
-        "total_lines": int(total_lines), "index_key": idx_key, "records_key": rec_key,
-        "record_lines": int(record_lines), "num_records": int(len(ends)), "uncompressed_size": int(len(inflated)),
-        "gzip_members": int(points["member_start"].sum())})
+        "total_lines": int(ix.total_lines), "index_key": idx_key, "records_key": rec_key,
+        "record_lines": int(record_lines), "num_records": int(ix.num_records),
+        "uncompressed_size": int(ix.uncompressed_size), "gzip_members": int(ix.members), "bgzf": bool(ix.bgzf)})
 
 
 def load_window_table(cloud_object):

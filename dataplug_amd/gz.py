@@ -32,8 +32,17 @@ class _Result(ctypes.Structure):
                 ("points", ctypes.POINTER(_Point)), ("n_points", ctypes.c_uint64), ("members", ctypes.c_uint64)]
 
 
+POINTEX_DTYPE = np.dtype([("in_byte", "<u8"), ("out_byte", "<u8"), ("bits", "<u4"), ("member_start", "<u4"),
+                          ("prev_byte", "<i4"), ("window_len", "<u4")])
+
 _lib = None
 _ERRORS = {1: "invalid argument", 2: "out of memory", 3: "corrupt gzip/deflate data", 4: "truncated gzip stream"}
+_U64P = ctypes.POINTER(ctypes.c_uint64)
+
+
+def _check(rc: int, what: str) -> None:
+    if rc:
+        raise ValueError(f"{what}: {_ERRORS.get(rc, rc)}")
 
 
 def load():
@@ -48,6 +57,24 @@ def load():
         lib.dpgz_free.restype = None
         lib.dpgz_free.argtypes = [ctypes.POINTER(_Result)]
         lib.dpgz_abi_version.restype = ctypes.c_int
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        lib.dpgz_stream_new.restype = ctypes.c_int
+        lib.dpgz_stream_new.argtypes = [u64, ctypes.POINTER(vp)]
+        lib.dpgz_stream_free.restype = None
+        lib.dpgz_stream_free.argtypes = [vp]
+        lib.dpgz_stream_inflate.restype = ctypes.c_int
+        lib.dpgz_stream_inflate.argtypes = [vp, vp, u64, ctypes.c_int, vp, u64, _U64P, _U64P,
+                                            ctypes.POINTER(ctypes.c_int)]
+        lib.dpgz_stream_take.restype = ctypes.c_int
+        lib.dpgz_stream_take.argtypes = [vp, vp, u64, vp, u64, _U64P, _U64P]
+        lib.dpgz_stream_state.restype = ctypes.c_int
+        lib.dpgz_stream_state.argtypes = [vp, _U64P, _U64P, _U64P, _U64P, _U64P]
+        lib.dpgz_bgzf_scan.restype = ctypes.c_int
+        lib.dpgz_bgzf_scan.argtypes = [vp, u64, _U64P, _U64P, _U64P, u64, _U64P, _U64P]
+        lib.dpgz_inflate_members.restype = ctypes.c_int
+        lib.dpgz_inflate_members.argtypes = [vp, _U64P, _U64P, _U64P, _U64P, u64, vp, ctypes.c_int]
+        if lib.dpgz_abi_version() < 2:
+            raise ImportError(f"{LIB_PATH} is out of date: rebuild it with `python -m dataplug_amd.build`")
         _lib = lib
     return _lib
 
@@ -99,34 +126,59 @@ class _Shifter:
         return bytes([self.prev >> (8 - self.b)])
 
 
+def _members_from(src: Iterable[bytes]) -> Iterator[bytes]:
+    """Inflate consecutive gzip members from a compressed byte stream that starts at a member start
+    (zero padding between members tolerated), to the end of the stream."""
+    d = None
+    for c in src:
+        while c:
+            if d is None:
+                c = c.lstrip(b"\0")
+                if not c:
+                    break
+                d = zlib.decompressobj(wbits=31)
+            out = d.decompress(c)
+            if out:
+                yield out
+            if d.eof:
+                c = d.unused_data
+                d = None
+            else:
+                c = b""
+    if d is not None:
+        tail = d.flush()
+        if tail:
+            yield tail
+        if not d.eof:
+            raise ValueError("gzip stream: truncated member")
+
+
 def inflate_from(points: np.ndarray, i: int, window: bytes, fetch: Callable[[int], Iterable[bytes]]) -> Iterator[bytes]:
     """Inflated bytes from access point ``i`` to the end of the object.
 
     ``fetch(offset)`` yields the compressed object's bytes from ``offset`` onwards (chunks of any size;
-    the caller may stop iterating any time).  Member ends inside a shifted stream are not byte-
-    addressable, so at the end of a member the stream continues at the next member-start point."""
+    the caller may stop iterating any time).  From a member-start point the members that follow are inflated
+    in sequence from the same bytes (BGZF indexes keep only some member starts as points).  From a point
+    inside a member, the member's end is not byte-addressable in the shifted stream, so the stream continues
+    at the next member-start point (streams indexed block-wise keep every member start as a point)."""
     while i < len(points):
         p = points[i]
-        member = bool(p["member_start"])
-        if member:
-            d = zlib.decompressobj(wbits=31)
-            src = fetch(int(p["in_byte"]))
-            sh = None
-        else:
-            b = int(p["bits"])
-            d = zlib.decompressobj(wbits=-15, zdict=window) if window else zlib.decompressobj(wbits=-15)
-            src = fetch(int(p["in_byte"]) - (1 if b else 0))
-            sh = _Shifter(b)
+        if p["member_start"]:
+            yield from _members_from(fetch(int(p["in_byte"])))
+            return
+        b = int(p["bits"])
+        d = zlib.decompressobj(wbits=-15, zdict=window) if window else zlib.decompressobj(wbits=-15)
+        src = fetch(int(p["in_byte"]) - (1 if b else 0))
+        sh = _Shifter(b)
         for c in src:
-            if sh is not None:
-                c = sh.feed(c)
+            c = sh.feed(c)
             out = d.decompress(c)
             if out:
                 yield out
             if d.eof:
                 break
         else:
-            if sh is not None and not d.eof:
+            if not d.eof:
                 out = d.decompress(sh.flush())
                 if out:
                     yield out
@@ -145,3 +197,93 @@ def inflate_from(points: np.ndarray, i: int, window: bytes, fetch: Callable[[int
 
 def window_of(inflated: np.ndarray, out_byte: int) -> bytes:
     return inflated[max(0, out_byte - WINDOW):out_byte].tobytes()
+
+
+# ------------------------------------------------------------------------------------------ streaming
+def _addr(buf) -> int:
+    """Address of a writable/readable contiguous buffer (numpy array, bytearray, bytes, memoryview)."""
+    if isinstance(buf, np.ndarray):
+        return buf.ctypes.data
+    return np.frombuffer(buf, np.uint8).ctypes.data if len(buf) else 0
+
+
+class InflateStream:
+    """libdpgz's streaming inflater: compressed bytes in as they arrive, inflated bytes out into the caller's
+    buffer, access points (with their windows) collected on the way (see include/dpgz.h)."""
+
+    def __init__(self, span: int = 1 << 20):
+        h = ctypes.c_void_p()
+        _check(load().dpgz_stream_new(int(span), ctypes.byref(h)), "gzip stream")
+        self._h = h
+
+    def inflate(self, data, final: bool, out: np.ndarray, out_off: int, out_cap: int):
+        """(consumed, produced, at_end): inflate ``data`` into out[out_off : out_off + out_cap]."""
+        c, p, e = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_int(0)
+        keep = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+        _check(load().dpgz_stream_inflate(self._h, keep.ctypes.data, len(data), int(final),
+                                          out.ctypes.data + out_off, int(out_cap), ctypes.byref(c), ctypes.byref(p),
+                                          ctypes.byref(e)), "gzip stream")
+        return int(c.value), int(p.value), bool(e.value)
+
+    def take(self):
+        """(points as a POINTEX_DTYPE array, their windows concatenated as bytes) found since the last take."""
+        st = [ctypes.c_uint64(0) for _ in range(5)]
+        load().dpgz_stream_state(self._h, *[ctypes.byref(x) for x in st])
+        npts, nwin = int(st[3].value), int(st[4].value)
+        pts = np.zeros(npts, POINTEX_DTYPE)
+        win = np.zeros(max(1, nwin), np.uint8)
+        n, w = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(load().dpgz_stream_take(self._h, pts.ctypes.data if npts else None, npts, win.ctypes.data, nwin,
+                                       ctypes.byref(n), ctypes.byref(w)), "gzip stream")
+        return pts[: int(n.value)], win[: int(w.value)].tobytes()
+
+    def state(self):
+        """(compressed bytes consumed, inflated bytes produced, members started)."""
+        st = [ctypes.c_uint64(0) for _ in range(5)]
+        load().dpgz_stream_state(self._h, *[ctypes.byref(x) for x in st])
+        return int(st[0].value), int(st[1].value), int(st[2].value)
+
+    def close(self):
+        if self._h:
+            load().dpgz_stream_free(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def is_bgzf(head) -> bool:
+    """The first member carries its compressed size (BGZF "BC" extra subfield)."""
+    h = bytes(head[:64])
+    if len(h) < 18 or h[0] != 0x1F or h[1] != 0x8B or h[2] != 8 or not h[3] & 4:
+        return False
+    xlen = h[10] | (h[11] << 8)
+    q = 12
+    while q + 4 <= min(len(h), 12 + xlen):
+        slen = h[q + 2] | (h[q + 3] << 8)
+        if h[q:q + 2] == b"BC" and slen == 2:
+            return True
+        q += 4 + slen
+    return False
+
+
+def bgzf_scan(buf: np.ndarray):
+    """Complete BGZF members at the start of ``buf``: (in_off, in_len, out_len) uint64 arrays, bytes used."""
+    cap = len(buf) // 18 + 1
+    a, b, c = (np.zeros(cap, np.uint64) for _ in range(3))
+    n, used = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(load().dpgz_bgzf_scan(buf.ctypes.data if len(buf) else None, len(buf), a.ctypes.data_as(_U64P),
+                                 b.ctypes.data_as(_U64P), c.ctypes.data_as(_U64P), cap, ctypes.byref(n),
+                                 ctypes.byref(used)), "BGZF member table")
+    k = int(n.value)
+    return a[:k], b[:k], c[:k], int(used.value)
+
+
+def inflate_members(buf: np.ndarray, in_off, in_len, out_off, out_len, out_addr: int, threads: int) -> None:
+    """Inflate BGZF members of ``buf`` independently on ``threads`` threads, member i to out_addr + out_off[i]."""
+    arrs = [np.ascontiguousarray(x, np.uint64) for x in (in_off, in_len, out_off, out_len)]
+    _check(load().dpgz_inflate_members(buf.ctypes.data, *[x.ctypes.data_as(_U64P) for x in arrs], len(arrs[0]),
+                                       out_addr, int(threads)), "BGZF inflate")

@@ -50,8 +50,12 @@ SIGNATURES = [
     ("dp_delim_index_async", _c.c_int, [_p, _p, _u64, _u64, _u64, _u64, _c.c_uint32, _c.c_uint32, _c.c_uint32,
                                         _p, _c.c_int, _u64]),
     ("dp_delim_result", _c.c_int, [_p, _u64p, _u64p]),
+    ("dp_delim_ranges_async", _c.c_int, [_p, _p, _u64, _u64, _u64p, _u64, _c.c_uint32, _c.c_uint32, _c.c_uint32,
+                                         _u64, _p, _c.c_int, _u64]),
+    ("dp_delim_ranges_result", _c.c_int, [_p, _u64p, _u64p, _u64p]),
     ("dp_find_delim", _c.c_int, [_p, _p, _u64, _u64, _u64, _c.c_uint32, _i64p]),
     ("dp_stream_read", _c.c_int, [_p, _p, _u64, _c.c_int]),
+    ("dp_stream_rw", _c.c_int, [_p, _p, _u64, _p, _c.c_uint32, _c.c_int]),
     ("dp_timing_enable", _c.c_int, [_p, _c.c_int]),
     ("dp_timing_read", _c.c_int, [_p, _c.POINTER(_c.c_double), _u64p]),
     ("dp_debug_profile", _c.c_int, [_p, _u64p, _u64, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),

@@ -213,6 +213,48 @@ class ScanContext:
         check(self.lib.dp_delim_result(self.handle, ctypes.byref(n), ctypes.byref(nd)))
         return int(n.value), int(nd.value)
 
+    def delim_ranges_async(self, d_buf: int, buf_len: int, buf_base: int, ranges: np.ndarray, delim: int,
+                           every_k: int, emit_add: int, carry: int, d_out: int, out_mode: int, cap: int) -> None:
+        """dp_delim_ranges_async; ``ranges`` a contiguous uint64 array [lo0, hi0, lo1, hi1, ...] kept alive by
+        the caller until the result is collected."""
+        check(self.lib.dp_delim_ranges_async(self.handle, ctypes.c_void_p(d_buf), buf_len, buf_base,
+                                             ranges.ctypes.data_as(_U64P), len(ranges) // 2, int(delim),
+                                             int(every_k), int(emit_add), int(carry), ctypes.c_void_p(d_out),
+                                             int(out_mode), int(cap)))
+
+    def delim_ranges_result(self, nranges: int):
+        """(entries, delimiters seen, per-range cumulative delimiter counts)."""
+        n = ctypes.c_uint64(0)
+        nd = ctypes.c_uint64(0)
+        ends = np.zeros(nranges, np.uint64)
+        rc = self.lib.dp_delim_ranges_result(self.handle, ctypes.byref(n), ctypes.byref(nd), ends.ctypes.data_as(_U64P))
+        if rc == _lib.DP_ERR_CAPACITY:
+            e = DPCapacityError(rc, f"output capacity below {int(n.value)} entries")
+            e.needed = int(n.value)
+            raise e
+        check(rc)
+        return int(n.value), int(nd.value), ends
+
+    def delim_ranges(self, d_buf: int, buf_len: int, buf_base: int, ranges, delim: int = 10, every_k: int = 1,
+                     emit_add: int = 0, carry: int = 0, out_mode: int = 1, cap: Optional[int] = None):
+        """Synchronous dp_delim_ranges: (offsets, delimiters seen, per-range cumulative counts); out_mode 1
+        uint64, 0 uint32, 2 uint32 low words."""
+        rg = np.ascontiguousarray(np.asarray(ranges, dtype=np.uint64).reshape(-1))
+        span = int(sum(int(rg[2 * i + 1]) - int(rg[2 * i]) for i in range(len(rg) // 2)))
+        dtype = np.uint64 if out_mode == 1 else np.uint32
+        if cap is None:
+            cap = span // (16 * every_k) + 1024
+        while True:
+            out = self.workspace("out", cap * np.dtype(dtype).itemsize + 16)
+            self.delim_ranges_async(d_buf, buf_len, buf_base, rg, delim, every_k, emit_add, carry, out.ptr,
+                                    out_mode, cap)
+            try:
+                n, nd, ends = self.delim_ranges_result(len(rg) // 2)
+            except DPCapacityError as e:
+                cap = e.needed
+                continue
+            return self.d2h(np.empty(n, dtype), out.ptr), nd, ends
+
     def find_delim(self, d_buf: int, buf_len: int, buf_base: int, start: int, delim: int = 10) -> int:
         """First object offset >= start holding ``delim`` in the buffer, or -1."""
         pos = ctypes.c_int64(-1)
@@ -233,9 +275,15 @@ class ScanContext:
         ptr, n = self.upload(data, name="halo")
         return self.find_delim(ptr, n, buf_base, start, delim)
 
-    def stream_read(self, d_buf: int, nbytes: int, blocks_per_cu: int = 8) -> None:
+    def stream_read(self, d_buf: int, nbytes: int, blocks_per_cu: int = 0) -> None:
         """Calibration read of ``nbytes`` device bytes (async; time it with timing())."""
         check(self.lib.dp_stream_read(self.handle, ctypes.c_void_p(d_buf), nbytes, blocks_per_cu))
+
+    def stream_rw(self, d_in: int, nbytes: int, d_out: int, write_per_read: float, blocks_per_cu: int = 0) -> None:
+        """Calibration read of ``nbytes`` plus ``write_per_read * nbytes`` contiguous output bytes (async)."""
+        q = int(round(write_per_read * 65536))
+        check(self.lib.dp_stream_rw(self.handle, ctypes.c_void_p(d_in), nbytes, ctypes.c_void_p(d_out if q else 0),
+                                    q, blocks_per_cu))
 
     # ---------------------------------------------------------------- timing / geometry
     def timing(self, enable: bool) -> None:

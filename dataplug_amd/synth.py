@@ -285,3 +285,25 @@ def tiled_vcf(size: int, seed: int = 0, block: int = 64 * 2**20 - 333) -> TiledT
     base = vcf(block, seed)
     h = len(VCF_HEADER)
     return TiledText(base[:h], base[h:], size)
+
+
+def bgzf(raw: bytes, block: int = 65280, level: int = 6, eof: bool = True) -> bytes:
+    """BGZF (blocked gzip, as samtools/htslib write FASTQ.gz): independent gzip members of at most ``block``
+    inflated bytes, each carrying its compressed size in the "BC" extra subfield, plus the empty EOF member."""
+    import struct
+    import zlib
+    out = []
+
+    def member(data: bytes) -> bytes:
+        c = zlib.compressobj(level, zlib.DEFLATED, -15)
+        body = c.compress(data) + c.flush()
+        bsize = 18 + len(body) + 8 - 1
+        head = b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff" + struct.pack("<H", 6) + b"BC" + \
+            struct.pack("<HH", 2, bsize)
+        return head + body + struct.pack("<II", zlib.crc32(data) & 0xFFFFFFFF, len(data) & 0xFFFFFFFF)
+
+    for i in range(0, len(raw), block):
+        out.append(member(raw[i:i + block]))
+    if eof:
+        out.append(member(b""))
+    return b"".join(out)

@@ -33,11 +33,42 @@ typedef struct {
   uint64_t members;        /* gzip members seen */
 } dpgz_result;
 
+typedef struct {
+  uint64_t in_byte;        /* as dpgz_point */
+  uint64_t out_byte;
+  uint32_t bits;
+  uint32_t member_start;
+  int32_t prev_byte;       /* the inflated byte before out_byte, -1 at 0 */
+  uint32_t window_len;     /* bytes of this point's window in the blob dpgz_stream_take returns (0: member start) */
+} dpgz_point_ex;
+
+typedef struct dpgz_stream dpgz_stream;
+
 int dpgz_abi_version(void);
 /* Inflate a (multi-member) gzip stream; access points every `span` output bytes at deflate block
  * boundaries plus every member start.  out_hint: expected inflated size (0: guess). */
 int dpgz_build(const uint8_t* gz, uint64_t gz_len, uint64_t span, uint64_t out_hint, dpgz_result** result);
 void dpgz_free(dpgz_result* result);
+
+/* Streaming build: feed compressed bytes as they arrive (in_final = 1 with the last ones), get inflated
+ * bytes into `out` (at most out_cap; the call returns when the input is used up, the output is full or the
+ * stream ends: *at_end).  Access points found on the way queue up with their 32 KiB windows until taken. */
+int dpgz_stream_new(uint64_t span, dpgz_stream** out);
+void dpgz_stream_free(dpgz_stream* s);
+int dpgz_stream_inflate(dpgz_stream* s, const uint8_t* in, uint64_t in_len, int in_final, uint8_t* out,
+                        uint64_t out_cap, uint64_t* consumed, uint64_t* produced, int* at_end);
+int dpgz_stream_take(dpgz_stream* s, dpgz_point_ex* pts, uint64_t max_pts, uint8_t* windows, uint64_t win_cap,
+                     uint64_t* n_pts, uint64_t* n_win);
+int dpgz_stream_state(dpgz_stream* s, uint64_t* in_total, uint64_t* out_total, uint64_t* members,
+                      uint64_t* pending_pts, uint64_t* pending_win);
+
+/* BGZF-style members (FEXTRA "BC" subfield = compressed size - 1; ISIZE = inflated size): list the complete
+ * members at the start of `gz` (*used = bytes they span; DPGZ_ERR_ZLIB if a member is not of this kind),
+ * then inflate any of them independently on `threads` threads, each to out + out_off[i]. */
+int dpgz_bgzf_scan(const uint8_t* gz, uint64_t len, uint64_t* in_off, uint64_t* in_len, uint64_t* out_len,
+                   uint64_t cap, uint64_t* n, uint64_t* used);
+int dpgz_inflate_members(const uint8_t* gz, const uint64_t* in_off, const uint64_t* in_len, const uint64_t* out_off,
+                         const uint64_t* out_len, uint64_t n, uint8_t* out, int threads);
 
 #ifdef __cplusplus
 }

@@ -101,13 +101,31 @@ int dp_delim_index_async(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, ui
                          uint64_t end, uint32_t delim, uint32_t every_k, uint32_t emit_add, void* d_out,
                          int out_u64, uint64_t cap);
 int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
+/*
+ * General form: ascending, non-overlapping object ranges ranges[2*i] .. ranges[2*i+1] (inside the buffer)
+ * scanned as ONE delimiter stream whose ordinals start at `carry` (the delimiters before the first range,
+ * e.g. of the pieces of an inflated stream already indexed), so every_k selection continues across
+ * launches: entries are the g with (carry + g) % every_k == every_k - 1, written from d_out[0]; *n_out =
+ * (carry + n_delims) / every_k - carry / every_k.
+ *   out_mode 0: uint32 (DP_ERR_OVERFLOW at >= 2^32), 1: uint64, 2: uint32 low words (a paged index: split the
+ *   ranges at multiples of 2^32 and read each page's first entry from range_end).
+ *   range_end (host array of nranges, may be NULL): delimiters up to and including range i.
+ */
+int dp_delim_ranges_async(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base,
+                          const uint64_t* ranges, uint64_t nranges, uint32_t delim, uint32_t every_k,
+                          uint32_t emit_add, uint64_t carry, void* d_out, int out_mode, uint64_t cap);
+int dp_delim_ranges_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims, uint64_t* range_end);
 
 /* First object offset >= from holding `delim` in the buffer, or -1 (seek+readline of fasta.py:45-56). */
 int dp_find_delim(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, uint64_t from,
                   uint32_t delim, int64_t* pos);
 
-/* Calibration: read `bytes` (16-byte aligned) with a plain streaming kernel (async, timed like the scans). */
+/* Calibration (async, timed like the scans): read `bytes` (16-byte multiple) once with the best plain
+ * streaming kernel measured (the read-only ceiling next to the roofline fraction); dp_stream_rw also writes
+ * write_q16 / 65536 output bytes per input byte (contiguous, non-temporal), the DELIM index's traffic mix.
+ * blocks_per_cu <= 0: one 1024-thread workgroup per CU. */
 int dp_stream_read(dp_ctx* ctx, const void* d_buf, uint64_t bytes, int blocks_per_cu);
+int dp_stream_rw(dp_ctx* ctx, const void* d_in, uint64_t bytes, void* d_out, uint32_t write_q16, int blocks_per_cu);
 
 /* Kernel timing: HIP events around every scan-kernel launch on the ctx stream (off by default). */
 int dp_timing_enable(dp_ctx* ctx, int enable);

@@ -212,13 +212,21 @@ def test_vcf_line_index_and_partitions(monkeypatch):
 
 
 # ------------------------------------------------------------------------------------------------ FASTQ.gz
-def test_fastq_gz_reads():
+@pytest.mark.parametrize("kind,piece", [("multi", 64 << 20), ("multi", 200_003), ("bgzf", 300_007), ("bgzf", 64 << 20)])
+def test_fastq_gz_reads(kind, piece):
+    """FASTQ.gz preprocess through the streamed pipeline on the GPU (scan/gzindex.py): pieces of ``piece``
+    inflated bytes, so read ends straddle piece boundaries (and gzip member boundaries: two members of
+    different levels, or BGZF's 64 KiB members inflated on a thread pool); every read end equals the
+    reads' own line ends and the reference's read batches yield every line in order."""
     from dataplug_amd.formats.genomics.fastq import FASTQGZip, load_read_index, partition_reads_batches
     raw = synth.fastq(20_000, seed=4).tobytes()
-    blob = gzip.compress(raw[:1_000_003], 6) + gzip.compress(raw[1_000_003:], 1)     # two members
-    co = _co(FASTQGZip, blob, "r.fastq.gz", _mem("gpu_fastq"))
-    co.preprocess(extra_args={"span": 1 << 16})
-    assert co.attributes.gzip_members == 2
+    if kind == "multi":
+        blob = gzip.compress(raw[:1_000_003], 6) + gzip.compress(raw[1_000_003:], 1)     # two members
+    else:
+        blob = synth.bgzf(raw)
+    co = _co(FASTQGZip, blob, f"r_{kind}_{piece}.fastq.gz", _mem(f"gpu_fastq_{kind}_{piece}"))
+    co.preprocess(extra_args={"span": 1 << 16, "piece_bytes": piece})
+    assert co.attributes.gzip_members == (2 if kind == "multi" else -(-len(raw) // 65280) + 1)
     lines = raw.split(b"\n")[:-1]
     assert co.attributes.total_lines == len(lines) == 80_000
     ends = load_read_index(co)

@@ -327,3 +327,55 @@ def test_concurrent_threads_one_device():
 
     with cf.ThreadPoolExecutor(4) as ex:
         assert all(ex.map(worker, range(4)))
+
+
+@pytest.mark.parametrize("k,add", [(1, 0), (4, 1), (3, 0)])
+def test_delim_pieces_with_carry_equal_whole(ctx, k, add):
+    """A stream indexed piece by piece (FASTQ.gz: inflated pieces as they come): each launch continues the
+    every_k selection from the carried delimiter count, so the pieces' outputs concatenate to the whole."""
+    a = synth.fastq(30_000, seed=8)
+    whole, nd_whole = dpref.delim(a, 0, len(a), 10, k, add)
+    rng = np.random.default_rng(5)
+    cuts = np.sort(rng.choice(np.arange(1, len(a)), 9, replace=False)).tolist()
+    bounds = [0] + cuts + [len(a)]
+    d = ctx.workspace("t_in", len(a) + 64)
+    ctx.h2d(d.ptr, a)
+    got, carry = [], 0
+    for lo, hi in zip(bounds[:-1], bounds[1:]):
+        out, nd, ends = ctx.delim_ranges(d.ptr + lo, hi - lo, lo, [(lo, hi)], 10, k, add, carry=carry)
+        assert int(ends[-1]) == nd == int(np.count_nonzero(a[lo:hi] == 10))
+        got.append(out)
+        carry += nd
+    assert carry == nd_whole and np.array_equal(np.concatenate(got), whole)
+
+
+def test_delim_ranges_with_gaps_and_empty(ctx):
+    a = synth.vcf(3 << 20, seed=12)
+    d = ctx.workspace("t_in", len(a) + 64)
+    ctx.h2d(d.ptr, a)
+    ranges = [(0, 1000), (1000, 1000), (5000, 700_001), (700_001, 700_001), (1_000_000, 2_500_003),
+              (3_000_000, len(a))]
+    exp = np.concatenate([dpref.delim(a, lo, hi)[0] for lo, hi in ranges])
+    got, nd, ends = ctx.delim_ranges(d.ptr, len(a), 0, ranges)
+    assert np.array_equal(got, exp) and nd == len(exp)
+    assert ends.tolist() == np.cumsum([len(dpref.delim(a, lo, hi)[0]) for lo, hi in ranges]).tolist()
+    got4, nd4, _ = ctx.delim_ranges(d.ptr, len(a), 0, ranges, every_k=4, emit_add=1)
+    assert np.array_equal(got4, exp[3::4] + np.uint64(1))
+
+
+def test_delim_low_words_across_4gib_boundary(ctx):
+    """out_mode 2 (paged uint32 index): object bytes straddling offset 2^32, ranges split there; the low
+    words plus each page's first entry (range_end) rebuild the uint64 offsets."""
+    a = synth.csv((6 << 20) + 3, seed=14)
+    base = (1 << 32) - (3 << 20) - 7
+    d = ctx.workspace("t_in", len(a) + 64)
+    ctx.h2d(d.ptr, a)
+    split = 1 << 32
+    ranges = [(base, split), (split, base + len(a))]
+    with pytest.raises(OverflowError):
+        ctx.delim_ranges(d.ptr, len(a), base, ranges, out_mode=0)
+    low, nd, ends = ctx.delim_ranges(d.ptr, len(a), base, ranges, out_mode=2)
+    exp = dpref.delim(a, 0, len(a))[0] + np.uint64(base)
+    page = np.zeros(nd, np.uint64)
+    page[int(ends[0]):] = 1
+    assert np.array_equal((page << np.uint64(32)) | low.astype(np.uint64), exp)
