@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--size", type=int, default=None,
                    help="bytes per GPU (default 4 GiB fasta, 32 GiB csv) / object bytes (vcf, default 64 GiB)")
     p.add_argument("--chunks", type=int, default=4, help="FASTA map chunks per GPU (chunk_size = size / (chunks*N))")
+    p.add_argument("--index-dtype", choices=["u32p", "u64"], default="u32p",
+                   help="csv/vcf newline index form: u32p = uint32 low words + 4 GiB page counts (what "
+                        "co.preprocess stores), u64 = plain uint64 offsets")
     p.add_argument("--devices", default=None,
                    help="thread mode: comma-separated device of each worker (default 0..N-1)")
     p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) point")
@@ -194,21 +197,27 @@ class Steps:
         return dt, kern, res
 
 
-def stream_peak(ctx, d_ptr, nbytes, reps=5):
-    """Best read rate (B/s) of the plain read-only stream kernel over this buffer (measured roofline)."""
-    best = 0.0
+def stream_peak(ctx, d_ptr, nbytes, reps=5, write_per_read=0.0, d_out=0):
+    """Rate (B/s, read + written bytes) of the calibration stream kernel over this buffer: read-only (the
+    measured read roofline), or reading it while writing ``write_per_read`` bytes per input byte contiguously
+    (the measured ceiling of a scan that also writes its index: HBM reads and writes share the bus)."""
     n16 = nbytes // 16 * 16
-    for bpc in (4, 8):
-        ctx.stream_read(d_ptr, n16, bpc)
-        ctx.sync()
-        ctx.timing(True)
-        ctx.timing_read()
-        for _ in range(reps):
-            ctx.stream_read(d_ptr, n16, bpc)
-        ms, n = ctx.timing_read()
-        ctx.timing(False)
-        best = max(best, n16 / (ms / 1e3 / max(1, n)))
-    return best
+
+    def go():
+        if write_per_read:
+            ctx.stream_rw(d_ptr, n16, d_out, write_per_read)
+        else:
+            ctx.stream_read(d_ptr, n16)
+
+    go()
+    ctx.sync()
+    ctx.timing(True)
+    ctx.timing_read()
+    for _ in range(reps):
+        go()
+    ms, n = ctx.timing_read()
+    ctx.timing(False)
+    return n16 * (1.0 + write_per_read) / (ms / 1e3 / max(1, n))
 
 
 # ------------------------------------------------------------------------------------------ CPU baseline
@@ -336,6 +345,8 @@ def load_traffic(args, size, kernel):
     if pmc.get("object_bytes", size) != size or "hbm_traffic_bytes" not in pmc \
             or not pmc.get("kernel", kernel).startswith(kernel):
         return None, None
+    if args.workload != "fasta" and pmc.get("index_dtype", "u64") != args.index_dtype:
+        return None, None                              # a profile of the other index form
     return pmc["hbm_traffic_bytes"], os.path.relpath(os.path.realpath(path), REPO)
 
 
@@ -520,11 +531,15 @@ def main_fasta(args, world, rank, devs, team):
 def delim_worker(args, team, k, world, dev, keep_host):
     """configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3] (vcf: ONE
     64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong scaling): the
-    uint64 newline index (dp_delim_index), device-resident, timed like the FASTA line."""
+    newline index as co.preprocess builds it — uint32 low words with the ranges split at 4 GiB page
+    boundaries (dp_delim_ranges out_mode 2; --index-dtype u64: plain uint64) — device-resident, timed like
+    the FASTA line."""
     from dataplug_amd import synth
     from dataplug_amd.dist import rank_byte_range
     from dataplug_amd.scan import ScanContext
+    from dataplug_amd.scan.objects import page_ranges
     csv_mode = args.workload == "csv"
+    paged = args.index_dtype == "u32p"
     size = args.size or ((32 << 30) if csv_mode else (64 << 30))
     t0 = time.perf_counter()
     obj = synth.tiled_csv(size, seed=9 + k) if csv_mode else synth.tiled_vcf(size, seed=9)
@@ -541,35 +556,48 @@ def delim_worker(args, team, k, world, dev, keep_host):
     del stage
     gen_s = time.perf_counter() - t0
     cap = n_exp + 1024
-    d_outs = (ctxs[0].workspace("bench_out", 8 * cap), ctxs[1].workspace("bench_out", 8 * cap))
+    item = 4 if paged else 8
+    d_outs = (ctxs[0].workspace("bench_out", item * cap), ctxs[1].workspace("bench_out", item * cap))
+    rg = np.ascontiguousarray(np.asarray(page_ranges(begin, end) if paged else [(begin, end)], np.uint64).reshape(-1))
+    nr = len(rg) // 2
 
     def launch(i):
-        ctxs[i % 2].delim_index_async(d_in.ptr, nbytes, begin, begin, end, 10, 1, 0, d_outs[i % 2].ptr, True, cap)
+        ctxs[i % 2].delim_ranges_async(d_in.ptr, nbytes, begin, rg, 10, 1, 0, 0, d_outs[i % 2].ptr,
+                                       2 if paged else 1, cap)
 
     def collect(i):
-        return ctxs[i % 2].delim_result()
+        return ctxs[i % 2].delim_ranges_result(nr)
 
     S = Steps(team, ctxs, launch, collect)
     team.barrier()
     S.warm(args.warmup)
     dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
-    dt, _, (n_out, _) = S.timed(args.steps)
+    dt, _, (n_out, _, ends) = S.timed(args.steps)
     dt_ov, _, _ = S.timed(args.steps, serialize=False)
     verified = None
     if not args.no_verify:
         # every offset, against the object's analytic newline positions (synth.TiledText)
-        got = ctxs[0].d2h(np.empty(n_out, np.uint64), d_outs[(args.steps - 1) % 2].ptr)
+        got = ctxs[0].d2h(np.empty(n_out, np.uint32 if paged else np.uint64), d_outs[(args.steps - 1) % 2].ptr)
+        page_first = [0] + [int(e) for e in ends[:-1]]          # entry index where each page range starts
+        page_of = [int(rg[2 * j]) >> 32 for j in range(nr)]
         ok, i = n_out == n_exp, 0
         for piece in obj.delims_range(begin, end):
             if not ok:
                 break
-            ok = np.array_equal(got[i:i + len(piece)], piece)
+            seg = got[i:i + len(piece)].astype(np.uint64)
+            if paged:                                            # rebuild uint64 from the page of each entry
+                j = np.searchsorted(np.asarray(page_first[1:], np.int64), np.arange(i, i + len(piece)), side="right")
+                seg |= np.asarray(page_of, np.uint64)[j] << np.uint64(32)
+            ok = np.array_equal(seg, piece)
             i += len(piece)
         verified = bool(ok and i == n_out)
         del got
+    wpr = item * n_out / nbytes
+    d_mix = ctxs[0].workspace("bench_mix", int(wpr * nbytes) + (1 << 20))
     out = {"dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn), "scanned": nbytes, "offsets": n_out,
-           "alg_bytes": nbytes + 8 * n_out, "verified": verified, "gen_s": gen_s, "size": size,
-           "stream_peak": stream_peak(ctxs[0], d_in.ptr, nbytes)}
+           "alg_bytes": nbytes + item * n_out, "verified": verified, "gen_s": gen_s, "size": size,
+           "stream_peak": stream_peak(ctxs[0], d_in.ptr, nbytes),
+           "mixed_peak": stream_peak(ctxs[0], d_in.ptr, nbytes, write_per_read=wpr, d_out=d_mix.ptr)}
     if keep_host:
         out["host"] = obj.bytes_range(begin, min(end, begin + (1 << 30)))
     for c in ctxs:
@@ -594,12 +622,14 @@ def main_delim(args, world, rank, devs, team):
     kern = max(r["kern_s"] for r in allres)
     ach = min(r["alg_bytes"] / r["kern_s"] for r in allres)
     peak_meas = min(r["stream_peak"] for r in allres)
+    mixed = min(r["mixed_peak"] for r in allres)
     cpu = cpu_baseline_delim(host) if host is not None else None
     traffic, traffic_src = load_traffic(args, allres[0]["scanned"], "scan_kernel<1") if world == 1 else (None, None)
     name = "CSV" if csv_mode else "VCF"
-    cfg = (f"'\\n' index (uint64), {size / GiB:g} GiB cities.csv-shaped object per GPU (BASELINE configs[2])"
+    idx = "uint32 low words + 4 GiB pages" if args.index_dtype == "u32p" else "uint64"
+    cfg = (f"'\\n' index ({idx}), {size / GiB:g} GiB cities.csv-shaped object per GPU (BASELINE configs[2])"
            if csv_mode else
-           f"'\\n' index (uint64) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
+           f"'\\n' index ({idx}) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
            f"(BASELINE configs[3])")
     out = {
         "metric": f"GiB/s scanned (device-resident) + offsets/s, {name} newline index",
@@ -625,8 +655,14 @@ def main_delim(args, world, rank, devs, team):
                      "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                      "kernel": "scan_kernel<DELIM>", "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(allres[0]["alg_bytes"]),
+                     "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)" % (
+                         4 if args.index_dtype == "u32p" else 8),
                      "measured_peak": round(peak_meas / 1e9, 1),
-                     "frac_of_measured_peak": round(ach / peak_meas, 4)},
+                     "frac_of_measured_peak": round(ach / peak_meas, 4),
+                     "measured_mixed_peak": round(mixed / 1e9, 1),
+                     "frac_of_mixed_peak": round(ach / mixed, 4),
+                     "note": "measured_peak: read-only stream kernel; measured_mixed_peak: the same kernel also "
+                             "writing the index's bytes per input byte (same run, same buffer)"},
         "cpu_baseline": cpu,
         "verified_bit_exact": None if args.no_verify else all(r["verified"] for r in allres),
         "gen_s": round(max(r["gen_s"] for r in allres), 2),

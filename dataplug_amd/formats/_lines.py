@@ -1,8 +1,10 @@
 """Newline index artefact shared by the CSV and VCF plugins, and the slice boundaries derived from it.
 
 The reference finds CSV/VCF slice boundaries at ``get()`` time by scanning a padded byte range in Python
-(csv.py:52-105, vcf.py:88-149).  Here ``preprocess`` builds the sorted ``uint64`` offsets of every ``'\\n'``
-on the GPU once, stores them at ``s3://<bucket>.meta/<key>.lines``, and a partition strategy resolves each
+(csv.py:52-105, vcf.py:88-149).  Here ``preprocess`` builds the sorted offsets of every ``'\\n'`` on the GPU
+once — as uint32 low words plus the entry count below each 4 GiB page boundary (the GPU writes half the
+bytes of a uint64 index; the pages live in the attributes) — stores them at ``s3://<bucket>.meta/<key>.lines``,
+and a partition strategy resolves each
 slice's exact byte range from that index, reproducing the reference's ``get()`` output (SURVEY.md §8(a)
 formulas, restated below with the clamps the reference's buffer arithmetic implies).
 """
@@ -20,27 +22,40 @@ _PRELOAD_BYTES = 256 << 20
 _BLOCK = 8192                      # entries per cached block for large indexes
 
 
-def store_line_index(cloud_object, offsets: np.ndarray) -> str:
+def store_line_index(cloud_object, offsets) -> dict:
+    """PUT the index at ``<key>.lines``; returns the attributes that describe it.
+
+    A ``scan.objects.PagedOffsets`` (the default build) is stored as uint32 LE low words, its 4 GiB page
+    counts in the attributes (``line_index_dtype="u32p"``, ``line_index_pages``); a plain array as uint64 LE."""
     key = cloud_object.meta_path.key + LINES_SUFFIX
-    cloud_object.storage.put_object(Body=np.ascontiguousarray(offsets, dtype="<u8").tobytes(),
-                                    Bucket=cloud_object.meta_path.bucket, Key=key,
+    paged = hasattr(offsets, "pages")
+    body = np.ascontiguousarray(offsets.low if paged else offsets, dtype="<u4" if paged else "<u8").tobytes()
+    cloud_object.storage.put_object(Body=body, Bucket=cloud_object.meta_path.bucket, Key=key,
                                     Metadata={"dataplug": __version__})
-    return key
+    attrs = {"line_index_key": key, "num_lines": int(len(offsets))}
+    if paged:
+        attrs.update(line_index_dtype="u32p", line_index_pages=[int(x) for x in offsets.pages])
+    return attrs
 
 
 class LineIndex:
-    """Sorted newline offsets; ``nxt(x)`` = 1 + first '\\n' at or after x (None if none)."""
+    """Sorted newline offsets; ``nxt(x)`` = 1 + first '\n' at or after x (None if none).
+
+    Reads either stored form: uint64 words, or uint32 low words + page counts (``pages[p-1]`` = entries
+    below p * 2^32), fetching blocks by ranged GETs when the index is large."""
 
     def __init__(self, offsets: Optional[np.ndarray] = None, storage=None, bucket: str = "", key: str = "",
-                 count: Optional[int] = None):
+                 count: Optional[int] = None, pages: Optional[list] = None):
         self._arr = None if offsets is None else np.asarray(offsets, dtype=np.uint64)
         self._storage, self._bucket, self._key = storage, bucket, key
+        self._pages = None if pages is None else np.asarray(pages, np.int64)
+        self._item = 8 if pages is None else 4
         self._blocks: "OrderedDict[int, np.ndarray]" = OrderedDict()
         if self._arr is None:
             if count is None:
-                count = int(storage.head_object(Bucket=bucket, Key=key)["ContentLength"]) // 8
+                count = int(storage.head_object(Bucket=bucket, Key=key)["ContentLength"]) // self._item
             self.count = int(count)
-            if self.count * 8 <= _PRELOAD_BYTES:
+            if self.count * self._item <= _PRELOAD_BYTES:
                 self._arr = self._fetch(0, self.count)
         else:
             self.count = len(self._arr)
@@ -51,15 +66,21 @@ class LineIndex:
         key = getattr(attrs, "line_index_key", None) if attrs is not None else None
         if not key:
             raise KeyError(f"{cloud_object!r} has no newline index: preprocess it with dataplug_amd (line_index=True)")
+        paged = getattr(attrs, "line_index_dtype", None) == "u32p"
         return cls(storage=cloud_object.storage, bucket=cloud_object.meta_path.bucket, key=key,
-                   count=getattr(attrs, "num_lines", None))
+                   count=getattr(attrs, "num_lines", None),
+                   pages=list(getattr(attrs, "line_index_pages")) if paged else None)
 
     def _fetch(self, i0: int, i1: int) -> np.ndarray:
         if i1 <= i0:
             return np.zeros(0, np.uint64)
-        res = self._storage.get_object(Bucket=self._bucket, Key=self._key, Range=f"bytes={8 * i0}-{8 * i1 - 1}")
-        return np.frombuffer(res["Body"].read(), dtype="<u8").astype(np.uint64, copy=False)
-
+        it = self._item
+        res = self._storage.get_object(Bucket=self._bucket, Key=self._key, Range=f"bytes={it * i0}-{it * i1 - 1}")
+        raw = res["Body"].read()
+        if self._pages is None:
+            return np.frombuffer(raw, dtype="<u8").astype(np.uint64, copy=False)
+        page = np.searchsorted(self._pages, np.arange(i0, i1, dtype=np.int64), side="right").astype(np.uint64)
+        return (page << np.uint64(32)) | np.frombuffer(raw, dtype="<u4").astype(np.uint64)
     def _block(self, b: int) -> np.ndarray:
         blk = self._blocks.get(b)
         if blk is None:

@@ -35,9 +35,8 @@ def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index
     df = pd.read_csv(io.StringIO("\n".join(top)), sep=separator)
     attrs = {"columns": df.columns.tolist(), "dtypes": df.dtypes.tolist()}
     if line_index:
-        offsets = scan_objects.line_index_object(cloud_object)
-        attrs["line_index_key"] = store_line_index(cloud_object, offsets)
-        attrs["num_lines"] = int(len(offsets))
+        offsets = scan_objects.line_index_object(cloud_object, paged=True)
+        attrs.update(store_line_index(cloud_object, offsets))
     return PreprocessingMetadata(attributes=attrs)
 
 

@@ -64,9 +64,8 @@ def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True) -> Prep
         header, meta, columns, body_offset = parse_vcf_header(f)
     attrs = {"columns": columns, "vcf_attributes": meta, "body_offset": body_offset}
     if line_index:
-        offsets = scan_objects.line_index_object(cloud_object, begin=body_offset)
-        attrs["line_index_key"] = store_line_index(cloud_object, offsets)
-        attrs["num_lines"] = int(len(offsets))
+        offsets = scan_objects.line_index_object(cloud_object, begin=body_offset, paged=True)
+        attrs.update(store_line_index(cloud_object, offsets))
     return PreprocessingMetadata(attributes=attrs, metadata="\n".join(header).encode("utf-8"))
 
 

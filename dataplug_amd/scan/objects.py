@@ -191,48 +191,107 @@ def fasta_index_chunk(co, data, chunk_offset: int, job: int = 0, u64: bool = Fal
 
 
 # ------------------------------------------------------------------------------------------ newline / record index
-def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int):
+PAGE = 1 << 32
+
+
+def page_ranges(lo: int, hi: int) -> List[Tuple[int, int]]:
+    """[lo, hi) split at multiples of 2^32: the ranges of a paged (uint32 low word) newline index."""
+    out, p = [], lo
+    while p < hi:
+        q = min(hi, (p // PAGE + 1) * PAGE)
+        out.append((p, q))
+        p = q
+    return out
+
+
+@dataclass
+class PagedOffsets:
+    """Sorted object offsets as uint32 low words plus, for every 4 GiB page boundary p * 2^32 (p >= 1) below
+    the end of the scanned bytes, the number of offsets before it: offset i = (page(i) << 32) | low[i] with
+    page(i) = bisect_right(pages, i).  Half the bytes of a uint64 index, written by the GPU directly
+    (dp_delim_ranges out_mode 2), at the same information."""
+    low: np.ndarray
+    pages: List[int]
+
+    def __len__(self) -> int:
+        return len(self.low)
+
+    def to_u64(self, i0: int = 0, i1: Optional[int] = None) -> np.ndarray:
+        i1 = len(self.low) if i1 is None else i1
+        idx = np.arange(i0, i1, dtype=np.int64)
+        page = np.searchsorted(np.asarray(self.pages, np.int64), idx, side="right").astype(np.uint64)
+        return (page << np.uint64(32)) | self.low[i0:i1].astype(np.uint64)
+
+
+def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int, paged: bool = False):
     ctx = get_context(dev)
     n = hi - lo
     d = ctx.workspace("input", n + 64)
     fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, d.ptr)
-    return ctx.delim_index(d.ptr, n, lo, lo, hi, delim=delim, every_k=every_k, emit_add=emit_add, u64=True)
+    if not paged:
+        return ctx.delim_index(d.ptr, n, lo, lo, hi, delim=delim, every_k=every_k, emit_add=emit_add, u64=True)
+    rg = page_ranges(lo, hi)
+    low, nd, ends = ctx.delim_ranges(d.ptr, n, lo, rg, delim=delim, every_k=1, emit_add=0, out_mode=2)
+    return low, [(r, int(e)) for r, e in zip(rg, ends)]
+
+
+def line_parts(begin: int, end: int, n_devices: int, part_bytes: int = 16 << 30) -> List[Tuple[int, int]]:
+    """Raw byte parts of [begin, end) for a newline index (at most ``part_bytes`` each, at least one per
+    GPU); part k runs on GPU k mod n_devices and the parts' offsets concatenate to the whole index."""
+    if end <= begin:
+        return []
+    nparts = max(n_devices, -(-(end - begin) // part_bytes))
+    step = -(-(end - begin) // nparts)
+    bounds = [(begin + i * step, min(end, begin + (i + 1) * step)) for i in range(nparts)]
+    return [b for b in bounds if b[1] > b[0]]
 
 
 def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int = 10,
-                      max_devices: Optional[int] = None, part_bytes: int = 16 << 30) -> np.ndarray:
-    """Sorted uint64 offsets of every ``delim`` byte of object bytes [begin, end).
+                      max_devices: Optional[int] = None, part_bytes: int = 16 << 30, paged: bool = False):
+    """Sorted offsets of every ``delim`` byte of object bytes [begin, end): uint64, or with ``paged`` a
+    ``PagedOffsets`` (uint32 low words + 4 GiB page counts, the GPU writing half the bytes).
 
     The range is cut into independent parts (at most ``part_bytes`` each, at least one per GPU) scanned
     round-robin on the GPUs and concatenated in order."""
     end = co.size if end is None else end
     if end <= begin:
-        return np.zeros(0, np.uint64)
+        return PagedOffsets(np.zeros(0, np.uint32), []) if paged else np.zeros(0, np.uint64)
     devs = devices(max_devices, co)
-    nparts = max(len(devs), -(-(end - begin) // part_bytes))
-    step = -(-(end - begin) // nparts)
-    bounds = [(begin + i * step, min(end, begin + (i + 1) * step)) for i in range(nparts)]
-    bounds = [b for b in bounds if b[1] > b[0]]
+    bounds = line_parts(begin, end, len(devs), part_bytes)
 
     def run(k: int):
         lo, hi = bounds[k]
-        return _delim_group(devs[k % len(devs)], co, lo, hi, delim, 1, 0)[0]
+        r = _delim_group(devs[k % len(devs)], co, lo, hi, delim, 1, 0, paged=paged)
+        return r if paged else r[0]
 
     if len(bounds) == 1:
-        return run(0)
-    # one worker per GPU; parts of the same GPU run in order on that GPU's thread
-    by_dev = {}
-    for k in range(len(bounds)):
-        by_dev.setdefault(k % len(devs), []).append(k)
-    out = [None] * len(bounds)
+        out = [run(0)]
+    else:
+        # one worker per GPU; parts of the same GPU run in order on that GPU's thread
+        by_dev = {}
+        for k in range(len(bounds)):
+            by_dev.setdefault(k % len(devs), []).append(k)
+        out = [None] * len(bounds)
 
-    def worker(ks):
-        for k in ks:
-            out[k] = run(k)
+        def worker(ks):
+            for k in ks:
+                out[k] = run(k)
 
-    with cf.ThreadPoolExecutor(len(by_dev)) as ex:
-        list(ex.map(worker, by_dev.values()))
-    return np.concatenate(out)
+        with cf.ThreadPoolExecutor(len(by_dev)) as ex:
+            list(ex.map(worker, by_dev.values()))
+    if not paged:
+        return np.concatenate(out)
+    # pages[p - 1] = offsets before p * 2^32: 0 for the boundaries at or below begin, then the running count
+    # at every boundary inside (begin, end) — each starts one of the parts' page ranges
+    pages, before = [0] * (begin // PAGE), 0
+    for _, ranges in out:
+        prev = 0
+        for (lo, hi), cum in ranges:
+            if lo % PAGE == 0 and lo > begin:
+                pages.append(before)
+            before += cum - prev
+            prev = cum
+    return PagedOffsets(np.concatenate([o[0] for o in out]), pages)
 
 
 def record_index_bytes(data, delim: int = 10, every_k: int = 1, emit_add: int = 0, device: int = 0,

@@ -111,3 +111,18 @@ def test_two_rank_gloo(tmp_path):
     tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
     body_nl = cpu_ref.delim_index(tv.bytes_range(0, tv.size), len(tv.head), tv.size).tolist()
     assert res[0]["nl"] + res[1]["nl"] == body_nl
+
+
+def test_line_parts_cover_in_order():
+    from dataplug_amd.scan.objects import line_parts, page_ranges
+    for begin, end, g, pb in [(0, 100, 3, 1000), (1337, 64 << 30, 8, 16 << 30), (5, 5, 4, 10), (0, 7, 8, 100)]:
+        parts = line_parts(begin, end, g, pb)
+        if end > begin:
+            assert parts[0][0] == begin and parts[-1][1] == end
+            assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+            assert all(hi - lo <= pb for lo, hi in parts)
+        else:
+            assert parts == []
+    G = 1 << 30
+    assert page_ranges(3 * G, 9 * G) == [(3 * G, 4 * G), (4 * G, 8 * G), (8 * G, 9 * G)]
+    assert page_ranges(4 * G, 8 * G) == [(4 * G, 8 * G)]

@@ -44,6 +44,14 @@ def _index(co):
                          np.uint32)
 
 
+def _lines_u64(co):
+    """The stored newline index (uint32 low words + page counts) as uint64 offsets."""
+    from dataplug_amd.formats._lines import LineIndex
+    assert co.attributes.line_index_dtype == "u32p"
+    li = LineIndex.of(co)
+    return li._fetch(0, li.count)
+
+
 def _mem(name):
     MemoryStore._named.pop(name, None)
     return {"endpoint_url": f"memory://{name}"}
@@ -167,8 +175,7 @@ def test_csv_line_index_and_partitions(monkeypatch, devices):
         co = _co(fcsv.CSV, data, rec["object"] + devices, _mem(f"gpu_csv_{rec['object']}_{len(devices)}"))
         co.preprocess()
         assert co.attributes.columns == rec["columns"]
-        lines = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.attributes.line_index_key)
-                              ["Body"].read(), "<u8")
+        lines = _lines_u64(co)
         assert np.array_equal(lines, np.flatnonzero(np.frombuffer(data, np.uint8) == 10))
         for n, expected in rec["num_chunks"].items():
             for s, e in zip(co.partition(fcsv.partition_num_chunks, num_chunks=int(n)), expected):
@@ -186,8 +193,7 @@ def test_csv_large_multi_part(monkeypatch):
     data = synth.csv(96 << 20, 9)
     co = _co(fcsv.CSV, data.tobytes(), "big.csv", _mem("gpu_csv_big"))
     co.preprocess()
-    lines = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.attributes.line_index_key)
-                          ["Body"].read(), "<u8")
+    lines = _lines_u64(co)
     assert np.array_equal(lines, np.flatnonzero(data == 10))
     from oracle import cpu_ref
     obj = data.tobytes()

@@ -98,3 +98,58 @@ def test_header_cut_by_chunk_end_far_before_buffer_end(ctx):
     for c in cuts:
         nl = int(np.flatnonzero(host[c:c + 4096] == 10)[0]) + c
         assert ctx.find_delim(d.ptr, size, 0, c, 10) == nl
+
+
+def _check_delims(ctx, obj, lo, hi, d_ptr, stage):
+    """Newline index of object bytes [lo, hi) (uploaded 4 GiB at a time) against the TiledText analytic
+    offsets: every offset compared."""
+    step = 4 * GiB
+    for p in range(lo, hi, step):
+        q = min(hi, p + step)
+        ctx.h2d(d_ptr + (p - lo), obj.bytes_range(p, q, out=stage))
+    got, nd = ctx.delim_index(d_ptr, hi - lo, lo, lo, hi, delim=10, u64=True, cap=obj.count_range(lo, hi) + 64)
+    i = 0
+    for piece in obj.delims_range(lo, hi):
+        assert np.array_equal(got[i:i + len(piece)], piece), (lo, hi, i)
+        i += len(piece)
+    assert i == len(got) == nd
+    return nd
+
+
+def test_csv_32gib_configs2_every_offset(ctx):
+    """BASELINE configs[2]: the newline index (uint64) of a 32 GiB cities.csv-shaped object in one launch,
+    every one of its ~963 M offsets compared with the object's analytic newline positions."""
+    size = 32 * GiB
+    obj = synth.tiled_csv(size, seed=9)
+    d = ctx.workspace("full_in", size + 64)
+    stage = np.empty(4 * GiB, np.uint8)
+    nd = _check_delims(ctx, obj, 0, size, d.ptr, stage)
+    assert nd > 900_000_000
+
+
+def test_vcf_64gib_configs3_eight_parts():
+    """BASELINE configs[3]: one 64 GiB VCF whose body [body_offset, size) is cut by the product's part split
+    (scan.objects.line_parts) into 8 parts, one worker thread and context per part as
+    DATAPLUG_AMD_DEVICES=0,0,0,0,0,0,0,0 runs them; every offset of every part exact, and the parts'
+    indexes concatenate to the whole body's."""
+    import concurrent.futures as cf
+    from dataplug_amd.scan import ScanContext
+    from dataplug_amd.scan.objects import line_parts
+    size = 64 * GiB
+    obj = synth.tiled_vcf(size, seed=9)
+    parts = line_parts(len(obj.head), size, 8)
+    assert len(parts) == 8 and parts[0][0] == len(obj.head) and parts[-1][1] == size
+    assert all(parts[i][1] == parts[i + 1][0] for i in range(7))
+
+    def run(k):
+        lo, hi = parts[k]
+        c = ScanContext(0)
+        try:
+            d = c.workspace("in", hi - lo + 64)
+            return _check_delims(c, obj, lo, hi, d.ptr, np.empty(min(4 * GiB, hi - lo), np.uint8))
+        finally:
+            c.close()
+
+    with cf.ThreadPoolExecutor(4) as ex:            # 4 in flight: bounds host staging at 16 GiB
+        counts = list(ex.map(run, range(8)))
+    assert sum(counts) == obj.count_range(len(obj.head), size) > 800_000_000

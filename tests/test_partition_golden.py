@@ -18,6 +18,7 @@ from dataplug_amd import synth
 from dataplug_amd.cloudobject import CloudObject
 from dataplug_amd.entities import get_slices
 from dataplug_amd.formats._lines import SliceError, store_line_index
+from dataplug_amd.scan.objects import PagedOffsets
 from dataplug_amd.preprocessing.handler import upload_metadata
 from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
 from dataplug_amd.storage import MemoryStore
@@ -30,7 +31,7 @@ def _load(name):
         return json.load(f)
 
 
-def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, begin=0):
+def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, begin=0, paged=True):
     store = f"golden_{name}_{fmt.co_class.__name__}"
     MemoryStore._named.pop(store, None)
     co = CloudObject.from_s3(fmt, f"s3://dataplug/{name}", fetch=False, s3_config={"endpoint_url": f"memory://{store}"})
@@ -40,7 +41,7 @@ def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, b
     if nl:
         arr = np.frombuffer(data, np.uint8)
         off = np.flatnonzero(arr[begin:] == 10).astype(np.uint64) + np.uint64(begin)
-        attrs = dict(attrs, line_index_key=store_line_index(co, off), num_lines=len(off))
+        attrs = dict(attrs, **store_line_index(co, PagedOffsets(off.astype(np.uint32), []) if paged else off))
     upload_metadata(co, PreprocessingMetadata(metadata=meta, attributes=attrs))
     co.fetch()
     return co
@@ -70,11 +71,12 @@ def _vcf_objects():
         yield rec, data
 
 
-def test_csv_partitions_match_reference():
+@pytest.mark.parametrize("paged", [True, False])
+def test_csv_partitions_match_reference(paged):
     from dataplug_amd.formats.generic import csv as fcsv
     checked = 0
     for rec, data in _csv_objects():
-        co = _co(fcsv.CSV, rec["object"], data, {"columns": rec["columns"], "dtypes": rec["dtypes"]})
+        co = _co(fcsv.CSV, rec["object"], data, {"columns": rec["columns"], "dtypes": rec["dtypes"]}, paged=paged)
         cases = [(fcsv.partition_num_chunks, {"num_chunks": int(n)}, v) for n, v in rec["num_chunks"].items()]
         cases += [(fcsv.partition_chunk_size, {"chunk_size": int(c)}, v) for c, v in rec["chunk_size"].items()]
         for strat, kw, expected in cases:
@@ -93,12 +95,14 @@ def test_csv_partitions_match_reference():
     assert checked > 100
 
 
-def test_vcf_partitions_match_reference():
+@pytest.mark.parametrize("paged", [True, False])
+def test_vcf_partitions_match_reference(paged):
     from dataplug_amd.formats.genomics import vcf as fvcf
     for rec, data in _vcf_objects():
         co = _co(fvcf.VCF, rec["object"], data,
                  {"columns": rec["columns"], "vcf_attributes": rec["vcf_attributes"],
-                  "body_offset": rec["body_offset"]}, meta=rec["meta"].encode(), begin=rec["body_offset"])
+                  "body_offset": rec["body_offset"]}, meta=rec["meta"].encode(), begin=rec["body_offset"],
+                 paged=paged)
         for n, expected in rec["num_chunks"].items():
             slices = co.partition(fvcf.partition_num_chunks, num_chunks=int(n))
             assert [[s.range_0, s.range_1] for s in slices] == [e[:2] for e in expected]
@@ -161,3 +165,32 @@ def test_fastq_read_batches_match_reference():
     with pytest.raises(Exception) as e:
         read_pairs(10, 2)
     assert str(e.value) == g["non_multiple_of_4_error"]
+
+
+@pytest.mark.parametrize("preload", [True, False])
+def test_paged_line_index_across_4gib_pages(monkeypatch, preload):
+    """The stored paged form (uint32 low words + entries below each 4 GiB boundary) read back by LineIndex,
+    preloaded or block by block over ranged GETs: the same answers as the uint64 offsets."""
+    from dataplug_amd.formats import _lines
+    from dataplug_amd.scan.objects import PagedOffsets
+    if not preload:
+        monkeypatch.setattr(_lines, "_PRELOAD_BYTES", 1024)
+    rng = np.random.default_rng(3)
+    G = 1 << 30
+    off = np.unique(rng.integers(3 * G, 17 * G, 50_000).astype(np.uint64))
+    pages = [int(np.searchsorted(off, np.uint64(p << 32))) for p in range(1, 5)]   # boundaries 4, 8, 12, 16 GiB
+    co = _co(_lines_fmt(), "paged", b"x" * 16, {}, nl=False)
+    attrs = store_line_index(co, PagedOffsets(off.astype(np.uint32), pages))
+    assert attrs["line_index_dtype"] == "u32p" and attrs["line_index_pages"] == pages
+    li = _lines.LineIndex(storage=co.storage, bucket=co.meta_path.bucket, key=attrs["line_index_key"],
+                          count=attrs["num_lines"], pages=attrs["line_index_pages"])
+    assert np.array_equal(li._fetch(0, li.count), off)
+    for x in [0, 3 * G, 4 * G - 1, 4 * G, 4 * G + 1, 8 * G + 12345, 16 * G, 17 * G, int(off[777]), int(off[-1]) + 1]:
+        i = int(np.searchsorted(off, np.uint64(x)))
+        assert li.nxt(x) == (int(off[i]) + 1 if i < len(off) else None), x
+        assert li.contains(x) == (i < len(off) and int(off[i]) == x)
+
+
+def _lines_fmt():
+    from dataplug_amd.formats.generic.csv import CSV
+    return CSV
