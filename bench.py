@@ -59,9 +59,9 @@ def parse():
     p.add_argument("--size", type=int, default=None,
                    help="bytes per GPU (default 4 GiB fasta, 32 GiB csv) / object bytes (vcf, default 64 GiB)")
     p.add_argument("--chunks", type=int, default=4, help="FASTA map chunks per GPU (chunk_size = size / (chunks*N))")
-    p.add_argument("--index-dtype", choices=["u32p", "u64"], default="u32p",
-                   help="csv/vcf newline index form: u32p = uint32 low words + 4 GiB page counts (what "
-                        "co.preprocess stores), u64 = plain uint64 offsets")
+    p.add_argument("--index-dtype", choices=["u16b", "u32p", "u64"], default="u16b",
+                   help="csv/vcf newline index form: u16b = uint16 low words + 64 KiB block table (what "
+                        "co.preprocess stores), u32p = uint32 low words + 4 GiB page counts, u64 = plain uint64")
     p.add_argument("--devices", default=None,
                    help="thread mode: comma-separated device of each worker (default 0..N-1)")
     p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) point")
@@ -539,7 +539,7 @@ def delim_worker(args, team, k, world, dev, keep_host):
     from dataplug_amd.scan import ScanContext
     from dataplug_amd.scan.objects import page_ranges
     csv_mode = args.workload == "csv"
-    paged = args.index_dtype == "u32p"
+    fmt = args.index_dtype
     size = args.size or ((32 << 30) if csv_mode else (64 << 30))
     t0 = time.perf_counter()
     obj = synth.tiled_csv(size, seed=9 + k) if csv_mode else synth.tiled_vcf(size, seed=9)
@@ -547,23 +547,26 @@ def delim_worker(args, team, k, world, dev, keep_host):
     nbytes = end - begin
     n_exp = obj.count_range(begin, end)
     ctxs = (ScanContext(dev), ScanContext(dev))
-    d_in = ctxs[0].workspace("bench_in", nbytes + 64)
+    d_buf = ctxs[0].workspace("bench_in", nbytes + 64)
+    d_ptr = d_buf.ptr + (begin & 15)                       # object offset and device address congruent mod 16
     step = 4 << 30                                           # materialize + upload 4 GiB at a time
     stage = np.empty(min(step, nbytes), np.uint8)
     for p in range(begin, end, step):
         q = min(end, p + step)
-        ctxs[0].h2d(d_in.ptr + (p - begin), obj.bytes_range(p, q, out=stage))
+        ctxs[0].h2d(d_ptr + (p - begin), obj.bytes_range(p, q, out=stage))
     del stage
     gen_s = time.perf_counter() - t0
     cap = n_exp + 1024
-    item = 4 if paged else 8
-    d_outs = (ctxs[0].workspace("bench_out", item * cap), ctxs[1].workspace("bench_out", item * cap))
-    rg = np.ascontiguousarray(np.asarray(page_ranges(begin, end) if paged else [(begin, end)], np.uint64).reshape(-1))
+    item = {"u16b": 2, "u32p": 4, "u64": 8}[fmt]
+    mode = {"u16b": 3, "u32p": 2, "u64": 1}[fmt]
+    rg = np.ascontiguousarray(np.asarray(page_ranges(begin, end) if fmt == "u32p" else [(begin, end)],
+                                         np.uint64).reshape(-1))
     nr = len(rg) // 2
+    ob = ScanContext.out_bytes(cap, mode, rg)
+    d_outs = (ctxs[0].workspace("bench_out", ob), ctxs[1].workspace("bench_out", ob))
 
     def launch(i):
-        ctxs[i % 2].delim_ranges_async(d_in.ptr, nbytes, begin, rg, 10, 1, 0, 0, d_outs[i % 2].ptr,
-                                       2 if paged else 1, cap)
+        ctxs[i % 2].delim_ranges_async(d_ptr, nbytes, begin, rg, 10, 1, 0, 0, d_outs[i % 2].ptr, mode, cap)
 
     def collect(i):
         return ctxs[i % 2].delim_ranges_result(nr)
@@ -577,17 +580,23 @@ def delim_worker(args, team, k, world, dev, keep_host):
     verified = None
     if not args.no_verify:
         # every offset, against the object's analytic newline positions (synth.TiledText)
-        got = ctxs[0].d2h(np.empty(n_out, np.uint32 if paged else np.uint64), d_outs[(args.steps - 1) % 2].ptr)
+        last = d_outs[(args.steps - 1) % 2].ptr
+        got = ctxs[0].d2h(np.empty(n_out, {"u16b": np.uint16, "u32p": np.uint32, "u64": np.uint64}[fmt]), last)
         page_first = [0] + [int(e) for e in ends[:-1]]          # entry index where each page range starts
         page_of = [int(rg[2 * j]) >> 32 for j in range(nr)]
+        tab = ctxs[0].block_table(last, cap, rg).astype(np.int64) if fmt == "u16b" else None
         ok, i = n_out == n_exp, 0
         for piece in obj.delims_range(begin, end):
             if not ok:
                 break
             seg = got[i:i + len(piece)].astype(np.uint64)
-            if paged:                                            # rebuild uint64 from the page of each entry
-                j = np.searchsorted(np.asarray(page_first[1:], np.int64), np.arange(i, i + len(piece)), side="right")
+            idx = np.arange(i, i + len(piece))
+            if fmt == "u32p":                                    # rebuild uint64 from the page of each entry
+                j = np.searchsorted(np.asarray(page_first[1:], np.int64), idx, side="right")
                 seg |= np.asarray(page_of, np.uint64)[j] << np.uint64(32)
+            elif fmt == "u16b":                                  # ... from the 64 KiB block of each entry
+                blk = np.searchsorted(tab, idx, side="right").astype(np.uint64) - np.uint64(1)
+                seg |= (blk + np.uint64(begin >> 16)) << np.uint64(16)
             ok = np.array_equal(seg, piece)
             i += len(piece)
         verified = bool(ok and i == n_out)
@@ -595,9 +604,10 @@ def delim_worker(args, team, k, world, dev, keep_host):
     wpr = item * n_out / nbytes
     d_mix = ctxs[0].workspace("bench_mix", int(wpr * nbytes) + (1 << 20))
     out = {"dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn), "scanned": nbytes, "offsets": n_out,
-           "alg_bytes": nbytes + item * n_out, "verified": verified, "gen_s": gen_s, "size": size,
-           "stream_peak": stream_peak(ctxs[0], d_in.ptr, nbytes),
-           "mixed_peak": stream_peak(ctxs[0], d_in.ptr, nbytes, write_per_read=wpr, d_out=d_mix.ptr)}
+           "alg_bytes": nbytes + item * n_out + (8 * ScanContext.block_table_size(rg)[1] if fmt == "u16b" else 0),
+           "verified": verified, "gen_s": gen_s, "size": size,
+           "stream_peak": stream_peak(ctxs[0], d_buf.ptr, nbytes),
+           "mixed_peak": stream_peak(ctxs[0], d_buf.ptr, nbytes, write_per_read=wpr, d_out=d_mix.ptr)}
     if keep_host:
         out["host"] = obj.bytes_range(begin, min(end, begin + (1 << 30)))
     for c in ctxs:
@@ -626,7 +636,8 @@ def main_delim(args, world, rank, devs, team):
     cpu = cpu_baseline_delim(host) if host is not None else None
     traffic, traffic_src = load_traffic(args, allres[0]["scanned"], "scan_kernel<1") if world == 1 else (None, None)
     name = "CSV" if csv_mode else "VCF"
-    idx = "uint32 low words + 4 GiB pages" if args.index_dtype == "u32p" else "uint64"
+    idx = {"u16b": "uint16 low words + 64 KiB block table", "u32p": "uint32 low words + 4 GiB pages",
+           "u64": "uint64"}[args.index_dtype]
     cfg = (f"'\\n' index ({idx}), {size / GiB:g} GiB cities.csv-shaped object per GPU (BASELINE configs[2])"
            if csv_mode else
            f"'\\n' index ({idx}) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
@@ -655,8 +666,9 @@ def main_delim(args, world, rank, devs, team):
                      "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                      "kernel": "scan_kernel<DELIM>", "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(allres[0]["alg_bytes"]),
-                     "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)" % (
-                         4 if args.index_dtype == "u32p" else 8),
+                     "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)%s" % (
+                         {"u16b": 2, "u32p": 4, "u64": 8}[args.index_dtype],
+                         " + 8 B per 64 KiB block" if args.index_dtype == "u16b" else ""),
                      "measured_peak": round(peak_meas / 1e9, 1),
                      "frac_of_measured_peak": round(ach / peak_meas, 4),
                      "measured_mixed_peak": round(mixed / 1e9, 1),

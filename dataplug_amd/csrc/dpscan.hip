@@ -169,6 +169,8 @@ struct ScanArgs {
   uint64_t cap;                // entries (FASTA: pairs)
   int out_u64;
   uint32_t wrap32;             // DELIM uint32 output as low words (paged index): no overflow check
+  unsigned long long* blocktab;  // DELIM uint16 output: entries before each 64 KiB boundary (index - tab_j0)
+  uint64_t tab_j0, tab_n;
   uint64_t carry;              // DELIM: delimiters before this launch's first byte (a streamed object's pieces)
   uint32_t delim;              // DELIM: byte replicated x4
   uint32_t every_k;
@@ -880,7 +882,8 @@ __device__ __forceinline__ void phase_a_rec(PhaseA& pa, const Geo& g, int wave, 
 template <int MODE, int OUT64>
 __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint32_t lohi, uint64_t P, uint32_t S,
                                         int lane) {
-  typedef typename std::conditional<OUT64 != 0, uint64_t, uint32_t>::type OutT;
+  typedef typename std::conditional<OUT64 == 1, uint64_t,
+                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
   const int lo = (int)(lohi & 0xFFFFu), hi = (int)(lohi >> 16);
   const int hi16 = (hi + 15) & ~15;
   const uint8_t* src = A.base + wbase;
@@ -889,7 +892,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
     return a + 16 <= hi16 ? *reinterpret_cast<const v4u*>(src + a) : v4u{0u, 0u, 0u, 0u};
   };
   const uint64_t obj_off = A.obj_base - A.shift + wbase;
-  const bool near4g = !OUT64 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+  const bool near4g = OUT64 == 0 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
   bool ovf = false;
   if constexpr (MODE == kFasta) {
     const uint64_t b0 = 2 * P - S, last = 2 * A.cap - 1;
@@ -941,19 +944,32 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
 template <int MODE, int OUT64>
 __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t s, int wave, int lane,
                                         uint32_t& ev_tail) {
-  typedef typename std::conditional<OUT64 != 0, uint64_t, uint32_t>::type OutT;
+  typedef typename std::conditional<OUT64 == 1, uint64_t,
+                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
   const WaveRec& rr = sh.rec[s][wave];
   const uint64_t wbase = rfl64(rr.wbase);
   const uint32_t fl = rfl(rr.fl), ev0 = rfl(rr.ev0), nev = rfl(rr.nev);
   const uint64_t P = rfl64(sh.P[s][wave]);
   const uint32_t S = rfl(sh.S[s][wave]);
   ev_tail = ev0 + nev;
+  if constexpr (MODE == kDelim && OUT64 == 2) {
+    // uint16 low words: the entries before every 64 KiB boundary that starts a wave range (the ranges are
+    // split at the first such boundary, so every later one starts a range) locate each entry's block
+    // Written only by the range whose chunk holds the boundary byte itself (lo_w == 0, hi_w > 0): a range
+    // past the end of a chunk's last unit would write the count at that chunk's end, and the first range of
+    // a chunk starting just after the boundary would count bytes of the previous chunk.
+    const uint64_t off0 = A.obj_base - A.shift + wbase;
+    const uint64_t j = (off0 >> 16) - A.tab_j0;
+    const uint32_t lohi = rfl(rr.lohi);
+    const bool holds = (lohi & 0xFFFFu) == 0u && (lohi >> 16) != 0u;
+    if ((off0 & 0xFFFFull) == 0 && holds && off0 >= (A.tab_j0 << 16) && j < A.tab_n && lane == 0) A.blocktab[j] = P;
+  }
   if (fl & kFlDense) {
     dense_b<MODE, OUT64>(A, wbase, rfl(rr.lohi), P, S, lane);
     return;
   }
   const uint64_t obj_off = A.obj_base - A.shift + wbase;
-  const bool near4g = !OUT64 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+  const bool near4g = OUT64 == 0 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
   const uint16_t* evw = sh.ev[wave];
   bool ovf = false;
   if constexpr (MODE == kFasta) {
@@ -979,7 +995,7 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
     const uint64_t q0 = (Pc + r0) / k - A.carry / k;
     const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
 #if DP_PAIRSTORE
-    if constexpr (OUT64 != 0) {
+    if constexpr (OUT64 == 1) {
       // Every delimiter, uint64 output, the whole list in bounds (wave-uniform): two offsets per lane and
       // one 16-byte store, which halves the store instructions that queue behind the input loads.  An odd
       // q0 puts its first entry in a single store so that the pairs are 16-byte aligned.
@@ -1009,6 +1025,35 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
       }
     }
 #endif
+    if constexpr (OUT64 == 2) {
+      // uint16 low words, every delimiter, whole list in bounds: eight entries per lane, one 16-byte store;
+      // the first (8 - q0 % 8) % 8 entries go alone so that the groups are 16-byte aligned
+      if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
+        uint16_t* o = reinterpret_cast<uint16_t*>(A.out) + q0;
+        const uint32_t hh = (uint32_t)((8u - (uint32_t)(q0 & 7u)) & 7u);
+        const uint32_t h = hh < nq ? hh : nq;
+        if ((uint32_t)lane < h) o[lane] = (uint16_t)(add + evw[(ev0 + (uint32_t)lane) & kEvMask]);
+        const uint32_t m = nq - h, g = m >> 3;
+        for (uint32_t t = (uint32_t)lane; t < g; t += kWave) {
+          const uint32_t i = h + 8u * t;
+          uint32_t w[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t a = (uint32_t)(uint16_t)(add + evw[(ev0 + i + 2u * e) & kEvMask]);
+            const uint32_t b = (uint32_t)(uint16_t)(add + evw[(ev0 + i + 2u * e + 1u) & kEvMask]);
+            w[e] = a | (b << 16);
+          }
+          const v4u pk = {w[0], w[1], w[2], w[3]};
+#if DP_NTSTORE
+          __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + i));
+#else
+          *reinterpret_cast<v4u*>(o + i) = pk;
+#endif
+        }
+        for (uint32_t t = h + 8u * g + (uint32_t)lane; t < nq; t += kWave) o[t] = (uint16_t)(add + evw[(ev0 + t) & kEvMask]);
+        return;
+      }
+    }
     for (uint32_t t = (uint32_t)lane; t < nq; t += kWave) {
       const uint64_t q = q0 + t;
       const uint64_t val = add + evw[(ev0 + r0 + t * k) & kEvMask];
@@ -1535,6 +1580,7 @@ struct dp_ctx {
   int out_u64 = 0;
   uint32_t every_k = 1;
   uint64_t carry = 0;
+  std::vector<uint64_t> range_map;    // out_mode 3: caller range of each internal range (split at 64 KiB)
   uint64_t pend_off = 0, ctrl_off = 0;
   // timing
   bool timing = false;
@@ -1647,7 +1693,8 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
 
 int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t units,
                 void* d_out, int out_u64, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add,
-                uint64_t carry = 0, uint32_t wrap32 = 0) {
+                uint64_t carry = 0, uint32_t wrap32 = 0, unsigned long long* blocktab = nullptr, uint64_t tab_j0 = 0,
+                uint64_t tab_n = 0) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
   ScanArgs a;
   a.base = d_buf - shift;
@@ -1665,6 +1712,9 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.cap = cap;
   a.out_u64 = out_u64;
   a.wrap32 = wrap32;
+  a.blocktab = blocktab;
+  a.tab_j0 = tab_j0;
+  a.tab_n = tab_n;
   a.carry = carry;
   a.delim = delim * 0x01010101u;
   a.every_k = every_k;
@@ -1697,6 +1747,8 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
     hipLaunchKernelGGL((scan_kernel<kFasta, 0>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   else if (mode == kFasta)
     hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+  else if (out_u64 == 2)
+    hipLaunchKernelGGL((scan_kernel<kDelim, 2>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   else if (!out_u64)
     hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
   else
@@ -1762,7 +1814,7 @@ int dp_ctx_create(int device, dp_ctx** out) {
   int occ = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (scan_kernel<kFasta, 0>), kThreads, 0));
   const void* others[] = {(const void*)scan_kernel<kFasta, 1>, (const void*)scan_kernel<kDelim, 0>,
-                          (const void*)scan_kernel<kDelim, 1>};
+                          (const void*)scan_kernel<kDelim, 1>, (const void*)scan_kernel<kDelim, 2>};
   for (const void* k : others) {
     int o = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, kThreads, 0));
@@ -1966,21 +2018,55 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is already in flight on this ctx");
   if (every_k == 0) return fail(DP_ERR_INVALID, "every_k must be >= 1");
   if (delim > 255) return fail(DP_ERR_INVALID, "delim must be a byte");
-  if (out_mode < 0 || out_mode > 2) return fail(DP_ERR_INVALID, "out_mode must be 0 (uint32), 1 (uint64) or 2 (uint32 low words)");
+  if (out_mode < 0 || out_mode > 3)
+    return fail(DP_ERR_INVALID, "out_mode must be 0 (uint32), 1 (uint64), 2 (uint32 low words) or 3 (uint16 + blocks)");
   if (nranges == 0 || !ranges) return fail(DP_ERR_INVALID, "no ranges");
   for (uint64_t i = 0; i < nranges; ++i) {
     if (ranges[2 * i + 1] > ranges[2 * i] && !d_buf) return fail(DP_ERR_INVALID, "null buffer");
+    if (ranges[2 * i + 1] < ranges[2 * i]) return fail(DP_ERR_INVALID, "range end before its start");
     if (i && ranges[2 * i] < ranges[2 * i - 1]) return fail(DP_ERR_INVALID, "ranges must ascend without overlap");
+    if (out_mode == 3 && i && ranges[2 * i] != ranges[2 * i - 1])
+      return fail(DP_ERR_INVALID, "out_mode 3 needs contiguous ranges");
   }
   if (cap && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
+  // out_mode 3: split each range at its first 64 KiB boundary, so that every later boundary starts a wave
+  // range (the kernel records the entries before it there); the block table follows the entries in d_out
+  std::vector<uint64_t> rg(ranges, ranges + 2 * nranges);
+  c->range_map.clear();
+  unsigned long long* tab = nullptr;
+  uint64_t j0 = 0, ntab = 0;
+  if (out_mode == 3) {
+    rg.clear();
+    for (uint64_t i = 0; i < nranges; ++i) {
+      const uint64_t lo = ranges[2 * i], hi = ranges[2 * i + 1];
+      const uint64_t a64 = (lo + 0xFFFFull) & ~0xFFFFull;
+      if (lo < a64 && a64 < hi) {
+        rg.push_back(lo); rg.push_back(a64); c->range_map.push_back(i);
+        rg.push_back(a64); rg.push_back(hi); c->range_map.push_back(i);
+      } else {
+        rg.push_back(lo); rg.push_back(hi); c->range_map.push_back(i);
+      }
+    }
+    // wave ranges start 16-byte aligned in buffer coordinates: object offsets must share that alignment
+    if ((((uintptr_t)d_buf) - buf_base) & 15u)
+      return fail(DP_ERR_INVALID, "out_mode 3 needs d_buf and buf_base congruent mod 16 (place the bytes at "
+                                  "an address whose low 4 bits equal buf_base's)");
+    const uint64_t first = ranges[0], last = ranges[2 * nranges - 1];
+    j0 = first >> 16;
+    ntab = last > first ? ((last - 1) >> 16) - j0 + 1 : 1;
+    tab = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(d_out) + ((2 * cap + 15) & ~15ull));
+    if (!d_out) return fail(DP_ERR_INVALID, "out_mode 3 needs an output buffer (entries + block table)");
+  }
+  const uint64_t nr = rg.size() / 2;
   uint64_t units = 0;
-  rc = stage_chunks(c, d_buf, buf_len, buf_base, ranges, nranges, &units);
+  rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units);
   if (rc) return rc;
-  rc = launch_scan(c, kDelim, d_buf, buf_base, nranges, units, d_out, out_mode == 1, cap, delim, every_k, emit_add,
-                   carry, out_mode == 2);
+  const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
+  rc = launch_scan(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
+                   out_mode == 2, tab, j0, ntab);
   if (rc) return rc;
   c->inflight = kDelim;
-  c->nchunks = nranges;
+  c->nchunks = nr;
   c->cap = cap;
   c->out_u64 = out_mode == 1;
   c->every_k = every_k;
@@ -2003,7 +2089,7 @@ int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint6
   for (uint64_t i = 0; i < c->nchunks; ++i) {
     const uint64_t e = c->h_tab[c->pend_off + c->nchunks + i];
     if (e != ~0ull) nd = e;                             // empty ranges were never visited: carry the previous
-    if (range_end) range_end[i] = nd;
+    if (range_end) range_end[c->range_map.empty() ? i : c->range_map[i]] = nd;
   }
   const uint64_t nout = (carry + nd) / k - carry / k;
   if (n_delims) *n_delims = nd;

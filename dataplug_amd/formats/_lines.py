@@ -2,8 +2,9 @@
 
 The reference finds CSV/VCF slice boundaries at ``get()`` time by scanning a padded byte range in Python
 (csv.py:52-105, vcf.py:88-149).  Here ``preprocess`` builds the sorted offsets of every ``'\\n'`` on the GPU
-once — as uint32 low words plus the entry count below each 4 GiB page boundary (the GPU writes half the
-bytes of a uint64 index; the pages live in the attributes) — stores them at ``s3://<bucket>.meta/<key>.lines``,
+once — as uint16 low words plus the entry count below each 64 KiB boundary (the GPU writes a quarter of the
+bytes of a uint64 index; the block table is a separate small object) — stores them at
+``s3://<bucket>.meta/<key>.lines``,
 and a partition strategy resolves each
 slice's exact byte range from that index, reproducing the reference's ``get()`` output (SURVEY.md §8(a)
 formulas, restated below with the clamps the reference's buffer arithmetic implies).
@@ -25,31 +26,43 @@ _BLOCK = 8192                      # entries per cached block for large indexes
 def store_line_index(cloud_object, offsets) -> dict:
     """PUT the index at ``<key>.lines``; returns the attributes that describe it.
 
-    A ``scan.objects.PagedOffsets`` (the default build) is stored as uint32 LE low words, its 4 GiB page
-    counts in the attributes (``line_index_dtype="u32p"``, ``line_index_pages``); a plain array as uint64 LE."""
+    * ``scan.objects.BlockedOffsets`` (the default build, ``line_index_dtype="u16b"``): uint16 LE low words,
+      the 64 KiB block table (uint64 LE) at ``<key>.lines.blocks``, its first block in the attributes;
+    * ``scan.objects.PagedOffsets`` (``"u32p"``): uint32 LE low words, the 4 GiB page counts in the attributes;
+    * a plain array: uint64 LE."""
     key = cloud_object.meta_path.key + LINES_SUFFIX
-    paged = hasattr(offsets, "pages")
-    body = np.ascontiguousarray(offsets.low if paged else offsets, dtype="<u4" if paged else "<u8").tobytes()
-    cloud_object.storage.put_object(Body=body, Bucket=cloud_object.meta_path.bucket, Key=key,
-                                    Metadata={"dataplug": __version__})
+    st, bucket = cloud_object.storage, cloud_object.meta_path.bucket
+    meta = {"dataplug": __version__}
     attrs = {"line_index_key": key, "num_lines": int(len(offsets))}
-    if paged:
+    if hasattr(offsets, "table"):
+        st.put_object(Body=np.ascontiguousarray(offsets.low, "<u2").tobytes(), Bucket=bucket, Key=key, Metadata=meta)
+        bkey = key + ".blocks"
+        st.put_object(Body=np.ascontiguousarray(offsets.table, "<u8").tobytes(), Bucket=bucket, Key=bkey,
+                      Metadata=meta)
+        attrs.update(line_index_dtype="u16b", line_index_blocks_key=bkey, line_index_block0=int(offsets.j0))
+    elif hasattr(offsets, "pages"):
+        st.put_object(Body=np.ascontiguousarray(offsets.low, "<u4").tobytes(), Bucket=bucket, Key=key, Metadata=meta)
         attrs.update(line_index_dtype="u32p", line_index_pages=[int(x) for x in offsets.pages])
+    else:
+        st.put_object(Body=np.ascontiguousarray(offsets, "<u8").tobytes(), Bucket=bucket, Key=key, Metadata=meta)
     return attrs
 
 
 class LineIndex:
     """Sorted newline offsets; ``nxt(x)`` = 1 + first '\n' at or after x (None if none).
 
-    Reads either stored form: uint64 words, or uint32 low words + page counts (``pages[p-1]`` = entries
-    below p * 2^32), fetching blocks by ranged GETs when the index is large."""
+    Reads every stored form (uint64 words; uint32 low words + 4 GiB page counts; uint16 low words + 64 KiB
+    block table), fetching blocks of entries by ranged GETs when the index is large."""
 
     def __init__(self, offsets: Optional[np.ndarray] = None, storage=None, bucket: str = "", key: str = "",
-                 count: Optional[int] = None, pages: Optional[list] = None):
+                 count: Optional[int] = None, pages: Optional[list] = None, blocks: Optional[np.ndarray] = None,
+                 block0: int = 0):
         self._arr = None if offsets is None else np.asarray(offsets, dtype=np.uint64)
         self._storage, self._bucket, self._key = storage, bucket, key
         self._pages = None if pages is None else np.asarray(pages, np.int64)
-        self._item = 8 if pages is None else 4
+        self._blocks_tab = None if blocks is None else np.asarray(blocks, np.int64)
+        self._block0 = int(block0)
+        self._item = 2 if blocks is not None else (4 if pages is not None else 8)
         self._blocks: "OrderedDict[int, np.ndarray]" = OrderedDict()
         if self._arr is None:
             if count is None:
@@ -66,10 +79,17 @@ class LineIndex:
         key = getattr(attrs, "line_index_key", None) if attrs is not None else None
         if not key:
             raise KeyError(f"{cloud_object!r} has no newline index: preprocess it with dataplug_amd (line_index=True)")
-        paged = getattr(attrs, "line_index_dtype", None) == "u32p"
+        dt = getattr(attrs, "line_index_dtype", None)
+        kw = {}
+        if dt == "u32p":
+            kw["pages"] = list(getattr(attrs, "line_index_pages"))
+        elif dt == "u16b":
+            res = cloud_object.storage.get_object(Bucket=cloud_object.meta_path.bucket,
+                                                  Key=getattr(attrs, "line_index_blocks_key"))
+            kw["blocks"] = np.frombuffer(res["Body"].read(), "<u8")
+            kw["block0"] = int(getattr(attrs, "line_index_block0"))
         return cls(storage=cloud_object.storage, bucket=cloud_object.meta_path.bucket, key=key,
-                   count=getattr(attrs, "num_lines", None),
-                   pages=list(getattr(attrs, "line_index_pages")) if paged else None)
+                   count=getattr(attrs, "num_lines", None), **kw)
 
     def _fetch(self, i0: int, i1: int) -> np.ndarray:
         if i1 <= i0:
@@ -77,10 +97,15 @@ class LineIndex:
         it = self._item
         res = self._storage.get_object(Bucket=self._bucket, Key=self._key, Range=f"bytes={it * i0}-{it * i1 - 1}")
         raw = res["Body"].read()
-        if self._pages is None:
+        if it == 8:
             return np.frombuffer(raw, dtype="<u8").astype(np.uint64, copy=False)
-        page = np.searchsorted(self._pages, np.arange(i0, i1, dtype=np.int64), side="right").astype(np.uint64)
-        return (page << np.uint64(32)) | np.frombuffer(raw, dtype="<u4").astype(np.uint64)
+        idx = np.arange(i0, i1, dtype=np.int64)
+        if it == 4:
+            page = np.searchsorted(self._pages, idx, side="right").astype(np.uint64)
+            return (page << np.uint64(32)) | np.frombuffer(raw, dtype="<u4").astype(np.uint64)
+        blk = np.searchsorted(self._blocks_tab, idx, side="right").astype(np.uint64) - np.uint64(1)
+        return ((blk + np.uint64(self._block0)) << np.uint64(16)) | np.frombuffer(raw, dtype="<u2").astype(np.uint64)
+
     def _block(self, b: int) -> np.ndarray:
         blk = self._blocks.get(b)
         if blk is None:

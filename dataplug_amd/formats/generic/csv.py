@@ -25,7 +25,8 @@ if TYPE_CHECKING:
 logger = logging.getLogger(__name__)
 
 
-def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index: bool = True) -> PreprocessingMetadata:
+def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index: bool = True,
+                   index_format: str = "u16b") -> PreprocessingMetadata:
     import pandas as pd
 
     top = []
@@ -35,7 +36,7 @@ def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index
     df = pd.read_csv(io.StringIO("\n".join(top)), sep=separator)
     attrs = {"columns": df.columns.tolist(), "dtypes": df.dtypes.tolist()}
     if line_index:
-        offsets = scan_objects.line_index_object(cloud_object, paged=True)
+        offsets = scan_objects.line_index_object(cloud_object, fmt=index_format)
         attrs.update(store_line_index(cloud_object, offsets))
     return PreprocessingMetadata(attributes=attrs)
 

@@ -59,12 +59,12 @@ def parse_vcf_header(f):
     return header, meta, columns, pos
 
 
-def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True) -> PreprocessingMetadata:
+def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True, index_format: str = "u16b") -> PreprocessingMetadata:
     with cloud_object.open("rb") as f:
         header, meta, columns, body_offset = parse_vcf_header(f)
     attrs = {"columns": columns, "vcf_attributes": meta, "body_offset": body_offset}
     if line_index:
-        offsets = scan_objects.line_index_object(cloud_object, begin=body_offset, paged=True)
+        offsets = scan_objects.line_index_object(cloud_object, begin=body_offset, fmt=index_format)
         attrs.update(store_line_index(cloud_object, offsets))
     return PreprocessingMetadata(attributes=attrs, metadata="\n".join(header).encode("utf-8"))
 

@@ -235,17 +235,39 @@ class ScanContext:
         check(rc)
         return int(n.value), int(nd.value), ends
 
+    @staticmethod
+    def block_table_size(ranges: np.ndarray) -> Tuple[int, int]:
+        """(j0, entries) of the 64 KiB block table out_mode 3 writes for these ranges."""
+        first, last = int(ranges[0]), int(ranges[-1])
+        j0 = first >> 16
+        return j0, (((last - 1) >> 16) - j0 + 1) if last > first else 1
+
+    @staticmethod
+    def out_bytes(cap: int, out_mode: int, ranges: np.ndarray) -> int:
+        """Bytes of a dp_delim_ranges output buffer for ``cap`` entries (out_mode 3: + the block table)."""
+        if out_mode == 3:
+            return ((2 * cap + 15) & ~15) + 8 * ScanContext.block_table_size(ranges)[1] + 16
+        return cap * (8 if out_mode == 1 else 4) + 16
+
+    def block_table(self, d_out: int, cap: int, ranges: np.ndarray) -> np.ndarray:
+        """The 64 KiB block table of an out_mode 3 result: entries before (j0 + j) * 64 KiB (this launch)."""
+        j0, nt = self.block_table_size(ranges)
+        tab = self.d2h(np.empty(nt, np.uint64), d_out + ((2 * cap + 15) & ~15))
+        if int(ranges[0]) & 0xFFFF:
+            tab[0] = 0                                   # the boundary below the first byte: not a range start
+        return tab
+
     def delim_ranges(self, d_buf: int, buf_len: int, buf_base: int, ranges, delim: int = 10, every_k: int = 1,
                      emit_add: int = 0, carry: int = 0, out_mode: int = 1, cap: Optional[int] = None):
         """Synchronous dp_delim_ranges: (offsets, delimiters seen, per-range cumulative counts); out_mode 1
-        uint64, 0 uint32, 2 uint32 low words."""
+        uint64, 0 uint32, 2 uint32 low words, 3 uint16 low words (+ ``block_table``, returned as a 4th item)."""
         rg = np.ascontiguousarray(np.asarray(ranges, dtype=np.uint64).reshape(-1))
         span = int(sum(int(rg[2 * i + 1]) - int(rg[2 * i]) for i in range(len(rg) // 2)))
-        dtype = np.uint64 if out_mode == 1 else np.uint32
+        dtype = {0: np.uint32, 1: np.uint64, 2: np.uint32, 3: np.uint16}[out_mode]
         if cap is None:
             cap = span // (16 * every_k) + 1024
         while True:
-            out = self.workspace("out", cap * np.dtype(dtype).itemsize + 16)
+            out = self.workspace("out", self.out_bytes(cap, out_mode, rg))
             self.delim_ranges_async(d_buf, buf_len, buf_base, rg, delim, every_k, emit_add, carry, out.ptr,
                                     out_mode, cap)
             try:
@@ -253,7 +275,10 @@ class ScanContext:
             except DPCapacityError as e:
                 cap = e.needed
                 continue
-            return self.d2h(np.empty(n, dtype), out.ptr), nd, ends
+            vals = self.d2h(np.empty(n, dtype), out.ptr)
+            if out_mode == 3:
+                return vals, nd, ends, self.block_table(out.ptr, cap, rg)
+            return vals, nd, ends
 
     def find_delim(self, d_buf: int, buf_len: int, buf_base: int, start: int, delim: int = 10) -> int:
         """First object offset >= start holding ``delim`` in the buffer, or -1."""

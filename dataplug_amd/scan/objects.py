@@ -223,16 +223,27 @@ class PagedOffsets:
         return (page << np.uint64(32)) | self.low[i0:i1].astype(np.uint64)
 
 
-def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int, paged: bool = False):
-    ctx = get_context(dev)
-    n = hi - lo
-    d = ctx.workspace("input", n + 64)
-    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, d.ptr)
-    if not paged:
-        return ctx.delim_index(d.ptr, n, lo, lo, hi, delim=delim, every_k=every_k, emit_add=emit_add, u64=True)
-    rg = page_ranges(lo, hi)
-    low, nd, ends = ctx.delim_ranges(d.ptr, n, lo, rg, delim=delim, every_k=1, emit_add=0, out_mode=2)
-    return low, [(r, int(e)) for r, e in zip(rg, ends)]
+@dataclass
+class BlockedOffsets:
+    """Sorted object offsets as uint16 low words plus a table of the entries before every 64 KiB boundary:
+    offset i = ((j0 + j) << 16) | low[i] with j = bisect_right(table, i) - 1, table[0] = 0 (the boundary at
+    or below the first byte).  A quarter of the bytes of a uint64 index (for a 64 GiB object the table is
+    8 MiB), written by the GPU directly (dp_delim_ranges out_mode 3)."""
+    low: np.ndarray
+    table: np.ndarray
+    j0: int
+
+    def __len__(self) -> int:
+        return len(self.low)
+
+    def to_u64(self, i0: int = 0, i1: Optional[int] = None) -> np.ndarray:
+        i1 = len(self.low) if i1 is None else i1
+        idx = np.arange(i0, i1, dtype=np.int64)
+        blk = np.searchsorted(self.table.astype(np.int64), idx, side="right").astype(np.uint64) - np.uint64(1)
+        return ((blk + np.uint64(self.j0)) << np.uint64(16)) | self.low[i0:i1].astype(np.uint64)
+
+
+INDEX_FORMATS = ("u16b", "u32p", "u64")
 
 
 def line_parts(begin: int, end: int, n_devices: int, part_bytes: int = 16 << 30) -> List[Tuple[int, int]]:
@@ -246,23 +257,43 @@ def line_parts(begin: int, end: int, n_devices: int, part_bytes: int = 16 << 30)
     return [b for b in bounds if b[1] > b[0]]
 
 
+def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int, fmt: str = "u64"):
+    ctx = get_context(dev)
+    n = hi - lo
+    d = ctx.workspace("input", n + 64)
+    dp = d.ptr + (lo & 15)                # object offset and device address congruent mod 16 (out_mode 3 grid)
+    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp)
+    if fmt == "u64":
+        return ctx.delim_index(dp, n, lo, lo, hi, delim=delim, every_k=every_k, emit_add=emit_add, u64=True)
+    if fmt == "u32p":
+        rg = page_ranges(lo, hi)
+        low, nd, ends = ctx.delim_ranges(dp, n, lo, rg, delim=delim, out_mode=2)
+        return low, [(r, int(e)) for r, e in zip(rg, ends)]
+    low, nd, ends, tab = ctx.delim_ranges(dp, n, lo, [(lo, hi)], delim=delim, out_mode=3)
+    return low, tab
+
+
 def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int = 10,
-                      max_devices: Optional[int] = None, part_bytes: int = 16 << 30, paged: bool = False):
-    """Sorted offsets of every ``delim`` byte of object bytes [begin, end): uint64, or with ``paged`` a
-    ``PagedOffsets`` (uint32 low words + 4 GiB page counts, the GPU writing half the bytes).
+                      max_devices: Optional[int] = None, part_bytes: int = 16 << 30, fmt: str = "u64"):
+    """Sorted offsets of every ``delim`` byte of object bytes [begin, end) in one of ``INDEX_FORMATS``:
+    ``u64`` a uint64 array; ``u32p`` a ``PagedOffsets`` (uint32 low words + 4 GiB page counts); ``u16b`` a
+    ``BlockedOffsets`` (uint16 low words + a 64 KiB block table) — the GPU writes 8, 4 or 2 bytes per offset.
 
     The range is cut into independent parts (at most ``part_bytes`` each, at least one per GPU) scanned
     round-robin on the GPUs and concatenated in order."""
+    if fmt not in INDEX_FORMATS:
+        raise ValueError(f"index format must be one of {INDEX_FORMATS}, not {fmt!r}")
     end = co.size if end is None else end
     if end <= begin:
-        return PagedOffsets(np.zeros(0, np.uint32), []) if paged else np.zeros(0, np.uint64)
+        return {"u64": np.zeros(0, np.uint64), "u32p": PagedOffsets(np.zeros(0, np.uint32), []),
+                "u16b": BlockedOffsets(np.zeros(0, np.uint16), np.zeros(1, np.uint64), begin >> 16)}[fmt]
     devs = devices(max_devices, co)
     bounds = line_parts(begin, end, len(devs), part_bytes)
 
     def run(k: int):
         lo, hi = bounds[k]
-        r = _delim_group(devs[k % len(devs)], co, lo, hi, delim, 1, 0, paged=paged)
-        return r if paged else r[0]
+        r = _delim_group(devs[k % len(devs)], co, lo, hi, delim, 1, 0, fmt=fmt)
+        return r[0] if fmt == "u64" else r
 
     if len(bounds) == 1:
         out = [run(0)]
@@ -279,19 +310,33 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
 
         with cf.ThreadPoolExecutor(len(by_dev)) as ex:
             list(ex.map(worker, by_dev.values()))
-    if not paged:
+    if fmt == "u64":
         return np.concatenate(out)
-    # pages[p - 1] = offsets before p * 2^32: 0 for the boundaries at or below begin, then the running count
-    # at every boundary inside (begin, end) — each starts one of the parts' page ranges
-    pages, before = [0] * (begin // PAGE), 0
-    for _, ranges in out:
-        prev = 0
-        for (lo, hi), cum in ranges:
-            if lo % PAGE == 0 and lo > begin:
-                pages.append(before)
-            before += cum - prev
-            prev = cum
-    return PagedOffsets(np.concatenate([o[0] for o in out]), pages)
+    low = np.concatenate([o[0] for o in out])
+    if fmt == "u32p":
+        # pages[p - 1] = offsets before p * 2^32: 0 for the boundaries at or below begin, then the running
+        # count at every boundary inside (begin, end) — each starts one of the parts' page ranges
+        pages, before = [0] * (begin // PAGE), 0
+        for _, ranges in out:
+            prev = 0
+            for (lo, hi), cum in ranges:
+                if lo % PAGE == 0 and lo > begin:
+                    pages.append(before)
+                before += cum - prev
+                prev = cum
+        return PagedOffsets(low, pages)
+    # u16b: table[j - J0] = offsets before j * 64 KiB; a boundary inside part k comes from part k's own table
+    # (its count within the part) plus every earlier part's count
+    J0, J1 = begin >> 16, (end - 1) >> 16
+    table = np.zeros(J1 - J0 + 1, np.uint64)
+    before = 0
+    for (lo, hi), (lw, tab) in zip(bounds, out):
+        j0 = lo >> 16
+        js = np.arange(max(j0, J0), ((hi - 1) >> 16) + 1, dtype=np.int64)
+        inside = (js << 16) >= lo                        # boundaries at or after the part's first byte
+        table[js[inside] - J0] = np.uint64(before) + tab[js[inside] - j0]
+        before += len(lw)
+    return BlockedOffsets(low, table, J0)
 
 
 def record_index_bytes(data, delim: int = 10, every_k: int = 1, emit_add: int = 0, device: int = 0,

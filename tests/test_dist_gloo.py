@@ -8,6 +8,7 @@ import sys
 import textwrap
 
 import numpy as np
+import pytest
 
 from dataplug_amd.dist import rank_byte_range, split_groups
 
@@ -126,3 +127,35 @@ def test_line_parts_cover_in_order():
     G = 1 << 30
     assert page_ranges(3 * G, 9 * G) == [(3 * G, 4 * G), (4 * G, 8 * G), (8 * G, 9 * G)]
     assert page_ranges(4 * G, 8 * G) == [(4 * G, 8 * G)]
+
+
+@pytest.mark.parametrize("fmt", ["u16b", "u32p"])
+def test_line_index_parts_merge(monkeypatch, fmt):
+    """line_index_object's merge of per-part GPU outputs (parts at unaligned cuts, one per 'device'),
+    with each part's scan replaced by what the kernel returns for it (host logic only): the merged index
+    rebuilds every offset, across 64 KiB blocks and 4 GiB pages."""
+    from types import SimpleNamespace
+    from dataplug_amd.scan import objects
+    G = 1 << 30
+    rng = np.random.default_rng(7)
+    begin, end = 3 * G + 4321, 13 * G + 77
+    off = np.unique(rng.integers(begin, end, 200_000).astype(np.uint64))
+
+    def fake_group(dev, co, lo, hi, delim, every_k, emit_add, fmt="u64"):
+        sel = off[(off >= lo) & (off < hi)]
+        if fmt == "u32p":
+            rg = objects.page_ranges(lo, hi)
+            counts = np.cumsum([int(((sel >= a) & (sel < b)).sum()) for a, b in rg])
+            return sel.astype(np.uint32), [(r, int(c)) for r, c in zip(rg, counts)]
+        j0 = lo >> 16
+        nt = ((hi - 1) >> 16) - j0 + 1
+        tab = np.searchsorted(sel, (np.arange(j0, j0 + nt, dtype=np.uint64) << np.uint64(16))).astype(np.uint64)
+        if lo & 0xFFFF:
+            tab[0] = 0
+        return (sel & np.uint64(0xFFFF)).astype(np.uint16), tab
+
+    monkeypatch.setattr(objects, "_delim_group", fake_group)
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0,0")
+    co = SimpleNamespace(size=end)
+    res = objects.line_index_object(co, begin=begin, end=end, fmt=fmt, part_bytes=3 * G + 5)
+    assert len(res) == len(off) and np.array_equal(res.to_u64(), off)

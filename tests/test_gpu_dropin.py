@@ -45,9 +45,9 @@ def _index(co):
 
 
 def _lines_u64(co):
-    """The stored newline index (uint32 low words + page counts) as uint64 offsets."""
+    """The stored newline index (uint16 low words + 64 KiB block table) as uint64 offsets."""
     from dataplug_amd.formats._lines import LineIndex
-    assert co.attributes.line_index_dtype == "u32p"
+    assert co.attributes.line_index_dtype == "u16b"
     li = LineIndex.of(co)
     return li._fetch(0, li.count)
 

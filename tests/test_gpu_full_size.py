@@ -117,14 +117,26 @@ def _check_delims(ctx, obj, lo, hi, d_ptr, stage):
 
 
 def test_csv_32gib_configs2_every_offset(ctx):
-    """BASELINE configs[2]: the newline index (uint64) of a 32 GiB cities.csv-shaped object in one launch,
-    every one of its ~963 M offsets compared with the object's analytic newline positions."""
+    """BASELINE configs[2]: the newline index of a 32 GiB cities.csv-shaped object in one launch, in the
+    stored form (uint16 low words + 64 KiB block table, out_mode 3); every one of its ~963 M offsets, rebuilt
+    from the two, compared with the object's analytic newline positions."""
     size = 32 * GiB
     obj = synth.tiled_csv(size, seed=9)
     d = ctx.workspace("full_in", size + 64)
     stage = np.empty(4 * GiB, np.uint8)
-    nd = _check_delims(ctx, obj, 0, size, d.ptr, stage)
-    assert nd > 900_000_000
+    for p in range(0, size, 4 * GiB):
+        ctx.h2d(d.ptr + p, obj.bytes_range(p, min(size, p + 4 * GiB), out=stage))
+    del stage
+    n_exp = obj.count_range(0, size)
+    low, nd, ends, tab = ctx.delim_ranges(d.ptr, size, 0, [(0, size)], out_mode=3, cap=n_exp + 64)
+    assert nd == len(low) == n_exp > 900_000_000
+    i = 0
+    for piece in obj.delims_range(0, size):
+        idx = np.arange(i, i + len(piece), dtype=np.int64)
+        blk = np.searchsorted(tab.astype(np.int64), idx, side="right").astype(np.uint64) - np.uint64(1)
+        assert np.array_equal((blk << np.uint64(16)) | low[i:i + len(piece)].astype(np.uint64), piece), i
+        i += len(piece)
+    assert i == nd
 
 
 def test_vcf_64gib_configs3_eight_parts():

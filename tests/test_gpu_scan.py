@@ -379,3 +379,33 @@ def test_delim_low_words_across_4gib_boundary(ctx):
     page = np.zeros(nd, np.uint64)
     page[int(ends[0]):] = 1
     assert np.array_equal((page << np.uint64(32)) | low.astype(np.uint64), exp)
+
+
+@pytest.mark.parametrize("base", [0, 1337, (1 << 32) - (5 << 20) - 3])
+def test_delim_u16_blocks(ctx, base):
+    """out_mode 3 (the stored CSV/VCF index): uint16 low words plus the entries before every 64 KiB
+    boundary; the library splits each range at its first boundary so every later one starts a wave range.
+    Rebuilt offsets equal the oracle's, for unaligned starts, several contiguous ranges, offsets past 2^32,
+    dense blocks (every byte a newline) and empty blocks (none)."""
+    a = synth.csv((9 << 20) + 17, seed=15)
+    a[(2 << 20):(2 << 20) + 70_000] = 10                     # dense: > kDenseMax events per wave range
+    a[(5 << 20):(5 << 20) + 300_000] = ord("x")               # several blocks without a newline
+    d = ctx.workspace("t_in", len(a) + 64)
+    dp = d.ptr + (base & 15)                                   # object and device addresses congruent mod 16
+    ctx.h2d(dp, a)
+    n = len(a)
+    with pytest.raises(Exception):
+        ctx.delim_ranges(d.ptr + ((base + 1) & 15), n, base, [(base, base + n)], out_mode=3)
+    for ranges in ([(base, base + n)], [(base, base + 4097), (base + 4097, base + (3 << 20) + 5),
+                                       (base + (3 << 20) + 5, base + n)], [(base, base + 65540),
+                                       (base + 65540, base + n)]):
+        low, nd, ends, tab = ctx.delim_ranges(dp, n, base, ranges, out_mode=3)
+        exp = dpref.delim(a, 0, n)[0] + np.uint64(base)
+        assert nd == len(exp) and len(low) == len(exp)
+        j0 = base >> 16
+        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right").astype(np.uint64) - np.uint64(1)
+        got = ((blk + np.uint64(j0)) << np.uint64(16)) | low.astype(np.uint64)
+        assert np.array_equal(got, exp)
+        bounds = np.arange(j0, ((base + n - 1) >> 16) + 1, dtype=np.uint64) << np.uint64(16)
+        assert np.array_equal(tab[1:], np.searchsorted(exp, bounds[1:]).astype(np.uint64))
+        assert ends[-1] == nd

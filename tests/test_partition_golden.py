@@ -18,7 +18,7 @@ from dataplug_amd import synth
 from dataplug_amd.cloudobject import CloudObject
 from dataplug_amd.entities import get_slices
 from dataplug_amd.formats._lines import SliceError, store_line_index
-from dataplug_amd.scan.objects import PagedOffsets
+from dataplug_amd.scan.objects import BlockedOffsets, PagedOffsets
 from dataplug_amd.preprocessing.handler import upload_metadata
 from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
 from dataplug_amd.storage import MemoryStore
@@ -31,7 +31,19 @@ def _load(name):
         return json.load(f)
 
 
-def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, begin=0, paged=True):
+def _as_format(off: np.ndarray, fmt):
+    """The stored index forms built from plain uint64 offsets (what the GPU writes for each)."""
+    if fmt in (True, "u32p"):
+        return PagedOffsets(off.astype(np.uint32), [])
+    if fmt == "u16b":
+        j0 = int(off[0]) >> 16 if len(off) else 0
+        j1 = int(off[-1]) >> 16 if len(off) else 0
+        tab = np.searchsorted(off, np.arange(j0, j1 + 1, dtype=np.uint64) << np.uint64(16)).astype(np.uint64)
+        return BlockedOffsets((off & np.uint64(0xFFFF)).astype(np.uint16), tab, j0)
+    return off
+
+
+def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, begin=0, paged="u16b"):
     store = f"golden_{name}_{fmt.co_class.__name__}"
     MemoryStore._named.pop(store, None)
     co = CloudObject.from_s3(fmt, f"s3://dataplug/{name}", fetch=False, s3_config={"endpoint_url": f"memory://{store}"})
@@ -41,7 +53,7 @@ def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, b
     if nl:
         arr = np.frombuffer(data, np.uint8)
         off = np.flatnonzero(arr[begin:] == 10).astype(np.uint64) + np.uint64(begin)
-        attrs = dict(attrs, **store_line_index(co, PagedOffsets(off.astype(np.uint32), []) if paged else off))
+        attrs = dict(attrs, **store_line_index(co, _as_format(off, paged)))
     upload_metadata(co, PreprocessingMetadata(metadata=meta, attributes=attrs))
     co.fetch()
     return co
@@ -71,7 +83,7 @@ def _vcf_objects():
         yield rec, data
 
 
-@pytest.mark.parametrize("paged", [True, False])
+@pytest.mark.parametrize("paged", ["u16b", "u32p", "u64"])
 def test_csv_partitions_match_reference(paged):
     from dataplug_amd.formats.generic import csv as fcsv
     checked = 0
@@ -95,7 +107,7 @@ def test_csv_partitions_match_reference(paged):
     assert checked > 100
 
 
-@pytest.mark.parametrize("paged", [True, False])
+@pytest.mark.parametrize("paged", ["u16b", "u32p", "u64"])
 def test_vcf_partitions_match_reference(paged):
     from dataplug_amd.formats.genomics import vcf as fvcf
     for rec, data in _vcf_objects():
@@ -172,7 +184,7 @@ def test_paged_line_index_across_4gib_pages(monkeypatch, preload):
     """The stored paged form (uint32 low words + entries below each 4 GiB boundary) read back by LineIndex,
     preloaded or block by block over ranged GETs: the same answers as the uint64 offsets."""
     from dataplug_amd.formats import _lines
-    from dataplug_amd.scan.objects import PagedOffsets
+    from dataplug_amd.scan.objects import BlockedOffsets, PagedOffsets
     if not preload:
         monkeypatch.setattr(_lines, "_PRELOAD_BYTES", 1024)
     rng = np.random.default_rng(3)
@@ -194,3 +206,31 @@ def test_paged_line_index_across_4gib_pages(monkeypatch, preload):
 def _lines_fmt():
     from dataplug_amd.formats.generic.csv import CSV
     return CSV
+
+
+@pytest.mark.parametrize("preload", [True, False])
+def test_blocked_line_index_sparse_and_dense_blocks(monkeypatch, preload):
+    """uint16 low words + 64 KiB block table, read back by LineIndex (preloaded or block-fetched): empty
+    blocks, many entries per block, offsets past 2^32, a first block that starts below the first byte."""
+    from dataplug_amd.formats import _lines
+    if not preload:
+        monkeypatch.setattr(_lines, "_PRELOAD_BYTES", 1024)
+    rng = np.random.default_rng(4)
+    G = 1 << 30
+    dense = rng.integers(5 * G + 123, 5 * G + (1 << 20), 40_000)
+    sparse = rng.integers(5 * G + (1 << 20), 7 * G, 3_000)
+    off = np.unique(np.concatenate([dense, sparse]).astype(np.uint64))
+    bo = _as_format(off, "u16b")
+    assert np.array_equal(bo.to_u64(), off)
+    co = _co(_lines_fmt(), "blocked", b"x" * 16, {}, nl=False)
+    attrs = store_line_index(co, bo)
+    assert attrs["line_index_dtype"] == "u16b"
+    blocks = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=attrs["line_index_blocks_key"])
+                           ["Body"].read(), "<u8")
+    li = _lines.LineIndex(storage=co.storage, bucket=co.meta_path.bucket, key=attrs["line_index_key"],
+                          count=attrs["num_lines"], blocks=blocks, block0=attrs["line_index_block0"])
+    assert np.array_equal(li._fetch(0, li.count), off)
+    for x in [0, 5 * G, 5 * G + 123, 5 * G + 65536, 6 * G, int(off[9999]), int(off[-1]), int(off[-1]) + 1, 8 * G]:
+        i = int(np.searchsorted(off, np.uint64(x)))
+        assert li.nxt(x) == (int(off[i]) + 1 if i < len(off) else None), x
+        assert li.contains(x) == (i < len(off) and int(off[i]) == x)

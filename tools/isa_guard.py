@@ -18,7 +18,7 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "dataplug_amd", "csrc", "dpscan.hip")
-KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_111scan_kernelILi[01]ELi[01]EE\w*):", re.M)
+KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_111scan_kernelILi[01]ELi[012]EE\w*):", re.M)
 
 
 def compile_asm() -> str:
@@ -134,7 +134,7 @@ def check(asm_path: str):
     text = open(asm_path).read()
     problems = []
     kernels = KERNEL_RE.findall(text)
-    assert len(kernels) == 4, kernels
+    assert len(kernels) == 5, kernels
     for k in kernels:
         body = text[text.index(k + ":") + len(k) + 1:]
         body = body[:body.index(".Lfunc_end")]
