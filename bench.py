@@ -63,7 +63,8 @@ def parse():
                    help="csv/vcf newline index form: u16b = uint16 low words + 64 KiB block table (what "
                         "co.preprocess stores), u32p = uint32 low words + 4 GiB page counts, u64 = plain uint64")
     p.add_argument("--devices", default=None,
-                   help="thread mode: comma-separated device of each worker (default 0..N-1)")
+                   help="comma-separated device of each worker / local rank (default 0..N-1); e.g. 0,0,0,0 "
+                        "rehearses the multi-GPU split on one GPU")
     p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) point")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
@@ -111,11 +112,14 @@ def launch_mode(args):
         local = int(os.environ.get("LOCAL_RANK", "0"))
         if args.gpus not in (1, world):
             log(f"--gpus {args.gpus} != WORLD_SIZE {world}: one rank per GPU, using {world}")
-        if local >= device_count():
-            log(f"rank {rank}: local rank {local} but only {device_count()} device(s) visible")
+        dev = local
+        if args.devices:                                  # rehearsal: map local ranks to devices explicitly
+            dev = [int(x) for x in args.devices.split(",")][local]
+        if dev >= device_count():
+            log(f"rank {rank}: device {dev} but only {device_count()} device(s) visible")
             sys.exit(2)
         dist.init_process_group("gloo")
-        return world, rank, [local], dist
+        return world, rank, [dev], dist
     n = args.gpus
     devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
     if len(devs) != n:

@@ -85,6 +85,22 @@ static_assert(kRows * kBufs == kRangeRows && kRows >= 2 && kRows <= 8, "buffers 
 #define DP_PRIO_LEVELS 4u
 #endif
 constexpr uint32_t kRing = DP_RING;                // unit slots per workgroup (units in flight)
+// Units are claimed dynamically (a global ticket, by the coordinator, kClaimAhead steps ahead of the
+// workgroup's front data wave): a workgroup only ever claims a unit while it runs, so every unit a wait
+// depends on belongs to a running (or finished) workgroup — no co-residency assumption, and faster CUs
+// take more units.  The queue spans the ring plus the claim-ahead distance.
+#ifndef DP_CLAIM_FASTA
+#define DP_CLAIM_FASTA 4
+#endif
+#ifndef DP_CLAIM_DELIM
+#define DP_CLAIM_DELIM 2
+#endif
+#ifndef DP_CLAIM_AHEAD
+#define DP_CLAIM_AHEAD 3
+#endif
+constexpr uint32_t kClaimAhead = DP_CLAIM_AHEAD;
+constexpr uint32_t kUnitQ = 2 * DP_RING;
+static_assert(kUnitQ >= kRing + kClaimAhead + 2, "unit queue: ring + claim-ahead");
 constexpr uint32_t kEvCap = DP_EVCAP;              // 16-bit event entries per data wave (circular)
 constexpr uint32_t kEvMask = kEvCap - 1;
 constexpr uint32_t kDenseMax = 1024;               // events kept per wave range; more = dense
@@ -177,6 +193,7 @@ struct ScanArgs {
   uint32_t emit_add;
   uint32_t* err;
   unsigned long long* total;   // inclusive count at the last unit
+  unsigned int* ticket;        // [2]: next unit to claim, workgroups finished (both reset by the last one)
   long long* pending;          // FASTA: [nchunks] pair index whose end is unresolved at chunk end, or -1
   unsigned long long* chunk_end;  // [nchunks] inclusive count at the end of each (non-empty) chunk
 };
@@ -674,6 +691,8 @@ struct Shared {
   uint32_t done[kRing];                                     // data waves finished phase A of the slot's unit
   uint32_t ready[kRing];                                    // = unit index + 1 once P/S of the slot are set
   uint32_t front;                                           // highest step a data wave of the workgroup has started
+  uint32_t uq[kUnitQ];                                      // unit claimed for step k at [k % kUnitQ] (coordinator)
+  uint32_t uq_ready[kUnitQ];                                // = k + 1 once uq of step k is set
 };
 
 // ------------------------------------------------------------------------------------------ rows
@@ -1135,13 +1154,18 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
 #endif
 constexpr uint32_t kLbDepth = DP_LBDEPTH;          // look-back windows in flight per coordinator attempt
 
+// consecutive units per ticket atomic: one returning atomic on one address per unit caps the grid near
+// 20 units/us (measured: FASTA -16% at 1, -7% at 2, parity at 4); a longer run of consecutive units
+// per workgroup delays the next workgroup's look-back, which the event-heavy DELIM scan feels first
+// (CSV -23% at 4, +1% at 2)
+template <int MODE> constexpr uint32_t kClaimN = MODE == kFasta ? DP_CLAIM_FASTA : DP_CLAIM_DELIM;
+
 // Coordinator event loop.  Its descriptor loads queue behind the CU's in-flight input stream (~5 us),
 // so it never waits on one unit: each round it issues the look-back windows of up to kLbDepth composed
 // units at once, composes + publishes every unit whose 15 data waves are done while they travel (other
 // workgroups' look-backs wait on those), then resolves the windows in order until one is incomplete.
 template <int MODE>
-__device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uint32_t u0, uint32_t G, uint32_t K,
-                                            int lane, Shared& sh) {
+__device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int lane, Shared& sh) {
   PROF_DECL;
   set_prio(DP_COORD_PRIO);
   Cursor cur{0, 0, 0, 0, 0, 0};
@@ -1150,7 +1174,40 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
   uint32_t pub = 0, res = 0;
   uint32_t idle = 0;
   uint64_t idle_t0 = 0;
-  auto unit_of = [&](uint32_t k) { return u0 + k * G; };
+  const uint32_t nunits = (uint32_t)A.nunits;
+  uint32_t claimed = 0;                             // steps claimed so far
+  uint32_t K = kNoUnit;                             // the workgroup's step count, once a claim ran out of units
+  auto unit_of = [&](uint32_t k) { return sh.uq[k % kUnitQ]; };
+  // claim units for the steps up to kClaimAhead past the front data wave's (the wave at step k prefetches
+  // step k + 1's unit); one returning atomic per unit, on this wave (the data waves' loads are hand-waited)
+  uint32_t batch = 0, nbatch = 0;                   // consecutive units of the last claim not yet queued
+  auto claim_ahead = [&]() {
+    bool any = false;
+    while (K == kNoUnit && claimed <= lds_ld(&sh.front) + kClaimAhead) {
+      if (nbatch == 0) {
+        uint32_t u = 0;
+        if (lane == 0) u = atomicAdd(&A.ticket[0], kClaimN<MODE>);
+        batch = rfl(u);
+        nbatch = kClaimN<MODE>;
+      }
+      const uint32_t u = batch++;
+      --nbatch;
+      const uint32_t v = u < nunits ? u : kNoUnit;
+      const uint32_t slot = claimed % kUnitQ;
+      if (lane == 0) {
+        sh.uq[slot] = v;
+        cbar();
+        lds_st(&sh.uq_ready[slot], claimed + 1u);
+      }
+      if (v == kNoUnit) K = claimed;
+#ifdef DP_TL_CLAIM
+      TL_STAMP(claimed, 2);
+#endif
+      ++claimed;
+      any = true;
+    }
+    return any;
+  };
   auto compose_ready = [&]() {
     bool any = false;
     while (pub < K && lds_ld(&sh.done[pub % kRing]) == (uint32_t)kDataWaves) {
@@ -1169,7 +1226,8 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, uin
     return any;
   };
   while (res < K) {
-    bool prog = compose_ready();
+    bool prog = claim_ahead();
+    prog |= compose_ready();
     PROF_MARK(0);
     if (res < pub) {
       const uint32_t D = pub - res < kLbDepth ? pub - res : kLbDepth;
@@ -1261,16 +1319,19 @@ struct DataWave {
   const ScanArgs& A;
   const Tab& T;
   Shared& sh;
-  uint32_t u0, G;
   int lane, wave;
   uint32_t ev_head = 0, ev_tail = 0;
   uint32_t jt = 0;                                   // oldest unit whose phase B is not done
 
-  __device__ DataWave(const ScanArgs& a, const Tab& t, Shared& s, uint32_t u0_, uint32_t g_, int l, int w)
-      : A(a), T(t), sh(s), u0(u0_), G(g_), lane(l), wave(w) {}
+  __device__ DataWave(const ScanArgs& a, const Tab& t, Shared& s, int l, int w)
+      : A(a), T(t), sh(s), lane(l), wave(w) {}
 
-  // the unit of the workgroup's step k (>= nunits: past the end)
-  __device__ __forceinline__ uint32_t unit_of(uint32_t k) { return u0 + k * G; }
+  // the unit the coordinator claimed for the workgroup's step k (kNoUnit: past the last unit)
+  __device__ __forceinline__ uint32_t unit_of(uint32_t k) {
+    const uint32_t slot = k % kUnitQ;
+    if (!lds_wait_eq(&sh.uq_ready[slot], k + 1u, A.err)) return kNoUnit;
+    return rfl(sh.uq[slot]);
+  }
 
   __device__ __forceinline__ void finish(bool block, int wslot PROF_ARG) {
     const uint32_t s = jt % kRing;
@@ -1288,13 +1349,14 @@ struct DataWave {
   // k + 1; publish; phase B of ready units; prefetch of the last buffer.  While one buffer is scanned the
   // kBufs - 1 others are in flight.
   __device__ __forceinline__ bool step(uint32_t k, Geo& g, Buf (&b)[kBufs], Cursor& cur PROF_ARG) {
+    // sh.front = the workgroup's front step (the coordinator claims units ahead of it)
+    uint32_t front = 0;
+    if (lane == 0) front = __hip_atomic_fetch_max(&sh.front, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    front = rfl(front);
 #if DP_PRIO == 2
     // Issue priority = how many units this wave trails the workgroup's front wave (0..3): a unit's AGG
     // waits for its slowest wave, so the trailing waves take issue slots from the leading ones.
     {
-      uint32_t front = 0;
-      if (lane == 0) front = __hip_atomic_fetch_max(&sh.front, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      front = rfl(front);
       const uint32_t lag = front > k ? (front - k) << DP_LAGSHIFT : 0u;
       set_prio(lag < 3u ? lag : 3u);
     }
@@ -1323,7 +1385,9 @@ struct DataWave {
     WaveRec rec;
     phase_a_rec<MODE>(pa, g, wave, ev_head, rec);
     ev_head += rec.nev;
+#ifndef DP_TL_CLAIM
     if (wave == 0) TL_STAMP(k, 2);
+#endif
     if (lane == 0) {
       sh.rec[s][wave] = rec;
       cbar();
@@ -1348,11 +1412,13 @@ struct DataWave {
   __device__ __forceinline__ void run() {
     PROF_DECL;
     Cursor cur{0, 0, 0, 0, 0, 0};
+    const uint32_t u0 = unit_of(0);
+    if (u0 == kNoUnit) return;                         // every unit was claimed before this workgroup ran
     Geo g = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u0, cur);
     Buf b[kBufs];
 #pragma unroll
     for (int h = 0; h < kBufs; ++h) load_buf(b[h], A, g, wave, lane, h);
-    uint32_t K = 0;                                    // the workgroup's step count (u0 < nunits: >= 1)
+    uint32_t K = 0;                                    // the workgroup's step count (>= 1: u0 is a unit)
     for (bool more = true; more; ++K) more = step(K, g, b, cur PROF_PASS);
     drain_bufs(b);
     PROF_MARK(6);
@@ -1371,19 +1437,20 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   __shared__ Shared sh;
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_u0};
   const uint32_t G = gridDim.x;
-  const uint32_t u0 = blockIdx.x;
-  const uint32_t nunits = (uint32_t)A.nunits;                 // host: < 2^31 units
-  const uint32_t K = u0 < nunits ? (nunits - u0 + G - 1) / G : 0;   // units of this workgroup
   if (threadIdx.x < kRing) {
     sh.done[threadIdx.x] = 0;
     sh.ready[threadIdx.x] = 0;
   }
+  if (threadIdx.x < kUnitQ) sh.uq_ready[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh.front = 0;
   __syncthreads();
 #ifdef DP_LOADONLY
   // perf probe only (never a shipped build): the data waves' load structure without any compute or
   // synchronisation — the ceiling this grid/unit geometry can stream at
   if (wave != kCoord) {
+    const uint32_t nunits = (uint32_t)A.nunits;
+    const uint32_t u0 = blockIdx.x;
+    const uint32_t K = u0 < nunits ? (nunits - u0 + G - 1) / G : 0;
     Cursor cur{0, 0, 0, 0, 0, 0};
     Geo g = geo_of(T, (uint32_t)A.nchunks, nunits, u0, cur);
     Buf b[kBufs];
@@ -1406,10 +1473,19 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   return;
 #endif
   if (wave == kCoord) {
-    coordinator<MODE>(A, T, u0, G, K, lane, sh);
+    coordinator<MODE>(A, T, lane, sh);
   } else {
-    DataWave<MODE, OUT64> dw(A, T, sh, u0, G, lane, wave);
+    DataWave<MODE, OUT64> dw(A, T, sh, lane, wave);
     dw.run();
+  }
+  // every claim of this workgroup is done: the last workgroup to finish resets the claim counters for the
+  // next launch on this table (no per-launch memset)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (atomicAdd(&A.ticket[1], 1u) == G - 1u) {
+      atomicExch(&A.ticket[0], 0u);
+      atomicExch(&A.ticket[1], 0u);
+    }
   }
 }
 
@@ -1652,7 +1728,8 @@ int harvest_events(dp_ctx* c) {
 }
 
 // Lay out the chunk table in aligned coordinates and enqueue its upload when it changed.
-// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[4] (err | total | spare x2).
+// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[5] (err | total | spare x2 |
+// unit ticket: next unit, workgroups finished; zero between launches).
 // No per-launch reset: every launch rewrites pending / chunk_end of each non-empty chunk and total (when it
 // has units), so only the upload sets their defaults (-1, ~0, 0) and err = 0.  A launch that sets an err
 // bit drops last_tab, so the next one re-uploads (results of a failed launch are discarded anyway).
@@ -1673,7 +1750,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     if (hi > lo) units += (hi - (lo & ~15ull) + kUnitBytes - 1) / kUnitBytes;
   }
   tab[3 * n] = units;
-  const uint64_t words = 5 * n + 1 + 4;
+  const uint64_t words = 5 * n + 1 + 5;
   int rc = ensure_tab(c, words);
   if (rc) return rc;
   c->pend_off = 3 * n + 1;
@@ -1683,7 +1760,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(c->h_tab, tab.data(), tab.size() * 8);
     memset(c->h_tab + c->pend_off, 0xFF, 2 * n * 8);
-    memset(c->h_tab + c->ctrl_off, 0, 4 * 8);
+    memset(c->h_tab + c->ctrl_off, 0, 5 * 8);
     HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, words * 8, hipMemcpyHostToDevice, c->stream));
     c->last_tab.swap(tab);
   }
@@ -1721,6 +1798,7 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.emit_add = emit_add;
   a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
   a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
+  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
   a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
   a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
   if (units == 0) return DP_OK;
@@ -1995,7 +2073,7 @@ int dp_fasta_result(dp_ctx* c, uint64_t* n_pairs, int64_t* pending, uint64_t* ch
       prev = e;
     }
   }
-  if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out (grid not co-resident?)");
+  if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out");
   if (err & kErrOverflow) return fail(DP_ERR_OVERFLOW, "Python integer out of bounds for uint32");
   if (total > c->cap) return fail(DP_ERR_CAPACITY, "output capacity " + std::to_string(c->cap) + " < " +
                                                        std::to_string(total) + " pairs");
@@ -2094,7 +2172,7 @@ int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint6
   const uint64_t nout = (carry + nd) / k - carry / k;
   if (n_delims) *n_delims = nd;
   if (n_out) *n_out = nout;
-  if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out (grid not co-resident?)");
+  if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out");
   if (err & kErrOverflow) return fail(DP_ERR_OVERFLOW, "Python integer out of bounds for uint32");
   if (nout > c->cap) return fail(DP_ERR_CAPACITY, "output capacity " + std::to_string(c->cap) + " < " +
                                                       std::to_string(nout) + " offsets");

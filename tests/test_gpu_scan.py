@@ -4,6 +4,7 @@ Bit-exact for every case (integer/byte work).  Sizes here finish in seconds; the
 (4 GiB FASTA, GiB-scale CSV) are in test_gpu_full_size.py.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -256,8 +257,7 @@ def test_descriptor_epochs_wrap():
 def test_two_contexts_unserialized_every_step_exact():
     """bench.py's issue pattern WITHOUT dp_ctx_wait: two contexts on one GPU, step k + 1 enqueued before step
     k is collected, two different objects (and a FASTA / newline mix) so a stale or mixed-up output shows.
-    Every step's index is checked.  The library runs one persistent scan grid at a time per device (the
-    look-back needs every workgroup of a grid resident), so no launch may time out (DP_ERR_TIMEOUT)."""
+    Every step's index is checked and no launch may time out (DP_ERR_TIMEOUT)."""
     from dataplug_amd.scan import ScanContext
     objs = [synth.fasta((24 << 20) + 99, 12), synth.fasta((20 << 20) + 4097, 13)]
     plans = [cpu_ref.chunk_plan(len(o), math.ceil(len(o) / 4)) for o in objs]
@@ -327,6 +327,26 @@ def test_concurrent_threads_one_device():
 
     with cf.ThreadPoolExecutor(4) as ex:
         assert all(ex.map(worker, range(4)))
+
+
+def test_two_processes_one_gpu():
+    """Two processes scanning on the same GPU at once (torchrun ranks sharing a device): nothing in the
+    library orders their grids, so the two persistent grids split the CUs between them.  Units are claimed
+    by running workgroups only, so neither grid waits on a workgroup that cannot start: every scan exact,
+    no look-back timeout."""
+    import subprocess
+    import sys
+    helper = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_proc_scan.py")
+    procs = [subprocess.Popen([sys.executable, helper, str(seed), "40"], stdout=subprocess.PIPE,
+                              stderr=subprocess.STDOUT, text=True) for seed in (3, 4)]
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=100)[0])
+        except subprocess.TimeoutExpired:
+            p.kill()
+            outs.append(p.communicate()[0])
+    assert [p.returncode for p in procs] == [0, 0], outs
 
 
 @pytest.mark.parametrize("k,add", [(1, 0), (4, 1), (3, 0)])

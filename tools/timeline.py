@@ -4,7 +4,7 @@
 
 For every workgroup b (< 256) and its k-th unit u = b + k*G, the kernel stamps the realtime clock (100 MHz)
 when (0) the unit's AGG descriptor is published, (1) the coordinator resolved its prefix, (2) data wave 0
-finished phase A of it; word 3 holds the step's unit index (dynamic assignment).  This prints, per round k, medians over
+finished phase A of it (DP_TL_CLAIM builds: the coordinator claimed it); word 3 holds the step's unit index (dynamic assignment).  This prints, per round k, medians over
 workgroups, in microseconds from the launch's first stamp, plus the derived look-back latency: the time
 from the moment unit u's whole window was published (max AGG time over units u-G+1 .. u-1 and u's own
 previous prefix) to u's resolution.
@@ -46,13 +46,14 @@ def analyse(tl, grid, nunits):
     # unit index -> (b, k)
     pub = np.full(nunits, np.nan)
     res = np.full(nunits, np.nan)
+    w2 = np.full(nunits, np.nan)
     for b in range(grid):
         for k in range(TL_UNITS):
             if tl[b, k, 1] <= 0:
                 continue
             u = int(tl[b, k, 3])
             if u < nunits:
-                pub[u], res[u] = us[b, k, 0], us[b, k, 1]
+                pub[u], res[u], w2[u] = us[b, k, 0], us[b, k, 1], us[b, k, 2]
     # a unit's window is published once every earlier unit back to one already resolved has its AGG
     # (approximation: the 255 previous units' AGGs and the resolution of the unit 256 back)
     ready = np.full(nunits, np.nan)
@@ -70,6 +71,7 @@ def analyse(tl, grid, nunits):
             break
         rows.append({
             "k": k,
+            "w2_med": round(float(np.nanmedian(w2[sel])), 1),
             "pub_med": round(float(np.nanmedian(pub[sel])), 1),
             "pub_spread": round(float(np.nanmax(pub[sel]) - np.nanmin(pub[sel])), 1),
             "res_med": round(float(np.nanmedian(res[sel])), 1),
