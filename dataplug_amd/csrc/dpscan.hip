@@ -1149,6 +1149,9 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
 #ifndef DP_LBDEPTH
 #define DP_LBDEPTH 8
 #endif
+#ifndef DP_IDLE_SLEEP    // coordinator back-off (x 64 clocks) after a round without progress
+#define DP_IDLE_SLEEP 1
+#endif
 #ifndef DP_COORD_PRIO
 #define DP_COORD_PRIO 0
 #endif
@@ -1304,7 +1307,7 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
         if (lane == 0) atomicOr(A.err, kErrTimeout);
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(DP_IDLE_SLEEP);
       PROF_MARK(3);
     }
   }
@@ -1365,6 +1368,9 @@ struct DataWave {
 #endif
     const uint32_t s = k % kRing;
     wait_buf(b[0]);
+#ifdef DP_TL_DATA
+    if (wave == 0) TL_STAMP(k, 2);                    // the unit's first buffer landed
+#endif
     PROF_MARK(0);
     const uint32_t un = unit_of(k + 1u);
     const Geo gn = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, un, cur);
@@ -1385,7 +1391,7 @@ struct DataWave {
     WaveRec rec;
     phase_a_rec<MODE>(pa, g, wave, ev_head, rec);
     ev_head += rec.nev;
-#ifndef DP_TL_CLAIM
+#if !defined(DP_TL_CLAIM) && !defined(DP_TL_DATA)
     if (wave == 0) TL_STAMP(k, 2);
 #endif
     if (lane == 0) {

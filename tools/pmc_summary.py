@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--kernel", default="scan_kernel<0>")
     ap.add_argument("--alg-bytes", type=float, default=None)
     ap.add_argument("--object-bytes", type=int, default=None, help="scanned bytes per launch (bench.py checks it)")
+    ap.add_argument("--index-dtype", default=None, help="csv/vcf index form profiled (bench.py checks it)")
     args = ap.parse_args()
     os.makedirs(args.dst, exist_ok=True)
     out = counters(args.src, args.kernel)
@@ -49,6 +50,8 @@ def main():
     out["kernel"] = args.kernel
     if args.object_bytes:
         out["object_bytes"] = args.object_bytes
+    if args.index_dtype:
+        out["index_dtype"] = args.index_dtype
     for f in glob.glob(os.path.join(args.src, "**", "*kernel_stats.csv"), recursive=True):
         shutil.copy(f, os.path.join(args.dst, "kernel_stats.csv"))
     for f in glob.glob(os.path.join(args.src, "*.log")):

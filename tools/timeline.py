@@ -85,6 +85,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4 << 30)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--pre-stream", type=int, default=0,
+                    help="bytes of a read-only stream kernel enqueued right before the profiled scan (no host gap)")
     args = ap.parse_args()
     size = args.size
     ctx = ScanContext(0)
@@ -97,6 +99,8 @@ def main():
     chunks = np.asarray([(i * cs, min(size, (i + 1) * cs)) for i in range(size // cs)], np.uint64).reshape(-1)
     nunits = sum(-(-(min(size, (i + 1) * cs) - i * cs + (i * cs) % 16) // unit) for i in range(size // cs))
     for _ in range(2):
+        if args.pre_stream:
+            ctx.stream_read(d.ptr, min(size, args.pre_stream))
         ctx.fasta_index_async(d.ptr, size, 0, size, chunks, out.ptr, False, size // 256)
         ctx.fasta_result(len(chunks) // 2)
     tl = read_timeline(ctx)
