@@ -95,6 +95,9 @@ constexpr uint32_t kRing = DP_RING;                // unit slots per workgroup (
 #ifndef DP_CLAIM_DELIM
 #define DP_CLAIM_DELIM 2
 #endif
+#ifndef DP_TAIL            // the last DP_TAIL x G units are claimed one at a time
+#define DP_TAIL 0
+#endif
 #ifndef DP_CLAIM_AHEAD
 #define DP_CLAIM_AHEAD 3
 #endif
@@ -1152,8 +1155,15 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
 #ifndef DP_IDLE_SLEEP    // coordinator back-off (x 64 clocks) after a round without progress
 #define DP_IDLE_SLEEP 1
 #endif
-#ifndef DP_COORD_PRIO
-#define DP_COORD_PRIO 0
+// Coordinator issue priority.  At 0 it loses every arbitration to the data waves of its SIMD, which
+// (memory permitting) always have an instruction ready: on some XCDs the workgroups' first AGGs came
+// ~100 us late (tools/timeline.py; every look-back waits on them), and FASTA is 2-3 % faster at 3.  The
+// write-heavy CSV newline index is 4 % slower at 3 (its look-back polls then compete with phase B).
+#ifndef DP_COORD_PRIO_FASTA
+#define DP_COORD_PRIO_FASTA 3
+#endif
+#ifndef DP_COORD_PRIO_DELIM
+#define DP_COORD_PRIO_DELIM 0
 #endif
 constexpr uint32_t kLbDepth = DP_LBDEPTH;          // look-back windows in flight per coordinator attempt
 
@@ -1170,7 +1180,7 @@ template <int MODE> constexpr uint32_t kClaimN = MODE == kFasta ? DP_CLAIM_FASTA
 template <int MODE>
 __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int lane, Shared& sh) {
   PROF_DECL;
-  set_prio(DP_COORD_PRIO);
+  set_prio(MODE == kFasta ? DP_COORD_PRIO_FASTA : DP_COORD_PRIO_DELIM);
   Cursor cur{0, 0, 0, 0, 0, 0};
   uint64_t prevP = 0;
   uint32_t prevS = 0;
@@ -1184,14 +1194,21 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
   // claim units for the steps up to kClaimAhead past the front data wave's (the wave at step k prefetches
   // step k + 1's unit); one returning atomic per unit, on this wave (the data waves' loads are hand-waited)
   uint32_t batch = 0, nbatch = 0;                   // consecutive units of the last claim not yet queued
+  // near the end, single units and one step ahead, so no workgroup holds a long queue while others idle
+  const uint32_t tail = (uint32_t)DP_TAIL * gridDim.x;
+  uint32_t run = kClaimN<MODE>, ahead = kClaimAhead;
   auto claim_ahead = [&]() {
     bool any = false;
-    while (K == kNoUnit && claimed <= lds_ld(&sh.front) + kClaimAhead) {
+    while (K == kNoUnit && claimed <= lds_ld(&sh.front) + ahead) {
       if (nbatch == 0) {
         uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(&A.ticket[0], kClaimN<MODE>);
+        if (lane == 0) u = atomicAdd(&A.ticket[0], run);
         batch = rfl(u);
-        nbatch = kClaimN<MODE>;
+        nbatch = run;
+        if (batch + tail >= nunits) {
+          run = 1;
+          ahead = 1;
+        }
       }
       const uint32_t u = batch++;
       --nbatch;

@@ -1,6 +1,8 @@
 set -o pipefail
-O=gpurun_out/ab7; mkdir -p $O
+O=gpurun_out/ab12; mkdir -p $O
 L=dataplug_amd/lib
-for v in pdata pa; do
-DPSCAN_LIB=$L/libdpscan_v_$v.so timeout -k 10 120 python tools/timeline.py --out $O/tl_$v.npz > $O/tl_$v.log 2>&1 || exit 1
+for i in 1 2; do
+ for v in t0 t2 t4 t8; do
+  DPSCAN_LIB=$L/libdpscan_v_$v.so timeout -k 10 200 python tools/probe_perf.py --no-stream --reps 10 >> $O/probe.log 2>&1 || exit 1
+ done
 done
