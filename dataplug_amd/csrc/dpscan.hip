@@ -95,9 +95,6 @@ constexpr uint32_t kRing = DP_RING;                // unit slots per workgroup (
 #ifndef DP_CLAIM_DELIM
 #define DP_CLAIM_DELIM 2
 #endif
-#ifndef DP_TAIL            // the last DP_TAIL x G units are claimed one at a time
-#define DP_TAIL 0
-#endif
 #ifndef DP_CLAIM_AHEAD
 #define DP_CLAIM_AHEAD 3
 #endif
@@ -1194,21 +1191,14 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
   // claim units for the steps up to kClaimAhead past the front data wave's (the wave at step k prefetches
   // step k + 1's unit); one returning atomic per unit, on this wave (the data waves' loads are hand-waited)
   uint32_t batch = 0, nbatch = 0;                   // consecutive units of the last claim not yet queued
-  // near the end, single units and one step ahead, so no workgroup holds a long queue while others idle
-  const uint32_t tail = (uint32_t)DP_TAIL * gridDim.x;
-  uint32_t run = kClaimN<MODE>, ahead = kClaimAhead;
   auto claim_ahead = [&]() {
     bool any = false;
-    while (K == kNoUnit && claimed <= lds_ld(&sh.front) + ahead) {
+    while (K == kNoUnit && claimed <= lds_ld(&sh.front) + kClaimAhead) {
       if (nbatch == 0) {
         uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(&A.ticket[0], run);
+        if (lane == 0) u = atomicAdd(&A.ticket[0], kClaimN<MODE>);
         batch = rfl(u);
-        nbatch = run;
-        if (batch + tail >= nunits) {
-          run = 1;
-          ahead = 1;
-        }
+        nbatch = kClaimN<MODE>;
       }
       const uint32_t u = batch++;
       --nbatch;

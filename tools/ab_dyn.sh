@@ -1,8 +1,8 @@
 set -o pipefail
-O=gpurun_out/ab12; mkdir -p $O
+O=gpurun_out/ab15; mkdir -p $O
 L=dataplug_amd/lib
 for i in 1 2; do
- for v in t0 t2 t4 t8; do
+ for v in r16 r32; do
   DPSCAN_LIB=$L/libdpscan_v_$v.so timeout -k 10 200 python tools/probe_perf.py --no-stream --reps 10 >> $O/probe.log 2>&1 || exit 1
  done
 done
