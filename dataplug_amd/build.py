@@ -10,6 +10,7 @@ SRC = os.path.join(HERE, "csrc", "dpscan.hip")
 OUT = os.path.join(HERE, "lib", "libdpscan.so")
 OUT_PROF = os.path.join(HERE, "lib", "libdpscan_prof.so")   # diagnostics: in-kernel section timers
 GZ_SRC = os.path.join(HERE, "csrc", "dpgz.c")
+GZ_PAR_SRC = os.path.join(HERE, "csrc", "dpgz_par.c")     # parallel inflate of one gzip stream
 GZ_OUT = os.path.join(HERE, "lib", "libdpgz.so")            # host-side gzip access-point index (zlib)
 ARCH = os.environ.get("DPSCAN_ARCH", "gfx950")
 
@@ -34,7 +35,8 @@ def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=S
 def build_gz() -> str:
     os.makedirs(os.path.dirname(GZ_OUT), exist_ok=True)
     cc = os.environ.get("CC", "gcc")
-    subprocess.run([cc, "-O2", "-fPIC", "-shared", "-Wall", "-Wextra", "-o", GZ_OUT + ".tmp", GZ_SRC, "-lz", "-lpthread"], check=True)
+    subprocess.run([cc, "-O3", "-fPIC", "-shared", "-Wall", "-Wextra", "-o", GZ_OUT + ".tmp", GZ_SRC, GZ_PAR_SRC,
+                    "-lz", "-lpthread"], check=True)
     os.replace(GZ_OUT + ".tmp", GZ_OUT)
     return GZ_OUT
 

@@ -128,7 +128,7 @@ void dpgz_free(dpgz_result* r) {
   free(r);
 }
 
-int dpgz_abi_version(void) { return 2; }
+int dpgz_abi_version(void) { return 3; }
 
 /* ------------------------------------------------------------------------------------------ streaming
  * The same access points, built while the object streams through in bounded pieces (FASTQ.gz objects far

@@ -67,16 +67,18 @@ def window_table(inflated: np.ndarray, points: np.ndarray, newlines: np.ndarray)
 
 
 def preprocess_gzip(cloud_object: "CloudObject", record_lines: int = 4, span: int = SPAN,
-                    piece_bytes: int = gzindex.PIECE_BYTES) -> PreprocessingMetadata:
+                    piece_bytes: int = gzindex.PIECE_BYTES, inflate_threads: int = 0) -> PreprocessingMetadata:
     """gzipped.py:46-153: streams the object once (one GET, read in 1 MiB pieces like the reference's writes
     into gztool) through the bounded inflate -> HBM -> newline-scan pipeline of ``scan.gzindex``; stores the
-    windows (``<key>.idx``), the read ends (``<key>.records``) and the window table (parquet, the meta object)."""
+    windows (``<key>.idx``), the read ends (``<key>.records``) and the window table (parquet, the meta object).
+    ``inflate_threads``: host inflate threads (0: the process's CPU share; 1: zlib on one core)."""
     import pandas as pd
 
     ctx = get_context(scan_objects.devices(co=cloud_object)[0])
     res = cloud_object.storage.get_object(Bucket=cloud_object.path.bucket, Key=cloud_object.path.key)
     with res["Body"] as body:
-        ix = gzindex.index_stream(ctx, body.read, record_lines=record_lines, span=span, piece_bytes=piece_bytes)
+        ix = gzindex.index_stream(ctx, body.read, record_lines=record_lines, span=span, piece_bytes=piece_bytes,
+                                  threads=int(inflate_threads) or None)
     meta = cloud_object.meta_path
     idx_key, rec_key = meta.key + ".idx", meta.key + ".records"
     st = cloud_object.storage

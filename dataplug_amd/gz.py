@@ -73,7 +73,21 @@ def load():
         lib.dpgz_bgzf_scan.argtypes = [vp, u64, _U64P, _U64P, _U64P, u64, _U64P, _U64P]
         lib.dpgz_inflate_members.restype = ctypes.c_int
         lib.dpgz_inflate_members.argtypes = [vp, _U64P, _U64P, _U64P, _U64P, u64, vp, ctypes.c_int]
-        if lib.dpgz_abi_version() < 2:
+        lib.dpgz_par_new.restype = ctypes.c_int
+        lib.dpgz_par_new.argtypes = [u64, ctypes.c_int, ctypes.POINTER(vp)]
+        lib.dpgz_par_free.restype = None
+        lib.dpgz_par_free.argtypes = [vp]
+        lib.dpgz_par_set_region.restype = ctypes.c_int
+        lib.dpgz_par_set_region.argtypes = [vp, u64]
+        lib.dpgz_par_feed.restype = ctypes.c_int
+        lib.dpgz_par_feed.argtypes = [vp, vp, u64, ctypes.c_int]
+        lib.dpgz_par_read.restype = ctypes.c_int
+        lib.dpgz_par_read.argtypes = [vp, vp, u64, _U64P]
+        lib.dpgz_par_take.restype = ctypes.c_int
+        lib.dpgz_par_take.argtypes = [vp, u64, vp, u64, vp, u64, _U64P, _U64P]
+        lib.dpgz_par_state.restype = ctypes.c_int
+        lib.dpgz_par_state.argtypes = [vp, _U64P]
+        if lib.dpgz_abi_version() < 3:
             raise ImportError(f"{LIB_PATH} is out of date: rebuild it with `python -m dataplug_amd.build`")
         _lib = lib
     return _lib
@@ -246,6 +260,57 @@ class InflateStream:
     def close(self):
         if self._h:
             load().dpgz_stream_free(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class ParInflate:
+    """libdpgz's parallel inflater of one gzip stream (include/dpgz.h, csrc/dpgz_par.c): compressed bytes in,
+    inflated bytes out in order, the same access points as InflateStream, on ``threads`` cores."""
+
+    def __init__(self, span: int = 1 << 20, threads: int = 1, region_bytes: Optional[int] = None):
+        h = ctypes.c_void_p()
+        _check(load().dpgz_par_new(int(span), int(threads), ctypes.byref(h)), "gzip parallel inflate")
+        self._h = h
+        if region_bytes:
+            _check(load().dpgz_par_set_region(h, int(region_bytes)), "gzip parallel inflate")
+
+    def feed(self, data, final: bool = False) -> None:
+        keep = np.frombuffer(data, np.uint8) if len(data) else np.zeros(1, np.uint8)
+        _check(load().dpgz_par_feed(self._h, keep.ctypes.data, len(data), int(final)), "gzip stream")
+
+    def read_into(self, out: np.ndarray, off: int, cap: int) -> int:
+        """Copy up to ``cap`` inflated bytes to out[off:]; returns how many."""
+        n = ctypes.c_uint64(0)
+        _check(load().dpgz_par_read(self._h, out.ctypes.data + off, int(cap), ctypes.byref(n)), "gzip stream")
+        return int(n.value)
+
+    def stats(self) -> dict:
+        st = (ctypes.c_uint64 * 9)()
+        _check(load().dpgz_par_state(self._h, st), "gzip stream")
+        keys = ("consumed", "produced", "members", "unread", "points", "window_bytes", "ended", "batches",
+                "rejected")
+        return dict(zip(keys, (int(x) for x in st)))
+
+    def take(self, out_limit: int):
+        """(points with out_byte <= out_limit as POINTEX_DTYPE, their windows as bytes)."""
+        st = self.stats()
+        npts, nwin = st["points"], st["window_bytes"]
+        pts = np.zeros(max(1, npts), POINTEX_DTYPE)
+        win = np.zeros(max(1, nwin), np.uint8)
+        n, w = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        _check(load().dpgz_par_take(self._h, int(out_limit), pts.ctypes.data, npts, win.ctypes.data, nwin,
+                                    ctypes.byref(n), ctypes.byref(w)), "gzip stream")
+        return pts[: int(n.value)], win[: int(w.value)].tobytes()
+
+    def close(self):
+        if self._h:
+            load().dpgz_par_free(self._h)
             self._h = None
 
     def __del__(self):  # pragma: no cover

@@ -37,6 +37,7 @@ PIECE_BYTES = 64 << 20
 READ_BYTES = 1 << 20          # compressed bytes per GET-body read (the reference writes 64 KiB pieces)
 BGZF_BATCH = 16 << 20         # compressed bytes scanned for complete BGZF members at a time
 SPOOL_MEM = 64 << 20
+PAR_READ_BYTES = 4 << 20      # compressed bytes per read while a plain stream is inflated in parallel
 
 
 def pool_threads() -> int:
@@ -98,6 +99,8 @@ class _Inflater(threading.Thread):
             if gzlib.is_bgzf(first):
                 self.bgzf = True
                 self._run_bgzf(first)
+            elif self.threads > 1:
+                self._run_parallel(first)
             else:
                 self._run_stream(first)
         except BaseException as e:                      # surfaced by the scan thread
@@ -141,6 +144,50 @@ class _Inflater(threading.Thread):
                     return
         finally:
             st.close()
+
+    def _run_parallel(self, first: bytes):
+        """A plain gzip stream inflated on the thread pool (libdpgz dpgz_par_*: speculative block starts,
+        marker windows, CRC-checked), drained into the pieces in order."""
+        pi = gzlib.ParInflate(self.span, self.threads)
+        try:
+            final = len(first) == 0
+            pi.feed(first, final)
+            o0, slot, filled, out = 0, None, 0, None
+            while True:
+                while True:                                # move the inflated bytes into pieces
+                    if slot is None:
+                        slot = self._take_slot()
+                        if slot is None:
+                            return
+                        out, filled = self.pieces[slot], 0
+                    n = pi.read_into(out, filled, len(out) - filled)
+                    filled += n
+                    if filled == len(out):
+                        pts, win = pi.take(o0 + filled)
+                        self.ready.put(_Piece(slot, o0, filled, pts, win))
+                        o0 += filled
+                        slot = None
+                        continue
+                    if n == 0:
+                        break
+                st = pi.stats()
+                self.members = st["members"]
+                if st["ended"]:
+                    if slot is None:
+                        slot = self._take_slot()
+                        if slot is None:
+                            return
+                        filled = 0
+                    pts, win = pi.take(o0 + filled)
+                    self.ready.put(_Piece(slot, o0, filled, pts, win))
+                    return
+                if final:
+                    raise ValueError("gzip stream: truncated")
+                data = self.read(PAR_READ_BYTES)
+                final = len(data) == 0
+                pi.feed(data, final)
+        finally:
+            pi.close()
 
     def _run_bgzf(self, first: bytes):
         cbuf = np.frombuffer(first, np.uint8)

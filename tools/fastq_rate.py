@@ -3,9 +3,11 @@
     python tools/fastq_rate.py [--reads N] [--reps R] [--repeat K]
 
 A synthetic FASTQ (100 bp reads) in an in-process store (memory://), as
-* "gzip6": one gzip member (level 6) — deflate is serial: one inflate core;
-* "gzip6 xK": the same member K times (multi-member, still serial: member sizes are not in the headers),
-  K x larger inflated stream through the same bounded pipeline (host memory must not grow);
+* "gzip6 zlib": one gzip member (level 6) inflated by zlib on one core (the reference's gztool is serial too);
+* "gzip6": the same member inflated in parallel (libdpgz dpgz_par: speculative deflate block starts, marker
+  windows, CRC-checked) on the process's CPU share;
+* "gzip6 xK": the same member K times (multi-member), a K x larger inflated stream through the same bounded
+  pipeline (host memory must not grow);
 * "bgzf": BGZF 64 KiB members (level 6), inflated member-parallel on the host thread pool.
 For each: `co.preprocess()` of FASTQGZip end to end (one streamed GET, inflate into pinned pieces, H2D, the
 newline scan on the GPU with the ordinal carried across pieces, D2H of the read ends, window table + read
@@ -67,23 +69,25 @@ class PeakRSS:
         self._t.join()
 
 
-def run_case(name, blob, raw_len, exp_ends, reps):
+def run_case(name, blob, raw_len, exp_ends, reps, threads=0):
     key = f"r_{name.replace(' ', '_')}.fastq.gz"
     store = MemoryStore.named("fq")
     store.put("genomics", key, blob)
     co = CloudObject.from_s3(FASTQGZip, f"s3://genomics/{key}", s3_config={"endpoint_url": "memory://fq"})
-    co.preprocess(force=True)                               # warm: pandas/pyarrow, context, buffers
+    extra = {"inflate_threads": threads}
+    co.preprocess(force=True, extra_args=extra)             # warm: pandas/pyarrow, context, buffers
     ts, peak = [], 0
     for _ in range(reps):
         with PeakRSS() as pr:
             t0 = time.perf_counter()
-            co.preprocess(force=True)
+            co.preprocess(force=True, extra_args=extra)
             ts.append(time.perf_counter() - t0)
         peak = max(peak, pr.peak - pr.base)
     got = load_read_index(co)
     ok = bool(np.array_equal(got, exp_ends))
     t = min(ts)
-    out = {"case": name, "gzip_bytes": len(blob), "inflated_bytes": raw_len, "members": co.attributes.gzip_members,
+    out = {"case": name, "inflate_threads": threads or pool_threads(), "gzip_bytes": len(blob),
+           "inflated_bytes": raw_len, "members": co.attributes.gzip_members,
            "bgzf": co.attributes.bgzf, "preprocess_s": round(t, 3),
            "preprocess_inflated_GiB_per_s": round(raw_len / t / GiB, 3),
            "preprocess_gzip_GiB_per_s": round(len(blob) / t / GiB, 3),
@@ -112,8 +116,9 @@ def main():
     store = MemoryStore.named("fq")
     store.create_bucket("genomics")
     store.create_bucket("genomics.meta")
+    run_case("gzip6 zlib", g6, len(rb), exp_ends, args.reps, threads=1)
     run_case("gzip6", g6, len(rb), exp_ends, args.reps)
-    # K copies of the member: a K x larger stream (multi-member, serial), ends shifted per copy
+    # K copies of the member: a K x larger stream (multi-member), ends shifted per copy
     ek = np.concatenate([exp_ends + np.uint64(i * len(rb)) for i in range(args.repeat)])
     run_case(f"gzip6 x{args.repeat}", g6 * args.repeat, len(rb) * args.repeat, ek, 1)
     del ek
