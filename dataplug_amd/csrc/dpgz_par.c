@@ -37,7 +37,7 @@
 #define DTAB (256 + 30 * 128)
 #define CLTAB 128
 #define E_SUB 0x100000u
-#define REGION_MIN (1u << 20)           /* compressed bytes per region, at least (default) */
+#define REGION_MIN (2u << 20)           /* compressed bytes per region, at least (default) */
 #define NONE UINT64_MAX
 
 enum { K_BLOCK = 0, K_HEADER = 1, K_END = 2 };           /* what starts at a stop position */
@@ -1002,10 +1002,27 @@ int dpgz_par_feed(dpgz_par* s, const uint8_t* in, uint64_t in_len, int in_final)
   return DPGZ_OK;
 }
 
+typedef struct {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t n;
+} CopyJob;
+#define COPY_PART (1u << 20)
+static void job_copy(void* a, int i) {
+  CopyJob* c = (CopyJob*)a;
+  const uint64_t o = (uint64_t)i * COPY_PART;
+  memcpy(c->dst + o, c->src + o, c->n - o < COPY_PART ? c->n - o : COPY_PART);
+}
+
 int dpgz_par_read(dpgz_par* s, uint8_t* out, uint64_t cap, uint64_t* n) {
   if (!s || !n || (!out && cap)) return DPGZ_ERR_INVALID;
   const uint64_t k = s->olen - s->ohead < cap ? s->olen - s->ohead : cap;
-  if (k) memcpy(out, s->out + s->ohead, k);
+  if (k >= 4 * COPY_PART && s->threads > 1) {         /* into pinned pieces: one copy, on all threads */
+    CopyJob c = {out, s->out + s->ohead, k};
+    pfor((int)((k + COPY_PART - 1) / COPY_PART), s->threads, job_copy, &c);
+  } else if (k) {
+    memcpy(out, s->out + s->ohead, k);
+  }
   s->ohead += k;
   *n = k;
   return DPGZ_OK;

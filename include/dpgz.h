@@ -72,14 +72,14 @@ int dpgz_inflate_members(const uint8_t* gz, const uint64_t* in_off, const uint64
 
 /* Parallel inflate of one gzip stream (dpgz_par.c): speculative deflate block starts per region, 16-bit
  * marker windows resolved in order, every member's CRC-32 / ISIZE checked.  Feed compressed bytes (the
- * engine inflates a batch once threads x 1 MiB are pending, or everything with in_final), read the inflated
+ * engine inflates a batch once threads x 2 MiB are pending, or everything with in_final), read the inflated
  * bytes in order, take the access points (those of dpgz_stream, with windows) up to an output offset.
  * dpgz_par_state fills stats[9]: compressed bytes consumed, inflated bytes produced, members, inflated
  * bytes not read, points pending, window bytes pending, stream ended, batches, region starts rejected. */
 typedef struct dpgz_par dpgz_par;
 int dpgz_par_new(uint64_t span, int threads, dpgz_par** out);
 void dpgz_par_free(dpgz_par* s);
-int dpgz_par_set_region(dpgz_par* s, uint64_t bytes);   /* compressed bytes per region (default 1 MiB) */
+int dpgz_par_set_region(dpgz_par* s, uint64_t bytes);   /* compressed bytes per region (default 2 MiB) */
 int dpgz_par_feed(dpgz_par* s, const uint8_t* in, uint64_t in_len, int in_final);
 int dpgz_par_read(dpgz_par* s, uint8_t* out, uint64_t cap, uint64_t* n);
 int dpgz_par_take(dpgz_par* s, uint64_t out_limit, dpgz_point_ex* pts, uint64_t max_pts, uint8_t* windows,

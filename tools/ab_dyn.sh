@@ -1,4 +1,8 @@
 set -o pipefail
-O=gpurun_out/gzpar1; mkdir -p $O
-timeout -k 10 300 python -u -m pytest tests/test_gpu_dropin.py tests/test_gzpar_cpu.py tests/test_gzindex_cpu.py -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 &&
-timeout -k 10 600 python -u tools/fastq_rate.py > $O/fastq_rate.log 2>&1
+O=gpurun_out/ab16; mkdir -p $O
+L=dataplug_amd/lib
+for i in 1 2; do
+ for v in pre cur d1c d4c; do
+  DPSCAN_LIB=$L/libdpscan_v_$v.so timeout -k 10 300 python tools/probe_delim_modes.py --gib 8 >> $O/$v.log 2>&1 || exit 1
+ done
+done
