@@ -92,8 +92,14 @@ constexpr uint32_t kRing = DP_RING;                // unit slots per workgroup (
 #ifndef DP_CLAIM_FASTA
 #define DP_CLAIM_FASTA 4
 #endif
-#ifndef DP_CLAIM_DELIM
+#ifndef DP_CLAIM_DELIM     // DELIM units per claim once a unit holds more than DP_CLAIM_DENSE delimiters
 #define DP_CLAIM_DELIM 2
+#endif
+#ifndef DP_CLAIM_SPARSE    // ... and while they hold fewer
+#define DP_CLAIM_SPARSE 4
+#endif
+#ifndef DP_CLAIM_DENSE
+#define DP_CLAIM_DENSE 5500
 #endif
 #ifndef DP_CLAIM_AHEAD
 #define DP_CLAIM_AHEAD 3
@@ -1166,8 +1172,9 @@ constexpr uint32_t kLbDepth = DP_LBDEPTH;          // look-back windows in fligh
 
 // consecutive units per ticket atomic: one returning atomic on one address per unit caps the grid near
 // 20 units/us (measured: FASTA -16% at 1, -7% at 2, parity at 4); a longer run of consecutive units
-// per workgroup delays the next workgroup's look-back, which the event-heavy DELIM scan feels first
-// (CSV -23% at 4, +1% at 2)
+// per workgroup delays the next workgroup's look-back, which an event-dense DELIM scan feels first (its
+// per-wave event lists fill): CSV (~6,900 delimiters per unit) -20% at 4 vs 2, while VCF (~3,100) and
+// FASTQ (~4,300) gain 5% at 4.  DELIM picks the run from the last composed unit's delimiter count.
 template <int MODE> constexpr uint32_t kClaimN = MODE == kFasta ? DP_CLAIM_FASTA : DP_CLAIM_DELIM;
 
 // Coordinator event loop.  Its descriptor loads queue behind the CU's in-flight input stream (~5 us),
@@ -1191,14 +1198,17 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
   // claim units for the steps up to kClaimAhead past the front data wave's (the wave at step k prefetches
   // step k + 1's unit); one returning atomic per unit, on this wave (the data waves' loads are hand-waited)
   uint32_t batch = 0, nbatch = 0;                   // consecutive units of the last claim not yet queued
+  uint32_t last_events = ~0u;                       // delimiters of the last composed unit (none yet: dense)
   auto claim_ahead = [&]() {
     bool any = false;
     while (K == kNoUnit && claimed <= lds_ld(&sh.front) + kClaimAhead) {
       if (nbatch == 0) {
         uint32_t u = 0;
-        if (lane == 0) u = atomicAdd(&A.ticket[0], kClaimN<MODE>);
+        // DELIM: long runs while the units are event-sparse, short ones once a unit is event-dense
+        const uint32_t run = MODE == kFasta ? kClaimN<MODE> : (last_events > (uint32_t)DP_CLAIM_DENSE ? kClaimN<MODE> : (uint32_t)DP_CLAIM_SPARSE);
+        if (lane == 0) u = atomicAdd(&A.ticket[0], run);
         batch = rfl(u);
-        nbatch = kClaimN<MODE>;
+        nbatch = run;
       }
       const uint32_t u = batch++;
       --nbatch;
@@ -1224,6 +1234,7 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
       const uint32_t s = pub % kRing;
       cbar();
       const Func f = compose_unit(sh, s, lane);
+      if constexpr (MODE == kDelim) last_events = (uint32_t)f.cF;
       const uint32_t up = unit_of(pub);
       if (lane == 0) {
         if (up > 0) st_desc(&A.desc[up], pack_agg(f) | A.epoch);
