@@ -778,10 +778,11 @@ static int grow(void** p, uint64_t* cap, uint64_t need, uint64_t elem) {
   return 0;
 }
 
-/* Byte at output offset x (x < out_total + batch bytes): from the batch's output or the unread output. */
+/* Queue an access point at output offset `out` with its window (the current member's last <= WIN bytes
+ * before it) and the byte before it.  hist: contiguous inflated bytes, hist[0] at output offset hist_base,
+ * covering at least WIN bytes before `out` (or everything since the stream start). */
 static int add_point(dpgz_par* s, uint64_t in_byte, uint32_t bits, uint64_t out, uint32_t member,
                      const uint8_t* hist, uint64_t hist_base) {
-  /* hist: contiguous bytes whose first byte is output offset hist_base, ending at out */
   if (grow((void**)&s->pts, &s->pcap, s->npts + 1, sizeof(dpgz_point_ex))) return -1;
   dpgz_point_ex* p = &s->pts[s->npts++];
   p->in_byte = in_byte;

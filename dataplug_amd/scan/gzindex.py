@@ -5,9 +5,10 @@ gzipped.py:46-153: the object streamed into ``gztool -i -x -I`` in 64 KiB writes
 count and the window table), rebuilt as a pipeline whose host memory does not grow with the object:
 
 * an inflater thread pulls compressed bytes from the GET body and inflates them (libdpgz) into one of a few
-  pinned piece buffers of ``piece_bytes`` — a plain gzip stream on one core (deflate is serial), BGZF-style
-  members (compressed size in their header) on a thread pool, member by member straight to their place in
-  the piece;
+  pinned piece buffers of ``piece_bytes`` — a plain gzip stream on the thread pool by speculative deflate
+  block starts (``dpgz_par``; zlib on one core when only one thread is available), BGZF-style members
+  (compressed size in their header) on the thread pool, member by member straight to their place in the
+  piece;
 * the calling thread copies each finished piece to HBM and runs ``dp_delim_ranges`` on it with the newline
   ordinal carried from the previous pieces, so ``every_k = record_lines`` selects read ends across piece
   boundaries (FASTQ: every 4th '\\n' + 1), while the inflater fills the next piece;
@@ -81,9 +82,11 @@ class GzIndex:
 class _Inflater(threading.Thread):
     """Fills pinned piece buffers from the compressed stream; hands finished pieces to the scan thread."""
 
-    def __init__(self, read: Callable[[int], bytes], pieces: List[np.ndarray], span: int, threads: int):
+    def __init__(self, read: Callable[[int], bytes], pieces: List[np.ndarray], span: int, threads: int,
+                 region_bytes: Optional[int] = None):
         super().__init__(daemon=True, name="dpgz-inflate")
         self.read, self.pieces, self.span, self.threads = read, pieces, span, threads
+        self.region_bytes = region_bytes
         self.free: "queue.Queue[int]" = queue.Queue()
         for i in range(len(pieces)):
             self.free.put(i)
@@ -148,7 +151,7 @@ class _Inflater(threading.Thread):
     def _run_parallel(self, first: bytes):
         """A plain gzip stream inflated on the thread pool (libdpgz dpgz_par_*: speculative block starts,
         marker windows, CRC-checked), drained into the pieces in order."""
-        pi = gzlib.ParInflate(self.span, self.threads)
+        pi = gzlib.ParInflate(self.span, self.threads, region_bytes=self.region_bytes)
         try:
             final = len(first) == 0
             pi.feed(first, final)
@@ -247,9 +250,11 @@ class _Inflater(threading.Thread):
 
 
 def index_stream(ctx: ScanContext, read: Callable[[int], bytes], record_lines: int = 4, span: int = 4 << 20,
-                 piece_bytes: int = PIECE_BYTES, n_pieces: int = 3, threads: Optional[int] = None) -> GzIndex:
+                 piece_bytes: int = PIECE_BYTES, n_pieces: int = 3, threads: Optional[int] = None,
+                 region_bytes: Optional[int] = None) -> GzIndex:
     """Stream a gzip object (``read(n)`` returns its next compressed bytes, b"" at the end) through the
-    inflate → HBM → newline-scan pipeline on ``ctx``'s GPU.  See the module doc."""
+    inflate → HBM → newline-scan pipeline on ``ctx``'s GPU.  See the module doc.  ``region_bytes``: compressed
+    bytes per speculative region of the parallel inflater (default 2 MiB; tests use small ones)."""
     k = int(record_lines)
     pins = [ctx.pinned(f"gzpiece{i}", piece_bytes) for i in range(n_pieces)]
     arrays = [p.array[:piece_bytes] for p in pins]
@@ -257,7 +262,7 @@ def index_stream(ctx: ScanContext, read: Callable[[int], bytes], record_lines: i
     cap = piece_bytes // (2 * k) + 1024                  # read ends per piece: at most one per 2k bytes
     d_out = ctx.workspace("gzends", 8 * cap + 16)
     res = GzIndex(ends=tempfile.SpooledTemporaryFile(SPOOL_MEM), windows=tempfile.SpooledTemporaryFile(SPOOL_MEM))
-    inf = _Inflater(read, arrays, span, threads or pool_threads())
+    inf = _Inflater(read, arrays, span, threads or pool_threads(), region_bytes)
     inf.start()
     carry = 0                                            # newlines before the current piece
     n_ends = 0                                           # read ends so far

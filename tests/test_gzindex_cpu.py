@@ -114,6 +114,19 @@ def test_stream_pieces_match_whole(piece, k):
     _check(ix, raw, blob, k, 1 << 16, bgzf=False)
 
 
+@pytest.mark.parametrize("threads,region", [(1, None), (4, 4096), (8, 1 << 14)])
+@pytest.mark.parametrize("piece", [1 << 16, 777_777])
+def test_parallel_inflate_pieces(threads, region, piece):
+    """The same multi-member stream through zlib on one core and the parallel inflater with small
+    speculative regions: identical read ends, window rows and windows, across piece boundaries."""
+    raw = synth.fastq(12_000, seed=3).tobytes()
+    blob = _multi(raw)
+    ix = gzindex.index_stream(OracleCtx(), _reader(blob, 55_555), record_lines=4, span=1 << 15, piece_bytes=piece,
+                              threads=threads, region_bytes=region)
+    assert ix.members == 3
+    _check(ix, raw, blob, 4, 1 << 15, bgzf=False)
+
+
 @pytest.mark.parametrize("piece", [1 << 17, 1_000_003])
 def test_bgzf_member_parallel(piece):
     raw = synth.fastq(15_000, seed=7).tobytes()
