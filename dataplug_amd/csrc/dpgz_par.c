@@ -140,6 +140,76 @@ static void fixed_init(void) {
   build_table(g_fixed.dist, DTAB, l + 288, 32, DBITS, 1);
 }
 
+/* ------------------------------------------------------------------------------------------ CRC-32
+ * gzip's CRC-32 by carry-less multiplication (x86-64 PCLMULQDQ): four 128-bit lanes folded 64 bytes at a
+ * time with x^(512±32) mod P, folded to one lane with x^(128±32) mod P, reduced 128 -> 64 -> 32 bits
+ * (Barrett); the bit-reflected constants of P = 0x104C11DB7.  zlib's table method for tails and for CPUs
+ * without the instruction (checked once). */
+#if defined(__x86_64__)
+#include <immintrin.h>
+__attribute__((target("pclmul,sse4.1"))) static uint32_t crc_fold(uint32_t state, const uint8_t* p, uint64_t n) {
+  /* state: the raw register (~crc); n >= 64, a multiple of 16 */
+  const __m128i k512 = _mm_set_epi64x(0x01c6e41596ll, 0x0154442bd4ll);
+  const __m128i k128 = _mm_set_epi64x(0x00ccaa009ell, 0x01751997d0ll);
+  const __m128i k64 = _mm_set_epi64x(0, 0x0163cd6124ll);
+  const __m128i pmu = _mm_set_epi64x(0x01f7011641ll, 0x01db710641ll);
+  const __m128i lo32 = _mm_setr_epi32(-1, 0, -1, 0);
+  __m128i a = _mm_xor_si128(_mm_loadu_si128((const __m128i*)p), _mm_cvtsi32_si128((int)state));
+  __m128i b = _mm_loadu_si128((const __m128i*)(p + 16));
+  __m128i c = _mm_loadu_si128((const __m128i*)(p + 32));
+  __m128i d = _mm_loadu_si128((const __m128i*)(p + 48));
+  p += 64;
+  n -= 64;
+  for (; n >= 64; p += 64, n -= 64) {
+    const __m128i a1 = _mm_clmulepi64_si128(a, k512, 0x11), a0 = _mm_clmulepi64_si128(a, k512, 0x00);
+    const __m128i b1 = _mm_clmulepi64_si128(b, k512, 0x11), b0 = _mm_clmulepi64_si128(b, k512, 0x00);
+    const __m128i c1 = _mm_clmulepi64_si128(c, k512, 0x11), c0 = _mm_clmulepi64_si128(c, k512, 0x00);
+    const __m128i d1 = _mm_clmulepi64_si128(d, k512, 0x11), d0 = _mm_clmulepi64_si128(d, k512, 0x00);
+    a = _mm_xor_si128(_mm_xor_si128(a1, a0), _mm_loadu_si128((const __m128i*)p));
+    b = _mm_xor_si128(_mm_xor_si128(b1, b0), _mm_loadu_si128((const __m128i*)(p + 16)));
+    c = _mm_xor_si128(_mm_xor_si128(c1, c0), _mm_loadu_si128((const __m128i*)(p + 32)));
+    d = _mm_xor_si128(_mm_xor_si128(d1, d0), _mm_loadu_si128((const __m128i*)(p + 48)));
+  }
+#define FOLD128(x, next) _mm_xor_si128(_mm_xor_si128(_mm_clmulepi64_si128(x, k128, 0x11), \
+                                                     _mm_clmulepi64_si128(x, k128, 0x00)), next)
+  a = FOLD128(a, b);
+  a = FOLD128(a, c);
+  a = FOLD128(a, d);
+  for (; n >= 16; p += 16, n -= 16) a = FOLD128(a, _mm_loadu_si128((const __m128i*)p));
+#undef FOLD128
+  /* 128 -> 64 bits */
+  __m128i t = _mm_clmulepi64_si128(a, k128, 0x10);
+  a = _mm_xor_si128(_mm_srli_si128(a, 8), t);
+  t = _mm_srli_si128(a, 4);
+  a = _mm_xor_si128(_mm_clmulepi64_si128(_mm_and_si128(a, lo32), k64, 0x00), t);
+  /* Barrett: 64 -> 32 bits */
+  t = _mm_clmulepi64_si128(_mm_and_si128(a, lo32), pmu, 0x10);
+  t = _mm_clmulepi64_si128(_mm_and_si128(t, lo32), pmu, 0x00);
+  a = _mm_xor_si128(a, t);
+  return (uint32_t)_mm_extract_epi32(a, 1);
+}
+static int g_pclmul = -1;
+#endif
+
+static uint32_t crc32_fast(uint32_t crc, const uint8_t* p, uint64_t n) {
+#if defined(__x86_64__)
+  if (g_pclmul < 0) g_pclmul = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1");
+  if (g_pclmul && n >= 64) {
+    const uint64_t m = n & ~15ull;
+    crc = ~crc_fold(~crc, p, m);
+    p += m;
+    n -= m;
+  }
+#endif
+  while (n > 0) {                                       /* zlib: uInt lengths */
+    const uInt k = n > (1u << 30) ? (1u << 30) : (uInt)n;
+    crc = (uint32_t)crc32(crc, p, k);
+    p += k;
+    n -= k;
+  }
+  return crc;
+}
+
 /* ------------------------------------------------------------------------------------------ bit input */
 /* >= 57 valid bits from bit position pos (zeros past the end of the input). */
 static inline uint64_t peek_at(const uint8_t* buf, uint64_t nbytes, uint64_t pos) {
@@ -726,7 +796,6 @@ static void job_find(void* a, int i) {
 static void job_decode(void* a, int k) {
   Batch* b = (Batch*)a;
   Region* r = &b->s->regs[b->idx[k]];
-  if (reserve(r, 4u << 20)) { r->rc = D_MEM; return; }
   decode_region(r, b->s->cin, b->nbytes, b->final && k == b->nkeep - 1);
 }
 
@@ -758,12 +827,12 @@ static void job_resolve(void* a, int k) {
   for (uint64_t e = 0; e < r->nev; ++e) {
     if (r->ev[e].kind == EV_BLOCK) continue;
     const uint64_t at = r->ev[e].out - WIN;
-    b->seg_crc[si] = (uint32_t)crc32(0L, d + from, (uInt)(at - from));
+    b->seg_crc[si] = crc32_fast(0u, d + from, at - from);
     b->seg_len[si] = at - from;
     ++si;
     from = at;
   }
-  b->seg_crc[si] = (uint32_t)crc32(0L, d + from, (uInt)(m - from));
+  b->seg_crc[si] = crc32_fast(0u, d + from, m - from);
   b->seg_len[si] = m - from;
 }
 
@@ -837,6 +906,7 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
     r->start = k == 0 ? s->pos : found[idx[k]];
     r->start_kind = k == 0 ? s->kind : K_BLOCK;
     r->stop_at = k + 1 < nkeep ? found[idx[k + 1]] : NONE;
+    r->n = 0;                                           /* the buffer is reused: only the window is kept */
     if (reserve(r, WIN + (4u << 20))) return DPGZ_ERR_MEMORY;
     if (k == 0) {                                       /* the known window, right-aligned */
       for (uint32_t j = 0; j < WIN; ++j) r->o[j] = j >= WIN - s->wl ? s->win[j - (WIN - s->wl)] : (uint16_t)(256 + j);
@@ -975,6 +1045,18 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
   return DPGZ_OK;
 }
 
+typedef struct {
+  uint8_t* dst;
+  const uint8_t* src;
+  uint64_t n;
+} CopyJob;
+#define COPY_PART (1u << 20)
+static void job_copy(void* a, int i) {
+  CopyJob* c = (CopyJob*)a;
+  const uint64_t o = (uint64_t)i * COPY_PART;
+  memcpy(c->dst + o, c->src + o, c->n - o < COPY_PART ? c->n - o : COPY_PART);
+}
+
 int dpgz_par_set_region(dpgz_par* s, uint64_t bytes) {
   if (!s || bytes < 64) return DPGZ_ERR_INVALID;
   s->region_min = bytes;
@@ -985,7 +1067,12 @@ int dpgz_par_feed(dpgz_par* s, const uint8_t* in, uint64_t in_len, int in_final)
   if (!s || (!in && in_len)) return DPGZ_ERR_INVALID;
   if (s->failed) return s->failed;
   if (grow((void**)&s->cin, &s->ccap, s->clen + in_len + 8, 1)) return s->failed = DPGZ_ERR_MEMORY;
-  if (in_len) memcpy(s->cin + s->clen, in, in_len);
+  if (in_len >= 4 * COPY_PART && s->threads > 1) {
+    CopyJob c = {s->cin + s->clen, in, in_len};
+    pfor((int)((in_len + COPY_PART - 1) / COPY_PART), s->threads, job_copy, &c);
+  } else if (in_len) {
+    memcpy(s->cin + s->clen, in, in_len);
+  }
   s->clen += in_len;
   const uint64_t want = (uint64_t)s->threads * s->region_min;
   for (;;) {
@@ -1001,18 +1088,6 @@ int dpgz_par_feed(dpgz_par* s, const uint8_t* in, uint64_t in_len, int in_final)
     }
   }
   return DPGZ_OK;
-}
-
-typedef struct {
-  uint8_t* dst;
-  const uint8_t* src;
-  uint64_t n;
-} CopyJob;
-#define COPY_PART (1u << 20)
-static void job_copy(void* a, int i) {
-  CopyJob* c = (CopyJob*)a;
-  const uint64_t o = (uint64_t)i * COPY_PART;
-  memcpy(c->dst + o, c->src + o, c->n - o < COPY_PART ? c->n - o : COPY_PART);
 }
 
 int dpgz_par_read(dpgz_par* s, uint8_t* out, uint64_t cap, uint64_t* n) {

@@ -1,8 +1,3 @@
 set -o pipefail
-O=gpurun_out/ab17; mkdir -p $O
-L=dataplug_amd/lib
-for i in 1 2; do
- for v in pre fix2 ad5 ad3; do
-  DPSCAN_LIB=$L/libdpscan_v_$v.so timeout -k 10 300 python tools/probe_delim_modes.py --gib 8 >> $O/$v.log 2>&1 || exit 1
- done
-done
+timeout -k 10 300 python tools/gz_par_rate.py --threads 1,8,16 > gpurun_out/gzrate3.log 2>&1 &&
+timeout -k 10 600 python -u tools/fastq_rate.py --device-gib 16 > gpurun_out/fastq_rate3.log 2>&1

@@ -25,8 +25,9 @@ def run(blob: bytes, threads: int, region: int, out: np.ndarray):
     t0 = time.perf_counter()
     total = 0
     step = 4 << 20
+    mv = memoryview(blob)
     for i in range(0, len(blob), step):
-        pi.feed(blob[i:i + step], i + step >= len(blob))
+        pi.feed(mv[i:i + step], i + step >= len(blob))
         while True:
             n = pi.read_into(out, 0, len(out))
             if not n:
