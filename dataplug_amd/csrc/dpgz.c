@@ -16,7 +16,7 @@
  *
  * Streaming form (dpgz_stream_*): the same points while the object passes through in bounded pieces, each
  * point carrying its own window.  BGZF-style members (compressed size in the header) are inflated
- * independently on a thread pool (dpgz_bgzf_scan + dpgz_inflate_members).
+ * independently on a thread pool (dpgz_bgzf_scan + dpgz_inflate_members, with dpgz_par.c's decoder).
  *
  * C ABI (declared in include/dpgz.h), no exceptions, int status (0 = ok).
  */
@@ -322,29 +322,23 @@ typedef struct {
   int rc;
 } members_job;
 
+/* dpgz_par.c's decoder for one whole member (faster than zlib's inflate on these CPUs; CRC-checked) */
+int dpgz__member(const uint8_t* gz, uint64_t len, uint8_t* out, uint64_t out_len, void** scratch);
+void dpgz__member_free(void* scratch);
+
 static void* members_worker(void* arg) {
   members_job* j = (members_job*)arg;
+  void* scratch = NULL;
   for (;;) {
     const uint64_t i = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
     if (i >= j->n || __atomic_load_n(&j->rc, __ATOMIC_RELAXED)) break;
-    z_stream z;
-    memset(&z, 0, sizeof(z));
-    int rc = DPGZ_OK;
-    if (inflateInit2(&z, 31) != Z_OK) rc = DPGZ_ERR_ZLIB;
-    if (rc == DPGZ_OK) {
-      z.next_in = (Bytef*)(j->gz + j->in_off[i]);
-      z.avail_in = (uInt)j->in_len[i];
-      z.next_out = j->out + j->out_off[i];
-      z.avail_out = (uInt)j->out_len[i];
-      const int zr = inflate(&z, Z_FINISH);
-      if (zr != Z_STREAM_END || z.total_out != j->out_len[i]) rc = zr == Z_BUF_ERROR ? DPGZ_ERR_TRUNCATED : DPGZ_ERR_ZLIB;
-      inflateEnd(&z);
-    }
+    const int rc = dpgz__member(j->gz + j->in_off[i], j->in_len[i], j->out + j->out_off[i], j->out_len[i], &scratch);
     if (rc) {
       int zero = 0;
       __atomic_compare_exchange_n(&j->rc, &zero, rc, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
     }
   }
+  dpgz__member_free(scratch);
   return NULL;
 }
 

@@ -685,6 +685,46 @@ static uint64_t find_block(Region* r, const uint8_t* buf, uint64_t nbytes, uint6
   return NONE;
 }
 
+/* One complete gzip member (header to trailer, nothing after it but zero padding) into out[0, out_len)
+ * exactly, CRC-32 and ISIZE checked; the BGZF member-parallel path.  *scratch: a decoder state this
+ * thread reuses (NULL at first; free with dpgz__member_free). */
+int dpgz__member(const uint8_t* gz, uint64_t len, uint8_t* out, uint64_t out_len, void** scratch) {
+  Region* r = (Region*)*scratch;
+  if (!r) {
+    r = (Region*)calloc(1, sizeof(Region));
+    if (!r) return DPGZ_ERR_MEMORY;
+    *scratch = r;
+  }
+  r->start = 0;
+  r->start_kind = K_HEADER;
+  r->stop_at = NONE;
+  r->floor0 = WIN;
+  r->n = 0;
+  if (reserve(r, WIN + out_len + 1024)) return DPGZ_ERR_MEMORY;
+  decode_region(r, gz, len, 1);
+  if (r->rc == D_MEM) return DPGZ_ERR_MEMORY;
+  if (r->rc == D_TRUNC) return DPGZ_ERR_TRUNCATED;
+  if (r->rc != D_OK || r->end_kind != K_END) return DPGZ_ERR_ZLIB;
+  const uint64_t m = r->n - WIN;
+  uint32_t crc = 0, nmend = 0;
+  uint64_t isize = 0;
+  for (uint64_t e = 0; e < r->nev; ++e)
+    if (r->ev[e].kind == EV_MEND) { crc = r->ev[e].crc; isize = r->ev[e].isize; ++nmend; }
+  if (nmend != 1 || m != out_len || (m & 0xFFFFFFFFull) != isize) return DPGZ_ERR_ZLIB;
+  const uint16_t* o = r->o + WIN;
+  for (uint64_t i = 0; i < m; ++i) out[i] = (uint8_t)o[i];
+  if (crc32_fast(0u, out, m) != crc) return DPGZ_ERR_ZLIB;
+  return DPGZ_OK;
+}
+
+void dpgz__member_free(void* scratch) {
+  Region* r = (Region*)scratch;
+  if (!r) return;
+  free(r->o);
+  free(r->ev);
+  free(r);
+}
+
 /* ------------------------------------------------------------------------------------------ the engine */
 struct dpgz_par {
   uint64_t span;

@@ -1246,9 +1246,18 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
     }
     return any;
   };
+#ifdef DP_TL_COORD
+  uint32_t it = 0;                                  // coordinator iterations traced into timeline slots 72..95
+#define TL_IT(e) do { if (it < 24u) TL_STAMP(72u + it, e); } while (0)
+#else
+#define TL_IT(e) do {} while (0)
+#endif
   while (res < K) {
+    TL_IT(0);
     bool prog = claim_ahead();
+    TL_IT(1);
     prog |= compose_ready();
+    TL_IT(2);
     PROF_MARK(0);
     if (res < pub) {
       const uint32_t D = pub - res < kLbDepth ? pub - res : kLbDepth;
@@ -1317,6 +1326,10 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
       }
       PROF_MARK(1);
     }
+    TL_IT(3);
+#ifdef DP_TL_COORD
+    it += prog ? 1u : 0u;
+#endif
     if (prog) {
       idle = 0;
       idle_t0 = 0;

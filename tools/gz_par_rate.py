@@ -53,6 +53,17 @@ def main():
     print(json.dumps({"inflated_bytes": len(raw), "gzip_bytes": len(blob),
                       "zlib_1core_GiB_per_s": round(len(raw) / tz / 2**30, 3)}), flush=True)
     out = np.zeros(64 << 20, np.uint8)
+    # BGZF: every member inflated independently (gz.bgzf_scan + gz.inflate_members), whole object at once
+    bg = np.frombuffer(synth.bgzf(raw, level=6), np.uint8)
+    a, ln, ol, used = gz.bgzf_scan(bg)
+    oo = np.concatenate(([0], np.cumsum(ol)[:-1])).astype(np.uint64)
+    big = np.zeros(int(ol.sum()), np.uint8)
+    for th in (int(x) for x in args.threads.split(",")):
+        t0 = time.perf_counter()
+        gz.inflate_members(bg, a, ln, oo, ol, big.ctypes.data, th)
+        dt = time.perf_counter() - t0
+        print(json.dumps({"bgzf_threads": th, "members": len(a), "GiB_per_s": round(len(big) / dt / 2**30, 3),
+                          "ok": big.tobytes() == ref}), flush=True)
     for th in (int(x) for x in args.threads.split(",")):
         n, dt, st = run(blob, th, args.region_kib << 10, out)
         print(json.dumps({"threads": th, "GiB_per_s": round(n / dt / 2**30, 3), "ok": n == len(ref),
