@@ -152,8 +152,32 @@ class _Inflater(threading.Thread):
         """A plain gzip stream inflated on the thread pool (libdpgz dpgz_par_*: speculative block starts,
         marker windows, CRC-checked), drained into the pieces in order."""
         pi = gzlib.ParInflate(self.span, self.threads, region_bytes=self.region_bytes)
+        # compressed bytes are read ahead on their own thread (up to 16 reads), so the GET body's copies
+        # overlap the engine's batches
+        inq: "queue.Queue[Optional[bytes]]" = queue.Queue(maxsize=16)
+        stop_reading = threading.Event()
+
+        def reader():
+            try:
+                while not stop_reading.is_set():
+                    data = self.read(PAR_READ_BYTES)
+                    while not stop_reading.is_set():
+                        try:
+                            inq.put(data, timeout=0.5)
+                            break
+                        except queue.Full:
+                            continue
+                    if not data:
+                        return
+            except BaseException as e:                   # surfaced by the inflater loop
+                self.error = e
+                inq.put(b"")
+
+        rt = threading.Thread(target=reader, daemon=True, name="dpgz-read")
         try:
             final = len(first) == 0
+            if not final:
+                rt.start()
             pi.feed(first, final)
             o0, slot, filled, out = 0, None, 0, None
             while True:
@@ -186,10 +210,15 @@ class _Inflater(threading.Thread):
                     return
                 if final:
                     raise ValueError("gzip stream: truncated")
-                data = self.read(PAR_READ_BYTES)
+                data = inq.get()
+                if self.error is not None:
+                    raise self.error
                 final = len(data) == 0
                 pi.feed(data, final)
         finally:
+            stop_reading.set()
+            if rt.is_alive():
+                rt.join()
             pi.close()
 
     def _run_bgzf(self, first: bytes):
@@ -228,12 +257,14 @@ class _Inflater(threading.Thread):
             gzlib.inflate_members(cbuf, a[:k], l[:k], out_off, o[:k], out.ctypes.data, self.threads)
             # member-start access points, at most one per span of inflated bytes
             rows = []
-            for i in range(k):
-                ob = o0 + int(out_off[i])
-                if last_point is None or ob - last_point >= self.span:
-                    pb = prev_byte if i == 0 else int(out[int(out_off[i]) - 1]) if out_off[i] else prev_byte
-                    rows.append((in_base + int(a[i]), ob, 0, 1, pb, 0))
-                    last_point = ob
+            starts = out_off[:k].astype(np.int64) + o0
+            i = 0 if last_point is None else int(np.searchsorted(starts, last_point + self.span))
+            while i < k:                                 # greedy: the first member start >= span past the last
+                ob = int(starts[i])
+                pb = int(out[ob - o0 - 1]) if ob > o0 else prev_byte
+                rows.append((in_base + int(a[i]), ob, 0, 1, pb, 0))
+                last_point = ob
+                i = int(np.searchsorted(starts, last_point + self.span))
             n = int(cum[k - 1])
             if n:
                 prev_byte = int(out[n - 1])
