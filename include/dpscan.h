@@ -6,9 +6,10 @@
  * the message of the last failure on the calling thread is available from dp_last_error().  No C++
  * exception crosses this boundary.  A dp_ctx is bound to one device and owns one stream plus the
  * scan workspace; use one ctx per host thread (calls on distinct ctx are thread-safe, and ctypes
- * releases the GIL around them).  Scan kernels of different ctx on one device run one after another
- * (each launch waits on the device for the previous one): the persistent scan grid needs every one
- * of its workgroups resident.
+ * releases the GIL around them).  Scan kernels of different ctx on one device (in one process) run one
+ * after another (each launch waits on the device for the previous one: one grid fills the chip).  The
+ * persistent grid's workgroups claim their units from a ticket at run time, so a grid never waits on a
+ * workgroup that has not started: grids of different processes may share a GPU.
  *
  * Reference interfaces each entry point replaces (CLOUDLAB-URV/dataplug @ 2025-07-11):
  *   dp_fasta_index  <- dataplug/formats/genomics/fasta.py:24-63 (preprocess_fasta: the per-chunk
