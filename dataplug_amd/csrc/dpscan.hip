@@ -1153,7 +1153,7 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
 }
 
 #ifndef DP_LBDEPTH
-#define DP_LBDEPTH 8
+#define DP_LBDEPTH 6
 #endif
 #ifndef DP_IDLE_SLEEP    // coordinator back-off (x 64 clocks) after a round without progress
 #define DP_IDLE_SLEEP 1
@@ -1168,7 +1168,10 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
 #ifndef DP_COORD_PRIO_DELIM
 #define DP_COORD_PRIO_DELIM 0
 #endif
-constexpr uint32_t kLbDepth = DP_LBDEPTH;          // look-back windows in flight per coordinator attempt
+// look-back windows in flight per coordinator attempt: 8 windows (64 VGPRs of descriptors) pushed the
+// coordinator path past the kernel's 128 VGPRs and spilled to scratch (44-52 B/lane); 6 spills nothing
+// (FASTA +1.4-2.3 % same box, DELIM +-1 %)
+constexpr uint32_t kLbDepth = DP_LBDEPTH;
 
 // consecutive units per ticket atomic: one returning atomic on one address per unit caps the grid near
 // 20 units/us (measured: FASTA -16% at 1, -7% at 2, parity at 4); a longer run of consecutive units
