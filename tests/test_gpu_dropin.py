@@ -7,6 +7,7 @@ CSV/VCF: the GPU newline index equals the bytes' '\\n' positions and the partiti
 get() outputs.  FASTQ.gz: total_lines and per-read ends on the inflated stream, read batches' lines."""
 import base64
 import gzip
+import io
 import builtins
 import json
 import os
@@ -241,6 +242,32 @@ def test_fastq_gz_reads(kind, piece):
     batches = co.partition(partition_reads_batches, num_batches=7)
     got = [ln for b in batches for ln in b.get()]
     assert got == [x.decode() for x in lines]
+
+
+@pytest.mark.parametrize("threads,region", [(16, 1 << 16), (6, 1 << 18)])
+def test_fastq_gz_parallel_inflate_on_gpu(threads, region):
+    """One ~14 MB gzip member inflated by the parallel engine with small speculative regions (many batches,
+    hundreds of region starts) streamed through the GPU newline scan in 1 MB pieces: every read end equals
+    the reads' own line ends, the access points and their windows equal the zlib stream index's."""
+    from dataplug_amd import gz as gzlib
+    from dataplug_amd.scan import get_context
+    from dataplug_amd.scan import gzindex
+    raw = synth.fastq(60_000, seed=9).tobytes()
+    blob = gzip.compress(raw, 6)
+    f = io.BytesIO(blob)
+    ix = gzindex.index_stream(get_context(0), lambda n: f.read(n), record_lines=4, span=1 << 18,
+                              piece_bytes=1_000_003, threads=threads, region_bytes=region)
+    nl = np.flatnonzero(np.frombuffer(raw, np.uint8) == 10).astype(np.uint64)
+    assert np.array_equal(np.frombuffer(ix.ends.read(), "<u8"), nl[3::4] + np.uint64(1))
+    assert ix.newlines == len(nl) and ix.uncompressed_size == len(raw) and ix.members == 1
+    _, pts = gzlib.build_index(blob, span=1 << 18)
+    assert [r[1] for r in ix.rows] == pts["in_byte"].tolist()
+    assert [r[2] for r in ix.rows] == pts["out_byte"].tolist()
+    assert [r[6] for r in ix.rows] == pts["bits"].tolist()
+    windows = ix.windows.read()
+    for r in ix.rows:
+        if not r[7]:
+            assert windows[r[5]:r[5] + r[4]] == raw[max(0, r[2] - 32768):r[2]]
 
 
 # ------------------------------------------------------------------------------------------ multi-GPU split
