@@ -7,10 +7,10 @@
 //   * fasta_resolve_kernel / find_kernel: the "header cut by the chunk end" fix-up (fasta.py:45-56).
 //
 // Single pass, memory-bound (no MFMA):
-//   * persistent grid, one 1024-thread workgroup per CU = 15 data waves + 1 coordinator wave.  Workgroup b
-//     owns the 240 KiB units u = b + k*G; data wave w owns a 16 KiB range of each (16 rows of 64 lanes x
-//     16 B, bounds-checked non-temporal buffer loads into DP_NBUF VGPR buffers: one scanned while the
-//     others are in flight, hand-waited).
+//   * persistent grid, one 1024-thread workgroup per CU = 15 data waves + 1 coordinator wave.  Workgroups
+//     claim runs of consecutive 240 KiB units from a global ticket while they run; data wave w owns a
+//     16 KiB range of each (16 rows of 64 lanes x 16 B, bounds-checked non-temporal buffer loads into
+//     DP_NBUF VGPR buffers: one scanned while the others are in flight, hand-waited).
 //   * byte classes: v_perm_b32 with all-ones data sources returns 0x00 for selector byte 12 and 0xFF for
 //     every other selector, so perm(-1, -1, w ^ (pattern ^ 0x0C0C0C0C)) flags the pattern bytes of w
 //     exactly (2 VALU per dword); v_dot4_i32_i8 packs 4 flags into a nibble.
@@ -26,8 +26,8 @@
 //     to the output at its final index (+ the state fix-up at the range start).  A data wave only waits for
 //     the coordinator once it is kRing units ahead.  Ranges with more than kDenseMax events ("dense") keep
 //     no list; their phase B rescans the range from the input with the now known state.
-//   * every wait is bounded (DP_ERR_TIMEOUT); units are statically strided over a grid of one workgroup
-//     per CU, so a unit only ever waits on lower units owned by running workgroups.
+//   * every wait is bounded (DP_ERR_TIMEOUT); units are claimed in increasing order by running workgroups
+//     only, so a unit only ever waits on lower units owned by running (or finished) workgroups.
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>

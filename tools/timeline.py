@@ -2,7 +2,7 @@
 
     DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof.so python tools/timeline.py [--size BYTES] [--out file.npz]
 
-For every workgroup b (< 256) and its k-th unit u = b + k*G, the kernel stamps the realtime clock (100 MHz)
+For every workgroup b (< 256) and its k-th step (the unit it claimed for it), the kernel stamps the realtime clock (100 MHz)
 when (0) the unit's AGG descriptor is published, (1) the coordinator resolved its prefix, (2) data wave 0
 finished phase A of it (DP_TL_CLAIM builds: the coordinator claimed it); word 3 holds the step's unit index (dynamic assignment).  This prints, per round k, medians over
 workgroups, in microseconds from the launch's first stamp, plus the derived look-back latency: the time
