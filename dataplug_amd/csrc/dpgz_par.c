@@ -237,6 +237,7 @@ typedef struct {
   uint64_t start;             /* bit position */
   int start_kind;             /* K_BLOCK or K_HEADER */
   uint64_t stop_at;           /* stop at this block start (NONE: run to the end of the input) */
+  uint64_t stop_after;        /* with stop_at NONE: stop at the first block start at or past this bit */
   uint64_t floor0;            /* lowest buffer index a back-reference may reach at the start */
   /* output */
   uint16_t* o;                /* [0, WIN): the window (bytes or markers), then the output */
@@ -593,7 +594,11 @@ static void decode_region(Region* r, const uint8_t* buf, uint64_t nbytes, int fi
       kind = K_BLOCK;
       continue;
     }
-    if (pos == r->stop_at) { r->end = pos; r->end_kind = K_BLOCK; return; }
+    if (pos == r->stop_at || (r->stop_at == NONE && pos >= r->stop_after)) {
+      r->end = pos;
+      r->end_kind = K_BLOCK;
+      return;
+    }
     if (r->stop_at != NONE && pos > r->stop_at) { r->overshoot = 1; r->end = pos; r->end_kind = K_BLOCK; return; }
     const uint64_t bstart = pos, ostart = r->n, evmark = r->nev;
     if (add_ev(r, pos, EV_BLOCK, 0, 0)) { r->rc = D_MEM; return; }
@@ -698,6 +703,7 @@ int dpgz__member(const uint8_t* gz, uint64_t len, uint8_t* out, uint64_t out_len
   r->start = 0;
   r->start_kind = K_HEADER;
   r->stop_at = NONE;
+  r->stop_after = NONE;
   r->floor0 = WIN;
   r->n = 0;
   if (reserve(r, WIN + out_len + 1024)) return DPGZ_ERR_MEMORY;
@@ -920,7 +926,12 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
   if (s->kind == K_END) return DPGZ_OK;
   const uint64_t nbytes = s->clen;
   const uint64_t b0 = s->pos >> 3;
-  const uint64_t avail = nbytes - b0;
+  /* at most two batches' worth of regions at a time (bounded memory whatever the caller feeds); the last
+   * region then stops at the first block start past the batch and the rest waits for the next batch */
+  const uint64_t cap_bytes = 2ull * (uint64_t)s->threads * s->region_min;
+  const int whole = nbytes - b0 <= cap_bytes;
+  const uint64_t avail = whole ? nbytes - b0 : cap_bytes;
+  if (!whole) final = 0;
   int nreg = (int)(avail / s->region_min);
   if (nreg > s->threads) nreg = s->threads;
   if (nreg < 1) nreg = 1;
@@ -946,6 +957,7 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
     r->start = k == 0 ? s->pos : found[idx[k]];
     r->start_kind = k == 0 ? s->kind : K_BLOCK;
     r->stop_at = k + 1 < nkeep ? found[idx[k + 1]] : NONE;
+    r->stop_after = k + 1 < nkeep || whole ? NONE : (b0 + avail) * 8;
     r->n = 0;                                           /* the buffer is reused: only the window is kept */
     if (reserve(r, WIN + (4u << 20))) return DPGZ_ERR_MEMORY;
     if (k == 0) {                                       /* the known window, right-aligned */
