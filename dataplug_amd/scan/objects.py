@@ -20,6 +20,13 @@ from ..storage.ranges import GET_PART as _GET_PART, GET_THREADS as _GET_THREADS,
 from .device import ScanContext, device_count, get_context
 
 _HALO0 = 64 << 10             # first look-ahead window when a header line crosses the fetched bytes
+# bytes one FASTA launch holds in HBM at most: a GPU's chunk group larger than this (an object far beyond
+# 288 GB x GPUs, or a small budget set for tests) is scanned in several passes of whole chunks
+MAX_LAUNCH_BYTES = 64 << 30
+
+
+def max_launch_bytes() -> int:
+    return int(os.environ.get("DATAPLUG_AMD_MAX_LAUNCH_BYTES", MAX_LAUNCH_BYTES))
 
 
 DEVICES_ATTR = "_dataplug_devices"
@@ -143,20 +150,46 @@ def fasta_groups(plan: Sequence[Tuple[int, int]], n_groups: int, size: int, halo
     return out
 
 
+def fasta_passes(plan: Sequence[Tuple[int, int]], g: FastaGroup, size: int, budget: int,
+                 halo: int = _HALO0) -> List[FastaGroup]:
+    """``g`` cut into consecutive runs of whole chunks whose bytes span at most ``budget`` (a chunk larger
+    than the budget is a pass of its own).  Chunks are independent (preprocess.py:39-51), so the passes'
+    pairs concatenate in chunk order like the groups' do."""
+    if g.buf_hi - g.lo <= budget:
+        return [g]
+    out = []
+    i = g.i0
+    while i < g.i1:
+        lo, hi = plan[i]
+        j = i + 1
+        while j < g.i1:
+            nlo, nhi = min(lo, plan[j][0]), max(hi, plan[j][1])
+            if min(size, nhi + halo) - nlo > budget:
+                break
+            lo, hi = nlo, nhi
+            j += 1
+        out.append(FastaGroup(i, j, lo, hi, min(size, hi + halo)))
+        i = j
+    return out
+
+
 def _fasta_group(dev: int, co, plan: Sequence[Tuple[int, int]], g: FastaGroup, u64: bool) -> np.ndarray:
     ctx = get_context(dev)
     size = co.size
-    n = g.buf_hi - g.lo
-    d = ctx.workspace("input", n + 64)
-    fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, g.lo, g.buf_hi, d.ptr)
-    pairs, pending, _ = ctx.fasta_index(d.ptr, n, g.lo, size, g.chunks(plan), u64=u64)
-    for p in pending[pending >= 0]:
-        start = int(pairs[p, 0])
-        end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, size, g.buf_hi)
-        if not u64 and end > 0xFFFFFFFF:
-            raise OverflowError(f"FASTA offset {end} does not fit the uint32 index (header at {start})")
-        pairs[p, 1] = end
-    return pairs
+    parts = []
+    for p_ in fasta_passes(plan, g, size, max_launch_bytes()):
+        n = p_.buf_hi - p_.lo
+        d = ctx.workspace("input", n + 64)
+        fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, p_.lo, p_.buf_hi, d.ptr)
+        pairs, pending, _ = ctx.fasta_index(d.ptr, n, p_.lo, size, p_.chunks(plan), u64=u64)
+        for p in pending[pending >= 0]:
+            start = int(pairs[p, 0])
+            end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, size, p_.buf_hi)
+            if not u64 and end > 0xFFFFFFFF:
+                raise OverflowError(f"FASTA offset {end} does not fit the uint32 index (header at {start})")
+            pairs[p, 1] = end
+        parts.append(pairs)
+    return parts[0] if len(parts) == 1 else np.concatenate(parts)
 
 
 def fasta_index_object(co, plan: Sequence[Tuple[int, int]], u64: bool = False,

@@ -269,3 +269,25 @@ def test_get_slices_first_error_in_slice_order():
     assert get_slices([S(i) for i in (0, 1, 2)], threads=4) == [0, 1, 2]
     with pytest.raises(ValueError, match="slice 3"):
         get_slices([S(i) for i in range(10)], threads=4)
+
+
+def test_fasta_passes_cover_group_in_order():
+    """scan.objects.fasta_passes: consecutive runs of whole chunks within the byte budget (a larger chunk
+    alone), covering the group's chunks exactly once, in order, each pass's fetched bytes within budget."""
+    from dataplug_amd.scan.objects import FastaGroup, fasta_passes
+    size = 10_000_000
+    plan = [(i * 700_000, min(size, (i + 1) * 700_000)) for i in range(15)]
+    g = FastaGroup(2, 13, plan[2][0], plan[12][1], min(size, plan[12][1] + 65_536))
+    for budget in (1 << 40, 3_000_000, 800_000, 100):
+        ps = fasta_passes(plan, g, size, budget)
+        assert ps[0].i0 == g.i0 and ps[-1].i1 == g.i1
+        assert all(a.i1 == b.i0 for a, b in zip(ps, ps[1:]))
+        for p in ps:
+            assert p.lo == min(c0 for c0, _ in plan[p.i0:p.i1]) and p.hi == max(c1 for _, c1 in plan[p.i0:p.i1])
+            assert p.buf_hi - p.lo <= budget or p.i1 - p.i0 == 1
+        if budget == 1 << 40:
+            assert ps == [g]
+    # the reference's cs == n - 1 quirk: every chunk reads to EOF, so every chunk is a pass of its own
+    quirk = [(i * 3, size) for i in range(4)]
+    gq = FastaGroup(0, 4, 0, size, size)
+    assert [(p.i0, p.i1) for p in fasta_passes(quirk, gq, size, size // 2)] == [(0, 1), (1, 2), (2, 3), (3, 4)]

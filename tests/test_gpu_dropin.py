@@ -108,6 +108,22 @@ def test_fasta_synthetic_groups(monkeypatch, devices, div):
     assert np.array_equal(_index(co), exp.reshape(-1).astype(np.uint32))
 
 
+@pytest.mark.parametrize("devices,div,budget", [("0", 64, 3 << 20), ("0,0,0", 9, 5 << 20), ("0", 1000, 1 << 20)])
+def test_fasta_launch_budget_passes(monkeypatch, devices, div, budget):
+    """A launch byte budget far below a GPU's group (DATAPLUG_AMD_MAX_LAUNCH_BYTES): each group is scanned
+    in several passes of whole chunks; the index still equals the reference's."""
+    from oracle import cpu_ref, dpref
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", devices)
+    monkeypatch.setenv("DATAPLUG_AMD_MAX_LAUNCH_BYTES", str(budget))
+    data = synth.fasta(24 << 20, 70 + div)
+    cs = -(-len(data) // div)
+    co = _co(FASTA, data.tobytes(), f"bud{div}", _mem(f"gpu_bud_{div}_{len(devices)}"))
+    co.preprocess(chunk_size=cs)
+    exp = dpref.fasta_pairs(data, cpu_ref.chunk_plan(len(data), cs))
+    assert np.array_equal(_index(co), exp.reshape(-1).astype(np.uint32))
+
+
 @pytest.mark.parametrize("part", [None, (1 << 20) + 13])
 @pytest.mark.parametrize("where", ["memory", "loopback"])
 def test_fasta_pipelined_fetch_many_parts(server, monkeypatch, part, where):
