@@ -7,6 +7,7 @@ returning `buffer_atomic_* … sc0`) into register(s) R until a wait that the lo
 vector-memory operations issued after it), no instruction may read or write R (dataflow over the
 kernel's basic blocks, tracking the ordered queue of outstanding vector-memory operations).  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
 (without an argument it compiles the kernel with -save-temps into a temp dir; DP_DEFINES=A=1,B adds -D's).
+It also fails if a scan kernel has a scratch segment (register spills to memory).
 """
 from __future__ import annotations
 
@@ -156,10 +157,27 @@ def check(asm_path: str):
     return problems
 
 
+def scratch(asm_path: str):
+    """Scan kernels with a private (scratch) segment: register spills to memory.  A spill reload in the
+    coordinator queues behind the CU's input stream (8 look-back windows did this: FASTA -2 %)."""
+    text = open(asm_path).read()
+    out = []
+    for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, re.S):
+        if "scan_kernel" not in m.group(1):
+            continue
+        sz = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(2))
+        if sz and int(sz.group(1)) > 0:
+            out.append((m.group(1), int(sz.group(1))))
+    return out
+
+
 if __name__ == "__main__":
     path = sys.argv[1] if len(sys.argv) > 1 else compile_asm()
     bad = check(path)
     for p in bad[:20]:
         print("touches an un-waited load destination:", p)
-    print("ISA guard:", "FAIL" if bad else "ok", len(bad))
-    sys.exit(1 if bad else 0)
+    spills = scratch(path)
+    for k, n in spills:
+        print(f"scratch segment of {n} B per lane (register spills) in {k}")
+    print("ISA guard:", "FAIL" if bad or spills else "ok", len(bad) + len(spills))
+    sys.exit(1 if bad or spills else 0)
