@@ -322,38 +322,39 @@ typedef struct {
   int rc;
 } members_job;
 
-/* dpgz_par.c's decoder for one whole member (faster than zlib's inflate on these CPUs; CRC-checked) */
+/* dpgz_par.c's decoder for one whole member (faster than zlib's inflate on these CPUs; CRC-checked), its
+ * per-thread state, and its process-wide thread pool */
 int dpgz__member(const uint8_t* gz, uint64_t len, uint8_t* out, uint64_t out_len, void** scratch);
-void dpgz__member_free(void* scratch);
+void* dpgz__scratch_get(void);
+void dpgz__scratch_put(void* scratch);
+void dpgz__global_for(int threads, int n, void (*fn)(void*, int), void* arg);
 
-static void* members_worker(void* arg) {
+#define MEMBERS_PER_ITEM 1u
+static void members_item(void* arg, int item) {
   members_job* j = (members_job*)arg;
-  void* scratch = NULL;
-  for (;;) {
-    const uint64_t i = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
-    if (i >= j->n || __atomic_load_n(&j->rc, __ATOMIC_RELAXED)) break;
+  void* scratch = dpgz__scratch_get();
+  const uint64_t i0 = (uint64_t)item * MEMBERS_PER_ITEM;
+  for (uint64_t i = i0; i < j->n && i < i0 + MEMBERS_PER_ITEM; ++i) {
+    if (__atomic_load_n(&j->rc, __ATOMIC_RELAXED)) break;
     const int rc = dpgz__member(j->gz + j->in_off[i], j->in_len[i], j->out + j->out_off[i], j->out_len[i], &scratch);
     if (rc) {
       int zero = 0;
       __atomic_compare_exchange_n(&j->rc, &zero, rc, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
     }
   }
-  dpgz__member_free(scratch);
-  return NULL;
+  dpgz__scratch_put(scratch);
 }
 
 int dpgz_inflate_members(const uint8_t* gz, const uint64_t* in_off, const uint64_t* in_len, const uint64_t* out_off,
                          const uint64_t* out_len, uint64_t n, uint8_t* out, int threads) {
   if ((!gz || !in_off || !in_len || !out_off || !out_len || !out) && n) return DPGZ_ERR_INVALID;
   members_job j = {gz, in_off, in_len, out_off, out_len, out, n, 0, DPGZ_OK};
-  int nt = threads > 0 ? threads : 1;
-  if ((uint64_t)nt > n) nt = (int)(n ? n : 1);
-  pthread_t th[256];
-  if (nt > 256) nt = 256;
-  int started = 0;
-  for (int t = 1; t < nt; ++t)
-    if (pthread_create(&th[t], NULL, members_worker, &j) == 0) ++started; else break;
-  members_worker(&j);
-  for (int t = 1; t <= started; ++t) pthread_join(th[t], NULL);
+  const uint64_t items = (n + MEMBERS_PER_ITEM - 1) / MEMBERS_PER_ITEM;
+  if (items > 0x7FFFFFFFull) return DPGZ_ERR_INVALID;
+  if (threads <= 1 || items <= 1) {
+    for (uint64_t k = 0; k < items; ++k) members_item(&j, (int)k);
+  } else {
+    dpgz__global_for(threads, (int)items, members_item, &j);
+  }
   return j.rc;
 }

@@ -23,6 +23,7 @@
  * bytes, 2 bytes per inflated byte of one batch, and the resolved output until it is read.
  */
 #include <pthread.h>
+#include <time.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -37,7 +38,7 @@
 #define DTAB (256 + 30 * 128)
 #define CLTAB 128
 #define E_SUB 0x100000u
-#define REGION_MIN (2u << 20)           /* compressed bytes per region, at least (default) */
+#define REGION_MIN (1u << 20)           /* compressed bytes per region, at least (default) */
 #define NONE UINT64_MAX
 
 enum { K_BLOCK = 0, K_HEADER = 1, K_END = 2 };           /* what starts at a stop position */
@@ -731,7 +732,143 @@ void dpgz__member_free(void* scratch) {
   free(r);
 }
 
+
 /* ------------------------------------------------------------------------------------------ the engine */
+/* ---- a parallel-for over a pool of worker threads that live as long as the engine (one batch runs 2-4
+ * parallel loops; creating and joining 15 threads per loop cost ~1 ms per batch) */
+typedef struct {
+  void (*fn)(void*, int);
+  void* arg;
+  int n;
+  int next;
+} PFor;
+static void pfor_worker(PFor* p) {
+  for (;;) {
+    const int i = __atomic_fetch_add(&p->next, 1, __ATOMIC_RELAXED);
+    if (i >= p->n) break;
+    p->fn(p->arg, i);
+  }
+}
+struct Pool;
+typedef struct {
+  struct Pool* p;
+  int id;
+} PoolWorker;
+typedef struct Pool {
+  pthread_t th[256];
+  PoolWorker w[256];
+  int n;                      /* workers (the calling thread is one more) */
+  pthread_mutex_t m;
+  pthread_cond_t go, done;
+  uint64_t gen;
+  int quit, active;
+  int limit;                  /* workers taking part in the current loop */
+  PFor* job;
+} Pool;
+static void* pool_main(void* a) {
+  PoolWorker* me = (PoolWorker*)a;
+  Pool* p = me->p;
+  uint64_t seen = 0;
+  pthread_mutex_lock(&p->m);
+  for (;;) {
+    while (p->gen == seen && !p->quit) pthread_cond_wait(&p->go, &p->m);
+    if (p->quit) break;
+    seen = p->gen;
+    PFor* j = p->job;
+    const int take = me->id < p->limit;
+    pthread_mutex_unlock(&p->m);
+    if (take) pfor_worker(j);
+    pthread_mutex_lock(&p->m);
+    if (--p->active == 0) pthread_cond_signal(&p->done);
+  }
+  pthread_mutex_unlock(&p->m);
+  return NULL;
+}
+static int pool_init(Pool* p, int workers) {
+  memset(p, 0, sizeof(*p));
+  pthread_mutex_init(&p->m, NULL);
+  pthread_cond_init(&p->go, NULL);
+  pthread_cond_init(&p->done, NULL);
+  for (int t = 0; t < workers && t < 256; ++t) {
+    p->w[t].p = p;
+    p->w[t].id = t;
+    if (pthread_create(&p->th[t], NULL, pool_main, &p->w[t]) != 0) break;
+    p->n++;
+  }
+  return 0;
+}
+static void pool_free(Pool* p) {
+  pthread_mutex_lock(&p->m);
+  p->quit = 1;
+  pthread_cond_broadcast(&p->go);
+  pthread_mutex_unlock(&p->m);
+  for (int t = 0; t < p->n; ++t) pthread_join(p->th[t], NULL);
+  pthread_cond_destroy(&p->go);
+  pthread_cond_destroy(&p->done);
+  pthread_mutex_destroy(&p->m);
+}
+/* fn(arg, i) for i in [0, n) on the calling thread and up to threads - 1 of the pool's workers */
+static void pool_for_n(Pool* p, int threads, int n, void (*fn)(void*, int), void* arg) {
+  PFor j = {fn, arg, n, 0};
+  if (p->n == 0 || n <= 1 || threads <= 1) {
+    pfor_worker(&j);
+    return;
+  }
+  pthread_mutex_lock(&p->m);
+  p->job = &j;
+  p->limit = threads - 1;
+  p->active = p->n;
+  p->gen++;
+  pthread_cond_broadcast(&p->go);
+  pthread_mutex_unlock(&p->m);
+  pfor_worker(&j);
+  pthread_mutex_lock(&p->m);
+  while (p->active) pthread_cond_wait(&p->done, &p->m);
+  pthread_mutex_unlock(&p->m);
+}
+static void pool_for(Pool* p, int n, void (*fn)(void*, int), void* arg) { pool_for_n(p, p->n + 1, n, fn, arg); }
+
+/* The BGZF member-parallel path (dpgz.c) runs on one process-wide pool, created at the first call with
+ * that call's thread count and kept (no thread creation per batch of members); calls are serialized.  Each
+ * thread keeps its member decoder state across calls (pthread key, freed at thread exit). */
+static Pool g_pool;
+static int g_pool_ready;
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static pthread_key_t g_scratch_key;
+static pthread_once_t g_scratch_once = PTHREAD_ONCE_INIT;
+static void scratch_key_init(void) { pthread_key_create(&g_scratch_key, dpgz__member_free); }
+void* dpgz__scratch_get(void) {
+  pthread_once(&g_scratch_once, scratch_key_init);
+  return pthread_getspecific(g_scratch_key);
+}
+void dpgz__scratch_put(void* scratch) {
+  pthread_once(&g_scratch_once, scratch_key_init);
+  pthread_setspecific(g_scratch_key, scratch);
+}
+static void pool_after_fork_child(void) {   /* the workers do not exist in a forked child: start over */
+  pthread_mutex_init(&g_pool_mu, NULL);
+  g_pool_ready = 0;
+}
+void dpgz__global_for(int threads, int n, void (*fn)(void*, int), void* arg) {
+  if (threads > 256) threads = 256;
+  pthread_mutex_lock(&g_pool_mu);
+  if (g_pool_ready && g_pool.n < threads - 1) {         /* more threads than the pool has: regrow it */
+    pool_free(&g_pool);
+    g_pool_ready = 0;
+  }
+  if (!g_pool_ready) {
+    static int atfork_done;
+    if (!atfork_done) {
+      pthread_atfork(NULL, NULL, pool_after_fork_child);
+      atfork_done = 1;
+    }
+    pool_init(&g_pool, threads - 1);
+    g_pool_ready = 1;
+  }
+  pool_for_n(&g_pool, threads, n, fn, arg);
+  pthread_mutex_unlock(&g_pool_mu);
+}
+
 struct dpgz_par {
   uint64_t span;
   int threads;
@@ -759,6 +896,8 @@ struct dpgz_par {
   int nregs;
   uint64_t batches, rejected;
   uint64_t region_min;
+  Pool pool;                  /* threads - 1 workers */
+  uint64_t ns[5];             /* time per phase: find, decode, windows, resolve, in-order bookkeeping */
 };
 
 int dpgz_par_new(uint64_t span, int threads, dpgz_par** out) {
@@ -771,15 +910,17 @@ int dpgz_par_new(uint64_t span, int threads, dpgz_par** out) {
   s->region_min = REGION_MIN;
   s->prev = -1;
   s->crc = (uint32_t)crc32(0L, Z_NULL, 0);
-  s->regs = (Region*)calloc((size_t)s->threads, sizeof(Region));
+  s->nregs = 2 * s->threads;                          /* regions per batch: two per thread (dynamic balance) */
+  s->regs = (Region*)calloc((size_t)s->nregs, sizeof(Region));
   if (!s->regs) { free(s); return DPGZ_ERR_MEMORY; }
-  s->nregs = s->threads;
+  pool_init(&s->pool, s->threads - 1);
   *out = s;
   return DPGZ_OK;
 }
 
 void dpgz_par_free(dpgz_par* s) {
   if (!s) return;
+  pool_free(&s->pool);
   for (int i = 0; i < s->nregs; ++i) {
     free(s->regs[i].o);
     free(s->regs[i].ev);
@@ -792,33 +933,6 @@ void dpgz_par_free(dpgz_par* s) {
   free(s);
 }
 
-/* ---- a tiny parallel-for over pthreads */
-typedef struct {
-  void (*fn)(void*, int);
-  void* arg;
-  int n;
-  int next;
-} PFor;
-static void* pfor_worker(void* a) {
-  PFor* p = (PFor*)a;
-  for (;;) {
-    const int i = __atomic_fetch_add(&p->next, 1, __ATOMIC_RELAXED);
-    if (i >= p->n) break;
-    p->fn(p->arg, i);
-  }
-  return NULL;
-}
-static void pfor(int n, int threads, void (*fn)(void*, int), void* arg) {
-  PFor p = {fn, arg, n, 0};
-  int nt = threads < n ? threads : n;
-  pthread_t th[256];
-  int started = 0;
-  for (int t = 1; t < nt; ++t)
-    if (pthread_create(&th[t], NULL, pfor_worker, &p) == 0) ++started; else break;
-  pfor_worker(&p);
-  for (int t = 1; t <= started; ++t) pthread_join(th[t], NULL);
-}
-
 typedef struct {
   dpgz_par* s;
   int final;
@@ -827,22 +941,36 @@ typedef struct {
   uint64_t* found;            /* found starts */
   int* idx;                   /* region slot of each kept start */
   int nkeep;
+  int nreg;
+  uint64_t stop_last;         /* the last region's stop_after (NONE: the batch holds the rest of the input) */
   uint8_t* dst;               /* the batch's resolved output */
   uint32_t* seg_crc;          /* per region: CRC of its output up to its first member end, then per member */
   uint64_t* seg_len;
   uint64_t* seg_off;          /* first segment of each region in seg_* */
 } Batch;
 
-static void job_find(void* a, int i) {
+static void job_find_decode(void* a, int i) {
   Batch* b = (Batch*)a;
-  if (i == 0) return;
-  b->found[i] = find_block(&b->s->regs[i], b->s->cin, b->nbytes, b->bound[i], b->bound[i + 1]);
-}
-
-static void job_decode(void* a, int k) {
-  Batch* b = (Batch*)a;
-  Region* r = &b->s->regs[b->idx[k]];
-  decode_region(r, b->s->cin, b->nbytes, b->final && k == b->nkeep - 1);
+  dpgz_par* s = b->s;
+  Region* r = &s->regs[i];
+  r->n = 0;                                             /* the buffer is reused: only the window is kept */
+  if (reserve(r, WIN + s->region_min * 5 / 2 + (1u << 16))) { r->rc = D_MEM; return; }
+  if (i > 0) {
+    b->found[i] = find_block(r, s->cin, b->nbytes, b->bound[i], b->bound[i + 1]);
+    if (b->found[i] == NONE) { r->rc = D_OK; return; }
+  }
+  r->start = i == 0 ? s->pos : b->found[i];
+  r->start_kind = i == 0 ? s->kind : K_BLOCK;
+  r->stop_at = NONE;
+  r->stop_after = i + 1 < b->nreg ? b->bound[i + 1] : b->stop_last;
+  if (i == 0) {                                         /* the known window, right-aligned */
+    for (uint32_t j = 0; j < WIN; ++j) r->o[j] = j >= WIN - s->wl ? s->win[j - (WIN - s->wl)] : (uint16_t)(256 + j);
+    r->floor0 = WIN - s->wl;
+  } else {
+    for (uint32_t j = 0; j < WIN; ++j) r->o[j] = (uint16_t)(256 + j);
+    r->floor0 = 0;
+  }
+  decode_region(r, s->cin, b->nbytes, b->final && i == b->nreg - 1);
 }
 
 static void job_resolve(void* a, int k) {
@@ -921,22 +1049,28 @@ static int add_point(dpgz_par* s, uint64_t in_byte, uint32_t bits, uint64_t out,
 }
 
 /* One batch over the pending compressed bytes.  Returns a DPGZ status; *progress = 1 if it moved. */
+static uint64_t now_ns(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
 static int par_batch(dpgz_par* s, int final, int* progress) {
   *progress = 0;
+  uint64_t t0 = now_ns(), t1;
   if (s->kind == K_END) return DPGZ_OK;
   const uint64_t nbytes = s->clen;
   const uint64_t b0 = s->pos >> 3;
   /* at most two batches' worth of regions at a time (bounded memory whatever the caller feeds); the last
    * region then stops at the first block start past the batch and the rest waits for the next batch */
-  const uint64_t cap_bytes = 2ull * (uint64_t)s->threads * s->region_min;
+  const uint64_t cap_bytes = 2ull * (uint64_t)s->nregs * s->region_min;
   const int whole = nbytes - b0 <= cap_bytes;
   const uint64_t avail = whole ? nbytes - b0 : cap_bytes;
   if (!whole) final = 0;
   int nreg = (int)(avail / s->region_min);
-  if (nreg > s->threads) nreg = s->threads;
+  if (nreg > s->nregs) nreg = s->nregs;
   if (nreg < 1) nreg = 1;
-  uint64_t bound[257], found[257];
-  int idx[257];
+  uint64_t bound[2 * 256 + 1], found[2 * 256 + 1];
+  int idx[2 * 256 + 1];
   for (int i = 0; i <= nreg; ++i) bound[i] = (b0 + avail * (uint64_t)i / (uint64_t)nreg) * 8;
   bound[0] = s->pos;
   found[0] = s->pos;
@@ -948,46 +1082,32 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
   B.bound = bound;
   B.found = found;
   B.idx = idx;
-  if (nreg > 1) pfor(nreg, s->threads, job_find, &B);
+  B.nreg = nreg;
+  B.stop_last = whole ? NONE : (b0 + avail) * 8;
+  /* every region: find its start (a block start in its nominal range; region 0 starts at the known position),
+   * then decode to the first block start at or past the next region's nominal start -- which is that
+   * region's found start when it is a true one.  Regions outnumber the threads (dynamic balance). */
+  pool_for(&s->pool, nreg, job_find_decode, &B);
+  t1 = now_ns(); s->ns[1] += t1 - t0; t0 = t1;
+  /* keep regions in order while each starts exactly where the previous kept one stopped (a region without
+   * a block start in its range is skipped: the previous one decodes through it) */
   int nkeep = 0;
-  for (int i = 0; i < nreg; ++i)
-    if (i == 0 || found[i] != NONE) idx[nkeep++] = i;
-  for (int k = 0; k < nkeep; ++k) {
-    Region* r = &s->regs[idx[k]];
-    r->start = k == 0 ? s->pos : found[idx[k]];
-    r->start_kind = k == 0 ? s->kind : K_BLOCK;
-    r->stop_at = k + 1 < nkeep ? found[idx[k + 1]] : NONE;
-    r->stop_after = k + 1 < nkeep || whole ? NONE : (b0 + avail) * 8;
-    r->n = 0;                                           /* the buffer is reused: only the window is kept */
-    if (reserve(r, WIN + (4u << 20))) return DPGZ_ERR_MEMORY;
-    if (k == 0) {                                       /* the known window, right-aligned */
-      for (uint32_t j = 0; j < WIN; ++j) r->o[j] = j >= WIN - s->wl ? s->win[j - (WIN - s->wl)] : (uint16_t)(256 + j);
-      r->floor0 = WIN - s->wl;
-    } else {
-      for (uint32_t j = 0; j < WIN; ++j) r->o[j] = (uint16_t)(256 + j);
-      r->floor0 = 0;
-    }
-  }
-  B.nkeep = nkeep;
-  pfor(nkeep, s->threads, job_decode, &B);
-  /* keep region k while region k-1 stopped exactly at its start */
-  int keep = 0;
-  for (int k = 0; k < nkeep; ++k) {
-    Region* r = &s->regs[idx[k]];
-    if (k > 0) {
-      Region* q = &s->regs[idx[k - 1]];
-      if (q->overshoot || q->rc != D_OK || q->end != r->start) {
-        if (q->overshoot) s->rejected++;
+  for (int i = 0; i < nreg; ++i) {
+    Region* r = &s->regs[i];
+    if (i > 0) {
+      if (found[i] == NONE) continue;
+      Region* q = &s->regs[idx[nkeep - 1]];
+      if (q->rc != D_OK || q->end != r->start) {
+        if (q->rc == D_OK) s->rejected++;
         break;
       }
     }
     if (r->rc == D_MEM) return DPGZ_ERR_MEMORY;
     if (r->rc == D_BAD) return DPGZ_ERR_ZLIB;           /* its start is a true boundary: corrupt data */
     if (r->rc == D_TRUNC) return DPGZ_ERR_TRUNCATED;
-    ++keep;
+    idx[nkeep++] = i;
     if (r->rc == D_INPUT) break;
   }
-  nkeep = keep;
   Region* lastr = &s->regs[idx[nkeep - 1]];
   uint64_t total = 0;
   for (int k = 0; k < nkeep; ++k) {
@@ -1032,7 +1152,9 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
   B.seg_len = seg_len;
   B.seg_off = seg_off;
   B.nkeep = nkeep;
-  pfor(nkeep, s->threads, job_resolve, &B);
+  t1 = now_ns(); s->ns[2] += t1 - t0; t0 = t1;
+  pool_for(&s->pool, nkeep, job_resolve, &B);
+  t1 = now_ns(); s->ns[3] += t1 - t0; t0 = t1;
   /* in order: CRC / ISIZE per member, access points with their windows */
   int rc = DPGZ_OK;
   const uint8_t* hist = s->out;                         /* output offset of hist[0]: */
@@ -1094,6 +1216,7 @@ static int par_batch(dpgz_par* s, int final, int* progress) {
   s->pos = lastr->end - endb * 8;
   s->batches++;
   *progress = 1;
+  s->ns[4] += now_ns() - t0;
   return DPGZ_OK;
 }
 
@@ -1121,12 +1244,12 @@ int dpgz_par_feed(dpgz_par* s, const uint8_t* in, uint64_t in_len, int in_final)
   if (grow((void**)&s->cin, &s->ccap, s->clen + in_len + 8, 1)) return s->failed = DPGZ_ERR_MEMORY;
   if (in_len >= 4 * COPY_PART && s->threads > 1) {
     CopyJob c = {s->cin + s->clen, in, in_len};
-    pfor((int)((in_len + COPY_PART - 1) / COPY_PART), s->threads, job_copy, &c);
+    pool_for(&s->pool, (int)((in_len + COPY_PART - 1) / COPY_PART), job_copy, &c);
   } else if (in_len) {
     memcpy(s->cin + s->clen, in, in_len);
   }
   s->clen += in_len;
-  const uint64_t want = (uint64_t)s->threads * s->region_min;
+  const uint64_t want = (uint64_t)s->nregs * s->region_min;
   for (;;) {
     if (s->kind == K_END) break;
     const uint64_t avail = s->clen - (s->pos >> 3);
@@ -1147,7 +1270,7 @@ int dpgz_par_read(dpgz_par* s, uint8_t* out, uint64_t cap, uint64_t* n) {
   const uint64_t k = s->olen - s->ohead < cap ? s->olen - s->ohead : cap;
   if (k >= 4 * COPY_PART && s->threads > 1) {         /* into pinned pieces: one copy, on all threads */
     CopyJob c = {out, s->out + s->ohead, k};
-    pfor((int)((k + COPY_PART - 1) / COPY_PART), s->threads, job_copy, &c);
+    pool_for(&s->pool, (int)((k + COPY_PART - 1) / COPY_PART), job_copy, &c);
   } else if (k) {
     memcpy(out, s->out + s->ohead, k);
   }
@@ -1187,5 +1310,6 @@ int dpgz_par_state(dpgz_par* s, uint64_t* stats) {
   stats[6] = s->kind == K_END;                /* the stream ended */
   stats[7] = s->batches;
   stats[8] = s->rejected;                     /* region starts dropped (not a block boundary) */
+  for (int i = 0; i < 5; ++i) stats[9 + i] = s->ns[i];   /* ns in find, decode, windows, resolve, bookkeeping */
   return DPGZ_OK;
 }

@@ -291,10 +291,10 @@ class ParInflate:
         return int(n.value)
 
     def stats(self) -> dict:
-        st = (ctypes.c_uint64 * 9)()
+        st = (ctypes.c_uint64 * 14)()
         _check(load().dpgz_par_state(self._h, st), "gzip stream")
         keys = ("consumed", "produced", "members", "unread", "points", "window_bytes", "ended", "batches",
-                "rejected")
+                "rejected", "ns_find", "ns_decode", "ns_windows", "ns_resolve", "ns_inorder")
         return dict(zip(keys, (int(x) for x in st)))
 
     def take(self, out_limit: int):

@@ -72,10 +72,13 @@ int dpgz_inflate_members(const uint8_t* gz, const uint64_t* in_off, const uint64
 
 /* Parallel inflate of one gzip stream (dpgz_par.c): speculative deflate block starts per region, 16-bit
  * marker windows resolved in order, every member's CRC-32 / ISIZE checked.  Feed compressed bytes (the
- * engine inflates a batch once threads x 2 MiB are pending, or everything with in_final), read the inflated
+ * engine inflates a batch once 2 x threads x 1 MiB are pending, or everything with in_final), read the inflated
  * bytes in order, take the access points (those of dpgz_stream, with windows) up to an output offset.
- * dpgz_par_state fills stats[9]: compressed bytes consumed, inflated bytes produced, members, inflated
- * bytes not read, points pending, window bytes pending, stream ended, batches, region starts rejected. */
+ * dpgz_par_state fills stats[14]: compressed bytes consumed, inflated bytes produced, members, inflated
+ * bytes not read, points pending, window bytes pending, stream ended, batches, region starts rejected, then
+ * nanoseconds spent in the block search (0: now part of each region's decode task), the speculative decode,
+ * the window chain, marker resolution + CRC, and the
+ * in-order bookkeeping (CRC combine, access points) of all batches. */
 typedef struct dpgz_par dpgz_par;
 int dpgz_par_new(uint64_t span, int threads, dpgz_par** out);
 void dpgz_par_free(dpgz_par* s);

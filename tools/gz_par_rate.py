@@ -67,7 +67,8 @@ def main():
     for th in (int(x) for x in args.threads.split(",")):
         n, dt, st = run(blob, th, args.region_kib << 10, out)
         print(json.dumps({"threads": th, "GiB_per_s": round(n / dt / 2**30, 3), "ok": n == len(ref),
-                          "batches": st["batches"], "rejected": st["rejected"]}), flush=True)
+                          "batches": st["batches"], "rejected": st["rejected"], "wall_ms": round(dt * 1e3, 1),
+                          **{k: round(v / 1e6, 1) for k, v in st.items() if k.startswith("ns_")}}), flush=True)
 
 
 if __name__ == "__main__":
