@@ -16,6 +16,7 @@ from typing import Optional, Tuple
 
 import numpy as np
 
+from ..storage.errors import ClientError
 from ..version import __version__
 
 LINES_SUFFIX = ".lines"
@@ -148,8 +149,28 @@ class LineIndex:
 
 class SliceError(ValueError):
     """The reference's ``get()`` fails for this slice (kept as an error, not papered over).  A ``ValueError``:
-    what the reference raises there (the negative ``seek`` of csv.py:75; its VCF range expansion past the end
-    of the object fails inside the storage client instead)."""
+    what the reference raises for the negative ``seek`` of csv.py:75."""
+
+
+class SliceRangeError(ClientError, SliceError):
+    """The reference's ``get()`` ends in a ranged GET that starts past the end of the object, which S3 answers
+    with InvalidRange (HTTP 416), a botocore ``ClientError``: its CSV buffer expansion (csv.py:81-94) writes
+    each fetched range after the read position and never reads it, so it fetches further and further on until
+    that happens; its VCF expansion (vcf.py:117-136) does when no '\\n' follows before the end.  Raised as the
+    storage ``ClientError`` the reference's caller would see (and, as every ``SliceError``, a ``ValueError``);
+    pinned by the golden slices of rows longer than the padding (tests/golden/csv_slices.json ``wide_csv``)."""
+
+    def __init__(self, message: str):
+        self.detail = message
+        ClientError.__init__(self, "InvalidRange", "GetObject", message, 416)
+
+    def __reduce__(self):                 # slices travel to joblib workers
+        return (SliceRangeError, (self.detail,))
+
+
+def slice_error(e: SliceError) -> SliceError:
+    """A fresh exception of the same kind (a slice raises it at every get())."""
+    return SliceRangeError(e.detail) if isinstance(e, SliceRangeError) else SliceError(*e.args)
 
 
 def csv_body(lines: LineIndex, size: int, r0: int, r1: int, chunk_id: int, num_chunks: int,
@@ -178,8 +199,9 @@ def csv_body(lines: LineIndex, size: int, r0: int, r1: int, chunk_id: int, num_c
                          f"CSVSlice.get seeks to a negative position (ValueError)")
     n = lines.nxt(be - padding - 1)
     if n is None or n > be:
-        raise SliceError(f"slice {chunk_id}: no newline in the last {padding + 1} bytes of its range; the "
-                         f"reference's buffer expansion (csv.py:81-94) cannot find one either")
+        raise SliceRangeError(f"slice {chunk_id}: no newline in the last {padding + 1} bytes of its range; the "
+                              f"reference's buffer expansion (csv.py:81-94) fetches ranges until one starts past "
+                              f"the end of the object")
     return start, n
 
 
@@ -200,6 +222,6 @@ def vcf_body(lines: LineIndex, size: int, r0: int, r1: int, chunk_id: int, num_c
         return start, be
     n = lines.nxt(be - 1)
     if n is None:
-        raise SliceError(f"slice {chunk_id}: no newline after byte {be - 1}; the reference's range expansion "
-                         f"requests bytes past the end of the object")
+        raise SliceRangeError(f"slice {chunk_id}: no newline after byte {be - 1}; the reference's range "
+                              f"expansion requests bytes past the end of the object")
     return start, n

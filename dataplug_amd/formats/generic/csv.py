@@ -17,7 +17,7 @@ from typing import TYPE_CHECKING, List, Optional
 from ...entities import CloudDataFormat, CloudObjectSlice, PartitioningStrategy
 from ...preprocessing.metadata import PreprocessingMetadata
 from ...scan import objects as scan_objects
-from .._lines import LineIndex, SliceError, csv_body, store_line_index
+from .._lines import LineIndex, SliceError, csv_body, slice_error, store_line_index
 
 if TYPE_CHECKING:
     from ...cloudobject import CloudObject
@@ -51,7 +51,7 @@ class CSV:
 
 class CSVSlice(CloudObjectSlice):
     def __init__(self, chunk_id, num_chunks, padding, *args, body: Optional[tuple] = None,
-                 error: Optional[str] = None, **kwargs):
+                 error: Optional[SliceError] = None, **kwargs):
         self.chunk_id = chunk_id
         self.num_chunks = num_chunks
         self.padding = padding
@@ -61,7 +61,7 @@ class CSVSlice(CloudObjectSlice):
 
     def get_bytes(self) -> bytes:
         if self.error is not None:
-            raise SliceError(self.error)
+            raise slice_error(self.error)
         co = self.cloud_object
         start, end = self.body
         data = b""
@@ -92,7 +92,7 @@ def _slices(cloud_object, chunk_size: int, num_chunks: int, padding: int) -> Lis
         try:
             body, err = csv_body(lines, size, r0, r1, i, num_chunks, padding), None
         except SliceError as e:
-            body, err = None, str(e)
+            body, err = None, e
         out.append(CSVSlice(range_0=r0, range_1=r1, chunk_id=i, num_chunks=num_chunks, padding=padding,
                             body=body, error=err))
     return out

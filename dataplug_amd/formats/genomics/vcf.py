@@ -16,7 +16,7 @@ from typing import TYPE_CHECKING, Dict, List, Optional, Union
 from ...entities import CloudDataFormat, CloudObjectSlice, PartitioningStrategy
 from ...preprocessing.metadata import PreprocessingMetadata
 from ...scan import objects as scan_objects
-from .._lines import LineIndex, SliceError, store_line_index, vcf_body
+from .._lines import LineIndex, SliceError, slice_error, store_line_index, vcf_body
 
 if TYPE_CHECKING:
     from ...cloudobject import CloudObject
@@ -84,7 +84,7 @@ class VCF:
 
 class VCFSlice(CloudObjectSlice):
     def __init__(self, chunk_id, num_chunks, padding, *args, body: Optional[tuple] = None,
-                 error: Optional[str] = None, **kwargs):
+                 error: Optional[SliceError] = None, **kwargs):
         self.chunk_id = chunk_id
         self.num_chunks = num_chunks
         self.padding = padding
@@ -94,7 +94,7 @@ class VCFSlice(CloudObjectSlice):
 
     def get(self) -> str:
         if self.error is not None:
-            raise SliceError(self.error)
+            raise slice_error(self.error)
         co = self.cloud_object
         start, end = self.body
         data = b""
@@ -121,7 +121,7 @@ def partition_num_chunks(cloud_object: "CloudObject", num_chunks: int, padding: 
         try:
             body, err = vcf_body(lines, size, r0, r1, i, num_chunks), None
         except SliceError as e:
-            body, err = None, str(e)
+            body, err = None, e
         out.append(VCFSlice(range_0=r0, range_1=r1, chunk_id=i, num_chunks=num_chunks, padding=padding,
                             body=body, error=err))
     return out

@@ -102,6 +102,25 @@ def csv(size: int, seed: int = 0) -> np.ndarray:
     return out
 
 
+def csv_wide(size: int, seed: int = 0, max_note: int = 1500) -> np.ndarray:
+    """``csv`` rows with an 11th column ``Note`` of 0..max_note ASCII characters: rows longer than the
+    reference's default slice padding (256 B), which reach CSVSlice.get's buffer expansion (csv.py:81-94)."""
+    base = csv(size, seed).tobytes().split(b"\n")[1:-1]
+    rng = np.random.default_rng(seed + 1)
+    rows = [CSV_HEADER[:-1] + b",Note\n"]
+    total = len(rows[0])
+    i = 0
+    while total < size:
+        r = base[i % len(base)] + b"," + b"n" * int(rng.integers(0, max_note + 1)) + b"\n"
+        rows.append(r)
+        total += len(r)
+        i += 1
+    out = np.frombuffer(b"".join(rows), np.uint8)[:size].copy()
+    if size:
+        out[-1] = 10
+    return out
+
+
 VCF_HEADER = (b"##fileformat=VCFv4.2\n"
               b"##source=dataplug_amd.synth\n"
               b"##INFO=<ID=NS,Number=1,Type=Integer,Description=\"Samples With Data\">\n"
@@ -132,6 +151,31 @@ def vcf(size: int, seed: int = 0) -> np.ndarray:
                 gts[v[j, 5] % 5], int(v[j, 6] % 60))
             rows.append(r)
             total += len(r)
+    out = np.frombuffer(b"".join(rows), np.uint8)[:size].copy()
+    if size:
+        out[-1] = 10
+    return out
+
+
+def vcf_wide(size: int, seed: int = 0, max_info: int = 1500) -> np.ndarray:
+    """``vcf`` rows whose INFO field carries an extra ``NOTE=`` of 0..max_info characters: rows longer than
+    the slice padding, which reach VCFSlice.get's range expansion (vcf.py:117-136)."""
+    base = vcf(size, seed).tobytes()
+    head_end = base.index(b"\n#CHROM") + 1
+    head_end = base.index(b"\n", head_end) + 1
+    body = base[head_end:].split(b"\n")[:-1]
+    rng = np.random.default_rng(seed + 1)
+    rows = [base[:head_end]]
+    total = len(rows[0])
+    i = 0
+    while total < size:
+        f = body[i % len(body)].split(b"\t")
+        if len(f) >= 8:
+            f[7] = f[7] + b";NOTE=" + b"v" * int(rng.integers(0, max_info + 1))
+        r = b"\t".join(f) + b"\n"
+        rows.append(r)
+        total += len(r)
+        i += 1
     out = np.frombuffer(b"".join(rows), np.uint8)[:size].copy()
     if size:
         out[-1] = 10

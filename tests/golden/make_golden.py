@@ -14,8 +14,10 @@ is INCLUSIVE like S3.  ``co.preprocess(chunk_size=...)`` then runs the reference
 Outputs (data only: inputs + the reference's outputs):
   fasta_cases.npz      fuzz + sample + synthetic FASTA inputs, chunk sizes, expected uint32 indexes
   fasta_slices.json    partition_chunks_strategy slices (+ get() bytes for the sample object)
-  csv_slices.json      CSV attrs + partition_num_chunks / partition_chunk_size get() outputs
-  vcf_slices.json      VCF attrs + header meta + partition_num_chunks get() outputs
+  csv_slices.json      CSV attrs + partition_num_chunks / partition_chunk_size get() outputs (cities.csv,
+                       synthetic, and rows longer than the 256 B padding: the buffer-expansion path)
+  vcf_slices.json      VCF attrs + header meta + partition_num_chunks get() outputs (sample.vcf, synthetic,
+                       and rows longer than the padding: the range-expansion path)
   fastq_batches.json   partition_reads_batches line pairs (gztool absent: parity unpinned beyond these)
 """
 from __future__ import annotations
@@ -77,7 +79,8 @@ def _install_stubs(store):
 
 
 class FakeS3:
-    """In-memory S3 with inclusive ``Range: bytes=a-b`` (S3 semantics, unlike filesystem.py:64-69)."""
+    """In-memory S3 with inclusive ``Range: bytes=a-b`` (S3 semantics, unlike filesystem.py:64-69); a range
+    starting at or past the object's end fails with InvalidRange (HTTP 416), as on S3."""
 
     def __init__(self, store):
         self.store = store
@@ -109,6 +112,8 @@ class FakeS3:
         code = 200
         if Range is not None:
             a, b = Range[len("bytes="):].split("-")
+            if int(a) >= len(d):                 # S3: a range starting at or past the end -> 416
+                raise ClientError("InvalidRange")
             d = d[int(a):int(b) + 1]
             code = 206
         return {"Body": io.BytesIO(d), "ResponseMetadata": {"HTTPStatusCode": code}}
@@ -247,7 +252,8 @@ def _get(s):
 def csv_slices():
     cities = open(os.path.join(REF, "examples/sample_data/cities.csv"), "rb").read()
     out = {"objects": []}
-    for name, data in [("cities", cities), ("synth_csv", bytes(synth.csv(1 << 16, 5)))]:
+    for name, data in [("cities", cities), ("synth_csv", bytes(synth.csv(1 << 16, 5))),
+                       ("wide_csv", bytes(synth.csv_wide(1 << 16, 5)))]:
         co = make_co(ref_csv.CSV, "dataplug", name, data)
         co.preprocess(force=True)
         rec = {"object": name, "sha256": synth.sha256(np.frombuffer(data, np.uint8)),
@@ -266,7 +272,8 @@ def csv_slices():
 def vcf_slices():
     sample = open(os.path.join(REF, "examples/sample_data/sample.vcf"), "rb").read()
     out = {"objects": []}
-    for name, data in [("sample", sample), ("synth_vcf", bytes(synth.vcf(1 << 16, 6)))]:
+    for name, data in [("sample", sample), ("synth_vcf", bytes(synth.vcf(1 << 16, 6))),
+                       ("wide_vcf", bytes(synth.vcf_wide(1 << 16, 6)))]:
         co = make_co(ref_vcf.VCF, "dataplug", name, data)
         co.preprocess(force=True)
         rec = {"object": name, "sha256": synth.sha256(np.frombuffer(data, np.uint8)),

@@ -181,6 +181,13 @@ def test_fasta_quirk_every_chunk_to_eof():
 
 
 # ------------------------------------------------------------------------------------------------ CSV / VCF
+def _ref_error(name):
+    """The exception class the golden recorded for the reference's get(): a builtin, or the storage
+    ClientError (a ranged GET past the end of the object, InvalidRange on S3)."""
+    from dataplug_amd.storage.errors import ClientError
+    return {"ClientError": ClientError}.get(name) or getattr(builtins, name)
+
+
 @pytest.mark.parametrize("devices", ["0", "0,0,0"])
 def test_csv_line_index_and_partitions(monkeypatch, devices):
     from dataplug_amd.formats.generic import csv as fcsv
@@ -188,7 +195,8 @@ def test_csv_line_index_and_partitions(monkeypatch, devices):
     monkeypatch.setenv("DATAPLUG_AMD_DEVICES", devices)
     g = json.load(open(os.path.join(GOLDEN, "csv_slices.json")))["objects"]
     for rec in g:
-        data = bytes(synth.csv(1 << 16, 5)) if rec["object"] == "synth_csv" else rec["num_chunks"]["1"][0][2].encode()
+        data = {"synth_csv": lambda: bytes(synth.csv(1 << 16, 5)), "wide_csv": lambda: bytes(synth.csv_wide(1 << 16, 5))}.get(
+            rec["object"], lambda: rec["num_chunks"]["1"][0][2].encode())()
         co = _co(fcsv.CSV, data, rec["object"] + devices, _mem(f"gpu_csv_{rec['object']}_{len(devices)}"))
         co.preprocess()
         assert co.attributes.columns == rec["columns"]
@@ -197,7 +205,7 @@ def test_csv_line_index_and_partitions(monkeypatch, devices):
         for n, expected in rec["num_chunks"].items():
             for s, e in zip(co.partition(fcsv.partition_num_chunks, num_chunks=int(n)), expected):
                 if isinstance(e[2], dict):
-                    with pytest.raises(getattr(builtins, e[2]["error"])) as ei:   # the reference's class
+                    with pytest.raises(_ref_error(e[2]["error"])) as ei:   # the reference's class
                         s.get()
                     assert isinstance(ei.value, SliceError)
                 else:
@@ -218,13 +226,15 @@ def test_csv_large_multi_part(monkeypatch):
         assert s.get() == cpu_ref.csv_slice_get(obj, co.attributes.columns, s.range_0, s.range_1, s.chunk_id, 25)
 
 
-def test_vcf_line_index_and_partitions(monkeypatch):
+@pytest.mark.parametrize("name", ["synth_vcf", "wide_vcf"])
+def test_vcf_line_index_and_partitions(monkeypatch, name):
+    """Golden VCF slices, incl. rows longer than the padding (the reference's range-expansion path)."""
     from dataplug_amd.formats.genomics import vcf as fvcf
     monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0")
     g = json.load(open(os.path.join(GOLDEN, "vcf_slices.json")))["objects"]
-    rec = [r for r in g if r["object"] == "synth_vcf"][0]
-    data = bytes(synth.vcf(1 << 16, 6))
-    co = _co(fvcf.VCF, data, "s.vcf", _mem("gpu_vcf"))
+    rec = [r for r in g if r["object"] == name][0]
+    data = bytes(synth.vcf(1 << 16, 6) if name == "synth_vcf" else synth.vcf_wide(1 << 16, 6))
+    co = _co(fvcf.VCF, data, name + ".vcf", _mem("gpu_" + name))
     co.preprocess()
     assert co.attributes.body_offset == rec["body_offset"] and co.attributes.columns == rec["columns"]
     meta = co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read().decode()
