@@ -1,0 +1,168 @@
+"""Time-bounded randomized parity campaign on the GPU: the HIP scan kernels (through the C ABI) against the C
+oracle (oracle/dpref.c) on random inputs, chunk plans, device misalignments and output forms.
+
+    python tools/fuzz_gpu.py [--seconds 240] [--seed 1] [--out gpurun_out/fuzz.json]
+
+FASTA: token soups and structured records (header lines 1 B - 300 KB, so headers span wave ranges, units and
+chunks; '\\r'; '>' inside sequence lines; runs of '>' or '\\n'), object sizes log-uniform in [1 B, 48 MiB],
+chunk plans of the reference (preprocess.py:38 floor plan with the tail dropped, including the
+chunk_size == num_chunks - 1 quirk of handler.py:37 that sends every chunk to EOF), uint32 or uint64 output.
+Every pair and every per-chunk count must equal the oracle's.  DELIM: random delimiter byte, [begin, end),
+every_k 1-5, emit_add 0/1, uint64 or uint32 output.  Exits non-zero on the first mismatch and keeps the case
+in gpurun_out/fuzz_fail.npz.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dataplug_amd.scan import ScanContext  # noqa: E402
+from oracle import cpu_ref, dpref  # noqa: E402
+
+
+def soup(rng, size):
+    p_gt, p_nl, p_cr = rng.uniform(0, 0.3), rng.uniform(0, 0.3), rng.uniform(0, 0.02)
+    p = np.array([p_gt, p_nl, p_cr, 1.0 - p_gt - p_nl - p_cr])
+    p = np.clip(p, 0, None)
+    p /= p.sum()
+    cls = rng.choice(4, size=size, p=p)
+    out = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size)].copy()
+    out[cls == 0] = 62
+    out[cls == 1] = 10
+    out[cls == 2] = 13
+    return out
+
+
+def records(rng, size):
+    parts, total = [], 0
+    hmax = int(rng.choice([40, 2000, 40000, 300000]))
+    wmax = int(rng.choice([1, 60, 5000, 100000]))
+    while total < size:
+        h = b">" + b"h" * int(rng.integers(0, hmax)) + (b"\r" if rng.random() < 0.1 else b"") + b"\n"
+        body_len = int(rng.integers(0, 4 * wmax + 1))
+        w = max(1, int(rng.integers(1, wmax + 1)))
+        body = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, body_len)].copy()
+        if body_len and rng.random() < 0.2:                     # '>' inside sequence lines
+            body[rng.integers(0, body_len, max(1, body_len // 500))] = 62
+        lines = [body[i:i + w].tobytes() + b"\n" for i in range(0, body_len, w)]
+        rec = h + b"".join(lines)
+        parts.append(rec)
+        total += len(rec)
+    return np.frombuffer(b"".join(parts)[:size], np.uint8).copy()
+
+
+def runs(rng, size):
+    out = soup(rng, size)
+    for _ in range(int(rng.integers(1, 6))):
+        a = int(rng.integers(0, max(1, size)))
+        b = min(size, a + int(rng.integers(1, 200000)))
+        out[a:b] = rng.choice([62, 10])
+    return out
+
+
+def make_object(rng):
+    size = int(math.exp(rng.uniform(0, math.log(48 << 20))))
+    kind = rng.choice(["soup", "records", "runs"])
+    a = {"soup": soup, "records": records, "runs": runs}[kind](rng, size)
+    return a, str(kind)
+
+
+def chunk_size(rng, size):
+    if size < 2:
+        return max(1, size)
+    r = rng.random()
+    if r < 0.1 and size <= (64 << 10):                           # the cs == num_chunks - 1 quirk (every chunk
+        # reads to EOF: ~num_chunks x the headers, so small objects only)
+        cs = int(math.isqrt(size))
+        while cs > 1 and size // cs != cs + 1:
+            cs -= 1
+        if cs >= 1 and size // cs == cs + 1:
+            return cs
+    if r < 0.6:
+        return max(1, math.ceil(size / int(rng.integers(1, 2000))))
+    return int(rng.integers(1, size + 1))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--seconds", type=float, default=240)
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--out", default="gpurun_out/fuzz.json")
+    args = ap.parse_args()
+    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    rng = np.random.default_rng(args.seed)
+    ctx = ScanContext(0)
+    stats = {"fasta_cases": 0, "fasta_pairs": 0, "quirk_cases": 0, "delim_cases": 0, "delim_offsets": 0,
+             "bytes": 0, "kinds": {}}
+    t0 = last = time.time()
+    while time.time() - t0 < args.seconds:
+        a, kind = make_object(rng)
+        size = len(a)
+        stats["bytes"] += size
+        stats["kinds"][kind] = stats["kinds"].get(kind, 0) + 1
+        off = int(rng.integers(0, 16))
+        buf = ctx.workspace("fz_in", size + 64)
+        if size:
+            ctx.h2d(buf.ptr + off, a)
+        # FASTA
+        cs = chunk_size(rng, size)
+        plan = cpu_ref.chunk_plan(size, cs) if size else []
+        quirk = bool(plan) and cs == len(plan) - 1
+        u64 = bool(rng.random() < 0.3)
+        exp = dpref.fasta_pairs(a, plan) if plan else np.zeros((0, 2), np.uint64)
+        if plan:
+            pairs, pending, cend = ctx.fasta_index(buf.ptr + off, size, 0, size, plan, u64=u64)
+            ok = (pending == -1).all() and np.array_equal(pairs.astype(np.uint64).reshape(-1, 2), exp)
+            k = 0
+            for i, (c0, c1) in enumerate(plan):
+                k += len(dpref.fasta_pairs(a, [(c0, c1)]))
+                ok = ok and int(cend[i]) == k
+            if not ok:
+                np.savez_compressed("gpurun_out/fuzz_fail.npz", data=a, plan=np.asarray(plan, np.uint64),
+                                    offset=off, u64=u64)
+                print(json.dumps({"FAIL": "fasta", "size": size, "kind": kind, "chunk_size": cs, "offset": off,
+                                  "u64": u64, "got": int(len(pairs)), "expected": int(len(exp))}), flush=True)
+                sys.exit(1)
+            stats["fasta_cases"] += 1
+            stats["fasta_pairs"] += int(len(exp))
+            stats["quirk_cases"] += int(quirk)
+        # DELIM
+        if size:
+            b0 = int(rng.integers(0, size + 1))
+            b1 = int(rng.integers(b0, size + 1))
+            delim = int(rng.choice([10, 62, 13, 65, int(rng.integers(0, 256))]))
+            k = int(rng.integers(1, 6))
+            add = int(rng.integers(0, 2))
+            du64 = bool(rng.random() < 0.7)
+            got, nd = ctx.delim_index(buf.ptr + off, size, 0, b0, b1, delim, k, add, u64=du64)
+            want, wnd = dpref.delim(a, b0, b1, delim, k, add)
+            if nd != wnd or not np.array_equal(got.astype(np.uint64), want):
+                np.savez_compressed("gpurun_out/fuzz_fail.npz", data=a, begin=b0, end=b1, delim=delim, k=k,
+                                    add=add, offset=off, u64=du64)
+                print(json.dumps({"FAIL": "delim", "size": size, "begin": b0, "end": b1, "delim": delim, "k": k,
+                                  "add": add, "offset": off}), flush=True)
+                sys.exit(1)
+            stats["delim_cases"] += 1
+            stats["delim_offsets"] += int(len(want))
+        if time.time() - last > 20:
+            last = time.time()
+            print(json.dumps({"t": round(last - t0), **{k: v for k, v in stats.items() if k != "kinds"}}), flush=True)
+    stats["seconds"] = round(time.time() - t0, 1)
+    stats["seed"] = args.seed
+    stats["ok"] = True
+    ctx.close()
+    with open(args.out, "w") as f:
+        json.dump(stats, f)
+    print(json.dumps(stats), flush=True)
+
+
+if __name__ == "__main__":
+    main()
