@@ -1,7 +1,9 @@
 """Time-bounded randomized parity campaign on the GPU: the HIP scan kernels (through the C ABI) against the C
 oracle (oracle/dpref.c) on random inputs, chunk plans, device misalignments and output forms.
 
-    python tools/fuzz_gpu.py [--seconds 240] [--seed 1] [--out gpurun_out/fuzz.json]
+    python tools/fuzz_gpu.py [--seconds 240] [--seed 1] [--mode kernel|object] [--out gpurun_out/fuzz.json]
+
+``--mode object`` runs co.preprocess() end to end instead (see object_mode).
 
 FASTA: token soups and structured records (header lines 1 B - 300 KB, so headers span wave ranges, units and
 chunks; '\\r'; '>' inside sequence lines; runs of '>' or '\\n'), object sizes log-uniform in [1 B, 48 MiB],
@@ -91,14 +93,79 @@ def chunk_size(rng, size):
     return int(rng.integers(1, size + 1))
 
 
+def object_mode(args, rng):
+    """co.preprocess() end to end through storage: random chunk plans split into 1-6 groups on this GPU
+    (dataplug_devices=[0]*g: the multi-GPU split with its 64 KiB halos, header ends past a group's halo
+    resolved from later bytes), sometimes a launch byte budget far below a group (passes of whole chunks),
+    sometimes the per-chunk joblib route; the stored index against the oracle."""
+    from dataplug_amd.cloudobject import CloudObject
+    from dataplug_amd.formats.genomics.fasta import FASTA
+    from dataplug_amd.storage import MemoryStore
+    stats = {"object_cases": 0, "pairs": 0, "bytes": 0, "groups": {}, "budget_cases": 0, "joblib_cases": 0}
+    t0 = last = time.time()
+    i = 0
+    while time.time() - t0 < args.seconds:
+        size = int(math.exp(rng.uniform(math.log(64), math.log(12 << 20))))
+        a = records(rng, size) if rng.random() < 0.7 else runs(rng, size)
+        cs = chunk_size(rng, size)
+        plan = cpu_ref.chunk_plan(size, cs)
+        groups = int(rng.integers(1, 7))
+        pc = {"dataplug_devices": [0] * groups}
+        if rng.random() < 0.15:
+            pc.update({"backend": "threading", "n_jobs": int(rng.integers(1, 5))})
+            stats["joblib_cases"] += 1
+        budget = None
+        if rng.random() < 0.25:
+            budget = int(rng.integers(64 << 10, 4 << 20))
+            os.environ["DATAPLUG_AMD_MAX_LAUNCH_BYTES"] = str(budget)
+            stats["budget_cases"] += 1
+        name = f"fz{i}"
+        MemoryStore._named.pop(name, None)
+        cfg = {"endpoint_url": f"memory://{name}"}
+        co = CloudObject.from_s3(FASTA, f"s3://data/k{i}", fetch=False, s3_config=cfg)
+        co.storage.create_bucket(Bucket="data")
+        co.storage.put_object(Body=a.tobytes(), Bucket="data", Key=f"k{i}")
+        co = CloudObject.from_s3(FASTA, f"s3://data/k{i}", s3_config=cfg)
+        co.preprocess(chunk_size=cs, parallel_config=pc)
+        os.environ.pop("DATAPLUG_AMD_MAX_LAUNCH_BYTES", None)
+        got = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read(),
+                            np.uint32)
+        exp = dpref.fasta_pairs(a, plan).reshape(-1).astype(np.uint32)
+        MemoryStore._named.pop(name, None)
+        if not np.array_equal(got, exp):
+            np.savez_compressed("gpurun_out/fuzz_fail.npz", data=a, chunk_size=cs, groups=groups,
+                                budget=-1 if budget is None else budget)
+            print(json.dumps({"FAIL": "object", "size": size, "chunk_size": cs, "groups": groups, "budget": budget,
+                              "parallel_config": {k: v for k, v in pc.items() if k != "dataplug_devices"},
+                              "got": int(len(got)), "expected": int(len(exp))}), flush=True)
+            sys.exit(1)
+        stats["object_cases"] += 1
+        stats["pairs"] += len(exp) // 2
+        stats["bytes"] += size
+        stats["groups"][groups] = stats["groups"].get(groups, 0) + 1
+        i += 1
+        if time.time() - last > 20:
+            last = time.time()
+            print(json.dumps({"t": round(last - t0), **{k: v for k, v in stats.items() if k != "groups"}}), flush=True)
+    return stats
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=240)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--mode", choices=["kernel", "object"], default="kernel")
     ap.add_argument("--out", default="gpurun_out/fuzz.json")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     rng = np.random.default_rng(args.seed)
+    if args.mode == "object":
+        stats = object_mode(args, rng)
+        stats.update({"seconds": args.seconds, "seed": args.seed, "ok": True, "mode": "object"})
+        with open(args.out, "w") as f:
+            json.dump(stats, f)
+        print(json.dumps(stats), flush=True)
+        return
     ctx = ScanContext(0)
     stats = {"fasta_cases": 0, "fasta_pairs": 0, "quirk_cases": 0, "delim_cases": 0, "delim_offsets": 0,
              "bytes": 0, "kinds": {}}
