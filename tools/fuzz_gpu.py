@@ -30,6 +30,11 @@ from dataplug_amd.scan import ScanContext  # noqa: E402
 from oracle import cpu_ref, dpref  # noqa: E402
 
 
+def _save_fail(**case):
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savez_compressed("gpurun_out/fuzz_fail.npz", **case)
+
+
 def soup(rng, size):
     p_gt, p_nl, p_cr = rng.uniform(0, 0.3), rng.uniform(0, 0.3), rng.uniform(0, 0.02)
     p = np.array([p_gt, p_nl, p_cr, 1.0 - p_gt - p_nl - p_cr])
@@ -70,8 +75,8 @@ def runs(rng, size):
     return out
 
 
-def make_object(rng):
-    size = int(math.exp(rng.uniform(0, math.log(48 << 20))))
+def make_object(rng, max_size=48 << 20):
+    size = int(math.exp(rng.uniform(0, math.log(max_size))))
     kind = rng.choice(["soup", "records", "runs"])
     a = {"soup": soup, "records": records, "runs": runs}[kind](rng, size)
     return a, str(kind)
@@ -105,7 +110,7 @@ def object_mode(args, rng):
     t0 = last = time.time()
     i = 0
     while time.time() - t0 < args.seconds:
-        size = int(math.exp(rng.uniform(math.log(64), math.log(12 << 20))))
+        size = int(math.exp(rng.uniform(math.log(64), math.log(getattr(args, "max_size", 12 << 20)))))
         a = records(rng, size) if rng.random() < 0.7 else runs(rng, size)
         cs = chunk_size(rng, size)
         plan = cpu_ref.chunk_plan(size, cs)
@@ -126,19 +131,21 @@ def object_mode(args, rng):
         co.storage.create_bucket(Bucket="data")
         co.storage.put_object(Body=a.tobytes(), Bucket="data", Key=f"k{i}")
         co = CloudObject.from_s3(FASTA, f"s3://data/k{i}", s3_config=cfg)
-        co.preprocess(chunk_size=cs, parallel_config=pc)
-        os.environ.pop("DATAPLUG_AMD_MAX_LAUNCH_BYTES", None)
+        try:
+            co.preprocess(chunk_size=cs, parallel_config=pc)
+        finally:
+            os.environ.pop("DATAPLUG_AMD_MAX_LAUNCH_BYTES", None)
         got = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read(),
                             np.uint32)
         exp = dpref.fasta_pairs(a, plan).reshape(-1).astype(np.uint32)
         MemoryStore._named.pop(name, None)
         if not np.array_equal(got, exp):
-            np.savez_compressed("gpurun_out/fuzz_fail.npz", data=a, chunk_size=cs, groups=groups,
+            _save_fail(data=a, chunk_size=cs, groups=groups,
                                 budget=-1 if budget is None else budget)
             print(json.dumps({"FAIL": "object", "size": size, "chunk_size": cs, "groups": groups, "budget": budget,
                               "parallel_config": {k: v for k, v in pc.items() if k != "dataplug_devices"},
                               "got": int(len(got)), "expected": int(len(exp))}), flush=True)
-            sys.exit(1)
+            raise SystemExit(1)
         stats["object_cases"] += 1
         stats["pairs"] += len(exp) // 2
         stats["bytes"] += size
@@ -166,12 +173,23 @@ def main():
             json.dump(stats, f)
         print(json.dumps(stats), flush=True)
         return
+    stats = kernel_mode(args, rng)
+    stats["seconds"] = round(stats.pop("_t"), 1)
+    stats["seed"] = args.seed
+    stats["ok"] = True
+    with open(args.out, "w") as f:
+        json.dump(stats, f)
+    print(json.dumps(stats), flush=True)
+
+
+def kernel_mode(args, rng):
+    """The kernels through the C ABI on random objects, chunk plans, misalignments and output forms."""
     ctx = ScanContext(0)
     stats = {"fasta_cases": 0, "fasta_pairs": 0, "quirk_cases": 0, "delim_cases": 0, "delim_offsets": 0,
              "bytes": 0, "kinds": {}}
     t0 = last = time.time()
     while time.time() - t0 < args.seconds:
-        a, kind = make_object(rng)
+        a, kind = make_object(rng, getattr(args, "max_size", 48 << 20))
         size = len(a)
         stats["bytes"] += size
         stats["kinds"][kind] = stats["kinds"].get(kind, 0) + 1
@@ -193,11 +211,11 @@ def main():
                 k += len(dpref.fasta_pairs(a, [(c0, c1)]))
                 ok = ok and int(cend[i]) == k
             if not ok:
-                np.savez_compressed("gpurun_out/fuzz_fail.npz", data=a, plan=np.asarray(plan, np.uint64),
+                _save_fail(data=a, plan=np.asarray(plan, np.uint64),
                                     offset=off, u64=u64)
                 print(json.dumps({"FAIL": "fasta", "size": size, "kind": kind, "chunk_size": cs, "offset": off,
                                   "u64": u64, "got": int(len(pairs)), "expected": int(len(exp))}), flush=True)
-                sys.exit(1)
+                raise SystemExit(1)
             stats["fasta_cases"] += 1
             stats["fasta_pairs"] += int(len(exp))
             stats["quirk_cases"] += int(quirk)
@@ -212,23 +230,19 @@ def main():
             got, nd = ctx.delim_index(buf.ptr + off, size, 0, b0, b1, delim, k, add, u64=du64)
             want, wnd = dpref.delim(a, b0, b1, delim, k, add)
             if nd != wnd or not np.array_equal(got.astype(np.uint64), want):
-                np.savez_compressed("gpurun_out/fuzz_fail.npz", data=a, begin=b0, end=b1, delim=delim, k=k,
+                _save_fail(data=a, begin=b0, end=b1, delim=delim, k=k,
                                     add=add, offset=off, u64=du64)
                 print(json.dumps({"FAIL": "delim", "size": size, "begin": b0, "end": b1, "delim": delim, "k": k,
                                   "add": add, "offset": off}), flush=True)
-                sys.exit(1)
+                raise SystemExit(1)
             stats["delim_cases"] += 1
             stats["delim_offsets"] += int(len(want))
         if time.time() - last > 20:
             last = time.time()
             print(json.dumps({"t": round(last - t0), **{k: v for k, v in stats.items() if k != "kinds"}}), flush=True)
-    stats["seconds"] = round(time.time() - t0, 1)
-    stats["seed"] = args.seed
-    stats["ok"] = True
+    stats["_t"] = time.time() - t0
     ctx.close()
-    with open(args.out, "w") as f:
-        json.dump(stats, f)
-    print(json.dumps(stats), flush=True)
+    return stats
 
 
 if __name__ == "__main__":
