@@ -120,6 +120,7 @@ def object_mode(args, rng):
             pc.update({"backend": "threading", "n_jobs": int(rng.integers(1, 5))})
             stats["joblib_cases"] += 1
         budget = None
+        prev_budget = os.environ.get("DATAPLUG_AMD_MAX_LAUNCH_BYTES")
         if rng.random() < 0.25:
             budget = int(rng.integers(64 << 10, 4 << 20))
             os.environ["DATAPLUG_AMD_MAX_LAUNCH_BYTES"] = str(budget)
@@ -133,8 +134,11 @@ def object_mode(args, rng):
         co = CloudObject.from_s3(FASTA, f"s3://data/k{i}", s3_config=cfg)
         try:
             co.preprocess(chunk_size=cs, parallel_config=pc)
-        finally:
-            os.environ.pop("DATAPLUG_AMD_MAX_LAUNCH_BYTES", None)
+        finally:                                      # the caller's own setting (if any) back
+            if prev_budget is None:
+                os.environ.pop("DATAPLUG_AMD_MAX_LAUNCH_BYTES", None)
+            else:
+                os.environ["DATAPLUG_AMD_MAX_LAUNCH_BYTES"] = prev_budget
         got = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read(),
                             np.uint32)
         exp = dpref.fasta_pairs(a, plan).reshape(-1).astype(np.uint32)
