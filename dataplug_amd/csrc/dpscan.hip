@@ -1532,6 +1532,299 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   }
 }
 
+// ------------------------------------------------------------------------------------------ FASTA, two kernels
+// The FASTA index as a map over 16 KiB ranges followed by a small placement kernel:
+//   * fasta_map_kernel: every wave streams its own ranges (r = global wave, + all waves, ...) with no
+//     inter-wave or inter-workgroup dependency — the geometry of the plain stream kernel.  Per range it
+//     writes a 16-byte summary (the range's header count and line state as a function of the incoming
+//     state, as in phase A) and its events (16-bit positions, under "no header pending at the range
+//     start") to the range's slot of a spill area.
+//   * fasta_place_kernel: one workgroup per block of 1024 range summaries (claimed in order from a
+//     ticket) scans them, resolves the block's prefix by a decoupled look-back over block descriptors,
+//     and copies every range's events to their final index with the pending-header fix-up of phase B.
+//     Ranges with more than kSpillCap events ("dense") are rescanned from the input (dense_b).
+// The one-pass kernel pays a fixed ~60 us per launch at its start and tail (its look-back chain couples
+// every unit to the grid's slowest); here the map streams like the calibration kernel and the placement
+// only touches the summaries (16 B per 16 KiB) and the events.
+constexpr uint32_t kSpillCap = 512;                 // events kept per range (1 KiB slot); more = dense
+constexpr uint32_t kPlaceBlock = 1024;              // range summaries per placement workgroup (one per thread)
+constexpr uint32_t kMapWaves = 16;                  // map kernel: 16 data waves per workgroup, no coordinator
+constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 0-3: sF, sT, fV, dense)
+
+struct MapArgs {
+  const uint8_t* base;         // 16-byte aligned; coordinates relative to it
+  uint64_t nchunks, nranges;
+  uint4* rec;                  // [nranges] range summaries
+  uint16_t* spill;             // [nranges][kSpillCap] event positions relative to the range
+};
+
+// Range r of the chunk table (ranges of kWaveBytes in each chunk's aligned coordinates): the Geo of a
+// one-range "unit" (lo_u / hi_u relative to the range, clamped like wave_lo / wave_hi of wave 0).
+__device__ __forceinline__ Geo range_geo(const Tab& T, uint32_t nchunks, uint32_t nranges, uint32_t r, Cursor& cur) {
+  Geo g;
+  if (r >= nranges) {
+    g.ubase = 0;
+    g.lo_u = g.hi_u = g.c = g.fl = 0;
+    return g;
+  }
+  if (!cur.valid || r < cur.u0 || r >= cur.u1) {
+    uint32_t c = 0, cn = nchunks;
+    while (cn - c > 1) {                               // a wave's ranges are strided: always a search
+      const uint32_t m = (c + cn) >> 1;
+      if ((uint32_t)T.u0[m] <= r) c = m; else cn = m;
+    }
+    cur.c = c;
+    cur.u0 = (uint32_t)T.u0[c];
+    cur.u1 = (uint32_t)T.u0[c + 1];
+    cur.lo = T.lo[c];
+    cur.hi = T.hi[c];
+    cur.valid = 1;
+  }
+  g.c = cur.c;
+  g.ubase = (cur.lo & ~15ull) + (uint64_t)(r - cur.u0) * (uint64_t)kWaveBytes;
+  g.lo_u = cur.lo > g.ubase ? (uint32_t)(cur.lo - g.ubase) : 0u;
+  const uint64_t hu = cur.hi - g.ubase;
+  g.hi_u = hu < (uint64_t)(kWaveBytes + 16) ? (uint32_t)hu : (uint32_t)(kWaveBytes + 16);
+  g.fl = kGeoValid | (r == cur.u0 ? kGeoFirst : 0u) | (r + 1 == cur.u1 ? kGeoLast : 0u);
+  return g;
+}
+
+__global__ void __launch_bounds__(kWave * kMapWaves) fasta_map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
+                                                                      const uint64_t* __restrict__ tab_hi,
+                                                                      const uint64_t* __restrict__ tab_r0) {
+  __shared__ __attribute__((aligned(16))) uint16_t sev[kMapWaves][kSpillCap];
+  const int lane = __lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
+  const uint32_t nranges = (uint32_t)M.nranges, nchunks = (uint32_t)M.nchunks;
+  const uint32_t NW = gridDim.x * kMapWaves;
+  uint32_t r = blockIdx.x * kMapWaves + (uint32_t)wave;
+  if (r >= nranges) return;
+  uint16_t* evw = sev[wave];
+  Cursor cur{0, 0, 0, 0, 0, 0};
+  Geo g = range_geo(T, nchunks, nranges, r, cur);
+  Buf b[kBufs];
+#pragma unroll
+  for (int h = 0; h < kBufs; ++h) load_buf(b[h], ScanArgs{M.base}, g, 0, lane, h);
+  for (;;) {
+    const uint32_t rn = r + NW;
+    const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
+    FState st{0u, 0u, 0u, -1, 0u, 0u};
+    const int lo = (int)g.lo_u, hi = (int)g.hi_u;
+    const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
+    auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kSpillCap - 1u ? rk : kSpillCap - 1u] = (uint16_t)pos; };
+#pragma unroll
+    for (int h = 0; h < kBufs; ++h) {
+      wait_buf(b[h]);                                 // this buffer landed; the other stays in flight
+      v4u x[kRows];
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
+      if (interior) fasta_rows<true>(x, b[h].la, h, lo, hi, lane, st, keep);
+      else fasta_rows<false>(x, b[h].la, h, lo, hi, lane, st, keep);
+      if (h + 1 < kBufs) load_buf(b[h], ScanArgs{M.base}, gn, 0, lane, h);
+    }
+    // the range's summary (phase_a_rec of a one-range unit) and its events
+    if (!st.nlseen) st.fV = st.S;
+    uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
+    if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
+    const bool dense = st.nev > kSpillCap;
+    const uint32_t n = dense ? 0u : st.nev;
+    cbar();
+    if ((uint32_t)lane * 8u < n) {
+      const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
+      __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(M.spill + (uint64_t)r * kSpillCap) + lane);
+    }
+    if (lane == 0) {
+      const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
+                          ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
+      M.rec[r] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+    }
+    load_buf(b[kBufs - 1], ScanArgs{M.base}, gn, 0, lane, kBufs - 1);
+    if (rn >= nranges) break;
+    r = rn;
+    g = gn;
+  }
+  drain_bufs(b);
+}
+
+// Wave-wide (64-lane) inclusive scan of range functions, lane 0 farthest.
+__device__ __forceinline__ Func32 f32_wave_scan(Func32 f) {
+  f = f32_then(f32_dpp<kRowShr1, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowShr2, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowShr4, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowShr8, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowBcast15, 0xA>(f), f);
+  f = f32_then(f32_dpp<kRowBcast31, 0xC>(f), f);
+  return f;
+}
+
+struct PlaceArgs {
+  const uint4* rec;
+  const uint16_t* spill;
+  uint64_t nranges, nblocks;
+  int count_only;              // no output buffer: counts, chunk ends and pending only
+};
+
+template <int OUT64>
+__global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, ScanArgs A,
+                                                                 const uint64_t* __restrict__ tab_lo,
+                                                                 const uint64_t* __restrict__ tab_hi,
+                                                                 const uint64_t* __restrict__ tab_r0) {
+  typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
+  constexpr int kPW = kPlaceBlock / kWave;           // 16 waves
+  __shared__ uint32_t s_blk;
+  __shared__ Func32 s_wagg[kPW];
+  __shared__ Func32 s_wex[kPW];
+  __shared__ uint64_t s_P;
+  __shared__ uint32_t s_S;
+  __shared__ uint32_t s_ndense;
+  __shared__ uint32_t s_dense[kPlaceBlock];
+  __shared__ uint64_t s_dP[kPlaceBlock];
+  __shared__ uint32_t s_dS[kPlaceBlock];
+  const int lane = __lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
+  if (threadIdx.x == 0) {
+    s_blk = atomicAdd(&A.ticket[0], 1u);             // blocks in claim order: a block only waits on lower,
+    s_ndense = 0;                                     // already running or finished, blocks
+  }
+  __syncthreads();
+  const uint32_t b = s_blk;
+  const uint64_t r = (uint64_t)b * kPlaceBlock + threadIdx.x;
+  const bool valid = r < PA.nranges;
+  uint4 rc = uint4{0u, 0u, 2u, 0u};                   // identity: no count, state kept
+  if (valid) rc = PA.rec[r];
+  const uint32_t cF = rc.x & 0xFFFFu, cT = rc.x >> 16, fl = rc.z;
+  const Func32 f{cF, cT, fl & 1u, (fl >> 1) & 1u};
+  const Func32 inc = f32_wave_scan(f);
+  const Func32 ex = Func32{dpp32<kWaveShr1, 0xF>(inc.cF, 0u), dpp32<kWaveShr1, 0xF>(inc.cT, 0u),
+                           dpp32<kWaveShr1, 0xF>(inc.sF, 0u), dpp32<kWaveShr1, 0xF>(inc.sT, 1u)};
+  if (lane == kWave - 1) s_wagg[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    Func32 w = lane < kPW ? s_wagg[lane] : Func32{0, 0, 0, 1};
+    Func32 wi = w;
+    wi = f32_then(f32_dpp<kRowShr1, 0xF>(wi), wi);
+    wi = f32_then(f32_dpp<kRowShr2, 0xF>(wi), wi);
+    wi = f32_then(f32_dpp<kRowShr4, 0xF>(wi), wi);
+    wi = f32_then(f32_dpp<kRowShr8, 0xF>(wi), wi);
+    const Func32 we = f32_dpp<kRowShr1, 0xF>(wi);
+    if (lane < kPW) s_wex[lane] = we;
+    const Func agg{(uint32_t)__builtin_amdgcn_readlane((int)wi.cF, kPW - 1),
+                   (uint32_t)__builtin_amdgcn_readlane((int)wi.cT, kPW - 1),
+                   (uint32_t)__builtin_amdgcn_readlane((int)wi.sF, kPW - 1) & 1u,
+                   (uint32_t)__builtin_amdgcn_readlane((int)wi.sT, kPW - 1) & 1u};
+    // the block's exclusive prefix: a decoupled look-back over the block descriptors
+    uint64_t P = 0;
+    uint32_t S = 0;
+    if (b > 0) {
+      if (lane == 0) st_desc(&A.desc[b], pack_agg(agg) | A.epoch);
+      const uint32_t W = lb_span(b, kNoUnit);
+      uint64_t t0 = 0;
+      for (uint32_t spins = 0;; ++spins) {
+        uint64_t d[kLbPer];
+        lb_load(A, b, W, lane, d);
+        if (lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S)) break;
+        if (wait_expired(spins, t0)) {
+          if (lane == 0) atomicOr(A.err, kErrTimeout);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const uint64_t P_incl = P + (S ? agg.cT : agg.cF);
+    const uint32_t S_out = S ? agg.sT : agg.sF;
+    if (lane == 0) {
+      st_desc(&A.desc[b], pack_prefix(P_incl, S_out) | A.epoch);
+      s_P = P;
+      s_S = S;
+    }
+  }
+  __syncthreads();
+  const uint64_t Pb = s_P;
+  const uint32_t Sb = s_S;
+  // this range's incoming state: the block prefix, then the waves before it, then the lanes before it
+  const Func32 wx = s_wex[wave];
+  const uint64_t Pw = Pb + (Sb ? wx.cT : wx.cF);
+  const uint32_t Sw = Sb ? wx.sT : wx.sF;
+  uint64_t P = Pw + (Sw ? ex.cT : ex.cF);
+  uint32_t S = (Sw ? ex.sT : ex.sF) & 1u;
+  if (fl & kRecFirst) S = 0u;                         // chunk start: no header pending
+  if (valid) {
+    const uint64_t P_incl = P + (S ? cT : cF);
+    const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
+    if (fl & kRecLast) {
+      A.chunk_end[rc.w] = P_incl;
+      A.pending[rc.w] = S_out ? (long long)P_incl - 1 : -1ll;
+    }
+    if (r + 1 == PA.nranges) A.total[0] = P_incl;
+  }
+  if (valid && !PA.count_only) {
+    const uint32_t c = rc.w;
+    const uint64_t lo = T.lo[c];
+    const uint64_t wbase = (lo & ~15ull) + (r - (uint64_t)T.u0[c]) * (uint64_t)kWaveBytes;
+    if (fl & kFlDense) {
+      s_dense[atomicAdd(&s_ndense, 1u)] = threadIdx.x;
+    } else {
+      const uint64_t obj_off = A.obj_base - A.shift + wbase;
+      const bool near4g = OUT64 == 0 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+      const uint32_t fn = rc.y & 0xFFFFu, nev = rc.y >> 16;
+      const uint32_t fV = (fl >> 2) & 1u;
+      const uint32_t skip = S & fV;
+      const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
+      const uint64_t b0 = 2 * P - S, last = 2 * A.cap - 1;
+      bool ovf = false;
+      auto emit = [&](uint64_t slot, uint32_t e) {
+        const uint64_t val = obj_off + e + (slot & 1u);
+        if (near4g) ovf |= val > 0xFFFFFFFFull;
+        put<OutT>(A.out, slot < last ? slot : last, val);
+      };
+      if (pre) emit(b0, fn - 1u);
+      const uint4* sp = reinterpret_cast<const uint4*>(PA.spill + r * kSpillCap);
+      const uint64_t base_slot = b0 + pre - skip;     // event k goes to base_slot + k (k >= skip)
+      for (uint32_t k0 = 0; k0 < nev; k0 += 8u) {
+        const uint4 v = sp[k0 >> 3];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (uint32_t e = 0; e < 8u; ++e) {
+          const uint32_t k = k0 + e;
+          if (k >= skip && k < nev) emit(base_slot + k, (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu);
+        }
+      }
+      if (ovf) atomicOr(A.err, kErrOverflow);
+    }
+  }
+  // dense ranges: one wave each, rescanned from the input with the now known state
+  __syncthreads();
+  const uint32_t nd = s_ndense;
+  if (nd) {
+    // every thread keeps its own (P, S); a wave fetches a dense range's through LDS
+    s_dP[threadIdx.x] = P;
+    s_dS[threadIdx.x] = S;
+    __syncthreads();
+    for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
+      const uint32_t t = s_dense[i];
+      const uint64_t rr = (uint64_t)b * kPlaceBlock + t;
+      const uint4 rq = PA.rec[rr];
+      const uint32_t c = rq.w;
+      const uint64_t lo = T.lo[c], hi = T.hi[c];
+      const uint64_t wbase = (lo & ~15ull) + (rr - (uint64_t)T.u0[c]) * (uint64_t)kWaveBytes;
+      const uint32_t lo_w = lo > wbase ? (uint32_t)(lo - wbase) : 0u;
+      const uint64_t hw = hi - wbase;
+      const uint32_t hi_w = hw < (uint64_t)(kWaveBytes + 16) ? (uint32_t)hw : (uint32_t)(kWaveBytes + 16);
+      dense_b<kFasta, OUT64>(A, wbase, lo_w | (hi_w << 16), s_dP[t], s_dS[t], lane);
+    }
+  }
+  // every block is done with the ticket: the last one resets it for the next launch on this table
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (atomicAdd(&A.ticket[1], 1u) == gridDim.x - 1u) {
+      atomicExch(&A.ticket[0], 0u);
+      atomicExch(&A.ticket[1], 0u);
+    }
+  }
+}
+
 // x - pa clamped to 0..16 (the byte bound inside one 16-byte lane), without 32-bit truncation
 __device__ __forceinline__ int lane_rel(uint64_t x, uint64_t pa) {
   return x <= pa ? 0 : (x - pa >= 16u ? 16 : (int)(x - pa));
@@ -1693,6 +1986,11 @@ struct dp_ctx {
   uint64_t h_cap = 0;
   std::vector<uint64_t> last_tab;     // last uploaded table (skip identical re-uploads)
   uint64_t* d_tab_uploaded = nullptr;
+  // two-kernel FASTA workspace: range summaries and event spill slots (grow-only)
+  uint4* d_rec = nullptr;
+  uint16_t* d_spill = nullptr;
+  uint64_t rec_cap = 0;               // ranges
+  bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
   uint64_t nchunks = 0, cap = 0;
@@ -1777,7 +2075,7 @@ int harvest_events(dp_ctx* c) {
 // has units), so only the upload sets their defaults (-1, ~0, 0) and err = 0.  A launch that sets an err
 // bit drops last_tab, so the next one re-uploads (results of a failed launch are discarded anyway).
 int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, const uint64_t* chunks,
-                 uint64_t n, uint64_t* nunits_out) {
+                 uint64_t n, uint64_t* nunits_out, uint64_t unit_bytes = kUnitBytes) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
   std::vector<uint64_t> tab(3 * n + 1);
   uint64_t units = 0;
@@ -1790,9 +2088,10 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     tab[i] = lo;
     tab[n + i] = hi;
     tab[2 * n + i] = units;
-    if (hi > lo) units += (hi - (lo & ~15ull) + kUnitBytes - 1) / kUnitBytes;
+    if (hi > lo) units += (hi - (lo & ~15ull) + unit_bytes - 1) / unit_bytes;
   }
   tab[3 * n] = units;
+  tab.push_back(unit_bytes);                          // (host-side only: a change of geometry re-uploads)
   const uint64_t words = 5 * n + 1 + 5;
   int rc = ensure_tab(c, words);
   if (rc) return rc;
@@ -1801,7 +2100,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
   if (tab != c->last_tab) {
     // the pinned mirror may still feed an earlier async copy: wait for the stream before rewriting it
     HIPCHK(hipStreamSynchronize(c->stream));
-    memcpy(c->h_tab, tab.data(), tab.size() * 8);
+    memcpy(c->h_tab, tab.data(), (3 * n + 1) * 8);
     memset(c->h_tab + c->pend_off, 0xFF, 2 * n * 8);
     memset(c->h_tab + c->ctrl_off, 0, 5 * 8);
     HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, words * 8, hipMemcpyHostToDevice, c->stream));
@@ -1883,6 +2182,95 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   return DP_OK;
 }
 
+// The two-kernel FASTA index (fasta_map_kernel + fasta_place_kernel) over a chunk table staged with
+// 16 KiB ranges.  Timed as one span: the HIP events bracket both kernels.
+int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
+                  int out_u64, uint64_t cap) {
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  if (nranges == 0) return DP_OK;
+  if (nranges >= 0xFFFFFFFFull) return fail(DP_ERR_INVALID, "launch exceeds 2^32 ranges of 16 KiB");
+  if (nranges > c->rec_cap) {
+    if (c->d_rec) HIPCHK(hipFree(c->d_rec));
+    if (c->d_spill) HIPCHK(hipFree(c->d_spill));
+    c->d_rec = nullptr;
+    c->d_spill = nullptr;
+    c->rec_cap = 0;
+    const uint64_t cap_r = nranges + nranges / 8 + 64;
+    HIPCHK(hipMalloc(&c->d_rec, cap_r * sizeof(uint4)));
+    HIPCHK(hipMalloc(&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t)));
+    c->rec_cap = cap_r;
+  }
+  const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
+  int rc = ensure_desc(c, nblocks);
+  if (rc) return rc;
+  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
+    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
+    c->desc_epoch = 0;
+  }
+  ScanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = d_buf - shift;
+  a.shift = shift;
+  a.obj_base = buf_base;
+  a.nchunks = n;
+  a.nunits = nranges;
+  a.desc = c->d_desc;
+  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
+  const int count_only = (cap == 0 || d_out == nullptr);
+  if (count_only) {
+    d_out = c->d_tab + c->ctrl_off + 2;
+    cap = 1;
+  }
+  a.out = d_out;
+  a.cap = cap;
+  a.out_u64 = out_u64;
+  a.every_k = 1;
+  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
+  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
+  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
+  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
+  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  MapArgs m;
+  m.base = a.base;
+  m.nchunks = n;
+  m.nranges = nranges;
+  m.rec = c->d_rec;
+  m.spill = c->d_spill;
+  PlaceArgs pa;
+  pa.rec = c->d_rec;
+  pa.spill = c->d_spill;
+  pa.nranges = nranges;
+  pa.nblocks = nblocks;
+  pa.count_only = count_only;
+  const uint64_t waves_needed = (nranges + kMapWaves - 1) / kMapWaves;
+  const unsigned grid = (unsigned)(waves_needed < (uint64_t)c->cus ? waves_needed : (uint64_t)c->cus);
+  const uint64_t* tlo = c->d_tab;
+  const uint64_t* thi = c->d_tab + n;
+  const uint64_t* tr0 = c->d_tab + 2 * n;
+  DeviceSerial& ds = g_serial[c->device];
+  std::lock_guard<std::mutex> lock(ds.m);
+  if (ds.last && ds.last_stream != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, ds.last, 0));
+  if (!c->ev_scan) HIPCHK(hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming | hipEventReleaseToDevice));
+  hipEvent_t e0;
+  rc = ev_begin(c, &e0);
+  if (rc) return rc;
+  hipLaunchKernelGGL(fasta_map_kernel, dim3(grid), dim3(kWave * kMapWaves), 0, c->stream, m, tlo, thi, tr0);
+  HIPCHK(hipGetLastError());
+  if (out_u64)
+    hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, c->stream, pa, a, tlo,
+                       thi, tr0);
+  else
+    hipLaunchKernelGGL((fasta_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, c->stream, pa, a, tlo,
+                       thi, tr0);
+  HIPCHK(hipGetLastError());
+  rc = ev_end(c);
+  if (rc) return rc;
+  HIPCHK(hipEventRecord(c->ev_scan, c->stream));
+  ds.last = c->ev_scan;
+  ds.last_stream = c->stream;
+  return DP_OK;
+}
+
 int check_ctx(dp_ctx* c) {
   if (!c) return fail(DP_ERR_INVALID, "null dp_ctx");
   HIPCHK(hipSetDevice(c->device));
@@ -1951,6 +2339,8 @@ int dp_ctx_create(int device, dp_ctx** out) {
   if (per_cu < 1) per_cu = 1;
   c->grid = c->cus * per_cu;
   if (c->grid > 256) c->grid = 256;   // one look-back window (G <= 256) per unit
+  const char* onepass = getenv("DP_FASTA_ONEPASS");
+  c->fasta_onepass = onepass && atoi(onepass) != 0;
   *out = c;
   return DP_OK;
 }
@@ -1970,6 +2360,8 @@ int dp_ctx_destroy(dp_ctx* c) {
     (void)hipEventDestroy(c->ev_scan);
   }
   if (c->d_desc) (void)hipFree(c->d_desc);
+  if (c->d_rec) (void)hipFree(c->d_rec);
+  if (c->d_spill) (void)hipFree(c->d_spill);
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->h_tab) (void)hipHostFree(c->h_tab);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -2063,9 +2455,15 @@ int dp_fasta_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint
   if (cap_pairs && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
   if (buf_base + buf_len > obj_size) return fail(DP_ERR_INVALID, "buffer extends beyond the object");
   uint64_t units = 0;
-  rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units);
-  if (rc) return rc;
-  rc = launch_scan(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0);
+  if (c->fasta_onepass) {
+    rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units);
+    if (rc) return rc;
+    rc = launch_scan(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0);
+  } else {
+    rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units, kWaveBytes);
+    if (rc) return rc;
+    rc = launch_fasta2(c, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs);
+  }
   if (rc) return rc;
   if (nchunks) {
     const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);

@@ -35,6 +35,7 @@ logger = logging.getLogger(__name__)
 
 
 INDEX_DTYPES = {"uint32": np.uint32, "uint64": np.uint64}
+GET_MANY_GROUP_BYTES = 256 << 20      # slice bytes fetched per coalesced group in FASTASlice.get_many
 
 
 def _index_dtype(index_dtype: str):
@@ -121,7 +122,6 @@ class FASTASlice(CloudObjectSlice):
         host buffer, and each slice is cut from it — instead of 1-2 GETs per slice.  Slices whose ranges the
         storage would not serve as plain byte ranges (empty or out-of-object) keep their own ``get()``, so
         results and errors are the reference's."""
-        from ...storage.ranges import Extents
         out = [None] * len(slices)
         by_obj = {}
         for i, s in enumerate(slices):
@@ -137,21 +137,41 @@ class FASTASlice(CloudObjectSlice):
                 out[i] = s.get()
         for co, idxs in by_obj.values():
             size = co.size
-            want = []
-            for i in idxs:
+            # bounded groups of neighbouring slices: one group's extents are held at a time, so the peak host
+            # memory is the results plus GET_MANY_GROUP_BYTES, not twice the requested bytes
+            order = sorted(idxs, key=lambda i: slices[i].range_0)
+            group, gbytes = [], 0
+            for j, i in enumerate(order):
                 s = slices[i]
-                want.append((s.range_0, min(s.range_1, size)))
+                group.append(i)
+                gbytes += min(s.range_1, size) - s.range_0
                 if s.header is not None:
-                    want.append((s.header[0], min(s.header[1], size)))
-            ext = Extents(co.storage, co.path.bucket, co.path.key, want, threads=threads)
-            for i in idxs:
-                s = slices[i]
-                body = ext.view(s.range_0, min(s.range_1, size))
-                if s.header is None:
-                    out[i] = bytes(body)
-                else:
-                    line = bytes(ext.view(s.header[0], min(s.header[1], size)))
-                    out[i] = line[:-1] + f" offset={s.offset}".encode() + b"\n" + bytes(body)
+                    gbytes += min(s.header[1], size) - s.header[0]
+                if gbytes >= GET_MANY_GROUP_BYTES or j + 1 == len(order):
+                    cls._cut_group(co, slices, group, out, threads)
+                    group, gbytes = [], 0
+        return out
+
+    @staticmethod
+    def _cut_group(co, slices, idxs, out, threads):
+        from ...storage.ranges import Extents
+        size = co.size
+        want = []
+        for i in idxs:
+            s = slices[i]
+            want.append((s.range_0, min(s.range_1, size)))
+            if s.header is not None:
+                want.append((s.header[0], min(s.header[1], size)))
+        ext = Extents(co.storage, co.path.bucket, co.path.key, want, threads=threads)
+        for i in idxs:
+            s = slices[i]
+            body = ext.view(s.range_0, min(s.range_1, size))
+            if s.header is None:
+                out[i] = bytes(body)
+            else:
+                line = bytes(ext.view(s.header[0], min(s.header[1], size)))
+                out[i] = line[:-1] + f" offset={s.offset}".encode() + b"\n" + bytes(body)
+        del ext
         return out
 
 

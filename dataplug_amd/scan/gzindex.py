@@ -32,6 +32,7 @@ from typing import Callable, List, Optional
 import numpy as np
 
 from .. import gz as gzlib
+from ._lib import DPCapacityError
 from .device import ScanContext
 
 PIECE_BYTES = 64 << 20
@@ -171,7 +172,12 @@ class _Inflater(threading.Thread):
                         return
             except BaseException as e:                   # surfaced by the inflater loop
                 self.error = e
-                inq.put(b"")
+                while not stop_reading.is_set():         # wake the consumer unless it has already left
+                    try:
+                        inq.put(b"", timeout=0.5)
+                        break
+                    except queue.Full:
+                        continue
 
         rt = threading.Thread(target=reader, daemon=True, name="dpgz-read")
         try:
@@ -238,10 +244,19 @@ class _Inflater(threading.Thread):
             if pending is None:
                 a, l, o, used = gzlib.bgzf_scan(cbuf)
                 if len(a) == 0:
+                    # no complete member: drop the zero padding already skipped, then read on (a member is at
+                    # most 64 KiB, so more input always completes one unless the stream ends)
+                    if used:
+                        cbuf = cbuf[used:].copy()
+                        in_base += used
                     if eof:
                         if len(cbuf) and (cbuf != 0).any():
                             raise ValueError("gzip stream: truncated BGZF member")
                         return
+                    more = self.read(BGZF_BATCH)
+                    eof = len(more) == 0
+                    if more:
+                        cbuf = np.concatenate((cbuf, np.frombuffer(more, np.uint8)))
                     continue
                 pending = (a, l, o, used)
             a, l, o, used = pending
@@ -290,7 +305,7 @@ def index_stream(ctx: ScanContext, read: Callable[[int], bytes], record_lines: i
     pins = [ctx.pinned(f"gzpiece{i}", piece_bytes) for i in range(n_pieces)]
     arrays = [p.array[:piece_bytes] for p in pins]
     d_piece = ctx.workspace("gzpiece", piece_bytes + 64)
-    cap = piece_bytes // (2 * k) + 1024                  # read ends per piece: at most one per 2k bytes
+    cap = piece_bytes // k + 1024                        # read ends per piece: at most one per k bytes (empty lines)
     d_out = ctx.workspace("gzends", 8 * cap + 16)
     res = GzIndex(ends=tempfile.SpooledTemporaryFile(SPOOL_MEM), windows=tempfile.SpooledTemporaryFile(SPOOL_MEM))
     inf = _Inflater(read, arrays, span, threads or pool_threads(), region_bytes)
@@ -310,8 +325,14 @@ def index_stream(ctx: ScanContext, read: Callable[[int], bytes], record_lines: i
             if n:
                 ctx.h2d_async(d_piece.ptr, pins[piece.slot].ptr, n)
                 rg = np.array([o0, o0 + n], np.uint64)
-                ctx.delim_ranges_async(d_piece.ptr, n, o0, rg, 10, k, 1, carry, d_out.ptr, 1, cap)
-                cnt, nd, _ = ctx.delim_ranges_result(1)
+                while True:
+                    ctx.delim_ranges_async(d_piece.ptr, n, o0, rg, 10, k, 1, carry, d_out.ptr, 1, cap)
+                    try:
+                        cnt, nd, _ = ctx.delim_ranges_result(1)
+                        break
+                    except DPCapacityError as e:         # cannot happen with the bound above; grow anyway
+                        cap = e.needed
+                        d_out = ctx.workspace("gzends", 8 * cap + 16)
                 ends = ctx.d2h(np.empty(cnt, np.uint64), d_out.ptr)
             # access points of this piece: line number = 1 + newlines before out_byte
             woff = 0

@@ -9,7 +9,9 @@ from __future__ import annotations
 
 import concurrent.futures as cf
 import os
+import threading
 from dataclasses import dataclass
+from functools import partial
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -119,10 +121,43 @@ def resolve_line_end(ctx: ScanContext, storage, bucket: str, key: str, size: int
     return size
 
 
+# ------------------------------------------------------------------------------------------ per-GPU workers
+_workers_lock = threading.Lock()
+_workers = {}
+
+
+def group_worker(device: int, slot: int = 0) -> cf.ThreadPoolExecutor:
+    """The long-lived worker thread of (device, slot): a one-thread executor whose thread keeps its
+    ``ScanContext`` — stream, pinned staging and HBM workspace — across calls, so a multi-GPU
+    ``co.preprocess`` allocates nothing once its buffers have grown to the object size.  ``slot`` tells
+    apart several groups on one device (``dataplug_devices=[0, 0]``, the one-GPU rehearsal of the split)."""
+    key = (int(device), int(slot))
+    with _workers_lock:
+        ex = _workers.get(key)
+        if ex is None:
+            ex = _workers[key] = cf.ThreadPoolExecutor(1, thread_name_prefix=f"dpscan-gpu{device}.{slot}")
+        return ex
+
+
+def run_on_devices(devs: Sequence[int], jobs: Sequence) -> list:
+    """Run job k (a callable taking no argument) on device devs[k]'s persistent worker; one job alone runs
+    on the calling thread (its own thread-local context).  Returns the results in job order."""
+    if len(jobs) == 1:
+        return [jobs[0]()]
+    seen = {}
+    futs = []
+    for k, job in enumerate(jobs):
+        d = devs[k]
+        slot = seen.get(d, 0)
+        seen[d] = slot + 1
+        futs.append(group_worker(d, slot).submit(job))
+    return [f.result() for f in futs]
+
+
 # ------------------------------------------------------------------------------------------ FASTA
 @dataclass(frozen=True)
 class FastaGroup:
-    """One GPU's share of a FASTA chunk plan: chunks [i0, i1) of the plan (contiguous, so the outputs
+    """One GPU's share of a FASTA scan plan: entries [i0, i1) of the plan (contiguous, so the outputs
     concatenate in chunk order like merge_fasta_metadata, fasta.py:66-74), the bytes they scan [lo, hi),
     and the bytes fetched into HBM [lo, buf_hi): ``hi`` plus a look-ahead halo, so a header line cut by the
     group's last chunk usually ends inside the same launch (resolve kernel) instead of a later GET."""
@@ -136,10 +171,71 @@ class FastaGroup:
         return list(plan[self.i0:self.i1])
 
 
+@dataclass(frozen=True)
+class FastaPiece:
+    """Bytes [a, b) of chunk ``chunk`` of the reference's plan, scanned as one launch chunk [a, end).  A
+    piece cut inside its chunk scans one byte past its end (end = b + 1): a '>' at b - 1 is then judged with
+    its next byte, as in the whole chunk (fasta.py:36 needs p + 1 < chunk end), while a '>' at b itself is
+    left to the next piece.  ``first``: a is the chunk's own start (the line state starts empty there)."""
+    chunk: int
+    a: int
+    b: int
+    end: int
+    first: bool
+
+
+def fasta_pieces(plan: Sequence[Tuple[int, int]], n_groups: int) -> List[List[FastaPiece]]:
+    """The reference's chunk plan cut into ``n_groups`` byte-balanced, contiguous runs of pieces (SURVEY.md
+    §8(e)).  Group boundaries fall at every total/n bytes of chunk data, so a plan with fewer chunks than
+    GPUs (the reference's canonical ``chunk_size = ceil(size / 4)`` on 8 GPUs) still fills every GPU; a
+    boundary within ``snap`` bytes of a chunk boundary moves there (no sliver pieces), so an equal-chunk plan
+    whose chunk count the group count divides is not cut at all."""
+    n_groups = max(1, int(n_groups))
+    lens = [max(0, c1 - c0) for c0, c1 in plan]
+    total = sum(lens)
+    starts = np.concatenate(([0], np.cumsum(lens, dtype=np.int64))) if plan else np.zeros(1, np.int64)
+    targets = sorted({(k * total) // n_groups for k in range(1, n_groups)} - {0, total}) if total else []
+    snap = min(1 << 20, total // (8 * n_groups)) if total else 0
+    bounds = []                                          # cumulative byte positions of the group boundaries
+    for t in targets:
+        i = int(np.searchsorted(starts, t, side="right")) - 1        # chunk holding byte t
+        near = min((int(starts[i]), int(starts[i + 1])), key=lambda x: abs(x - t)) if i + 1 < len(starts) else t
+        bounds.append(near if abs(near - t) <= snap else t)
+    bounds = sorted(set(b for b in bounds if 0 < b < total))
+    groups: List[List[FastaPiece]] = [[] for _ in range(len(bounds) + 1)]
+    for i, (c0, c1) in enumerate(plan):
+        s0, s1 = int(starts[i]), int(starts[i] + lens[i])
+        cuts = [b for b in bounds if s0 < b < s1]
+        edges = [s0] + cuts + [s1]
+        for j in range(len(edges) - 1):
+            a = c0 + (edges[j] - s0)
+            b = c0 + (edges[j + 1] - s0)
+            last = j == len(edges) - 2
+            g = int(np.searchsorted(np.asarray(bounds, np.int64), edges[j], side="right"))
+            groups[g].append(FastaPiece(i, a, b, b if last else b + 1, j == 0))
+    return [g for g in groups if g]
+
+
+def fasta_split(plan: Sequence[Tuple[int, int]], n_groups: int, size: int, halo: int = _HALO0):
+    """(pieces, scan plan, groups): ``fasta_pieces`` flattened in order, the launch chunks ``[(a, end)]`` of
+    those pieces, and one ``FastaGroup`` per GPU over that scan plan.  Used by ``fasta_index_object`` and by
+    bench.py's multi-GPU line (one thread or rank per group)."""
+    runs = fasta_pieces(plan, n_groups)
+    pieces = [p for r in runs for p in r]
+    scan_plan = [(p.a, p.end) for p in pieces]
+    groups, i = [], 0
+    for r in runs:
+        j = i + len(r)
+        lo = min(p.a for p in r)
+        hi = max(p.end for p in r)
+        groups.append(FastaGroup(i, j, lo, hi, min(size, hi + halo)))
+        i = j
+    return pieces, scan_plan, groups
+
+
 def fasta_groups(plan: Sequence[Tuple[int, int]], n_groups: int, size: int, halo: int = _HALO0) -> List[FastaGroup]:
-    """The multi-GPU split of one object's chunk plan (the reference runs the chunks as
-    independent map jobs, preprocess.py:39-51): ``split_groups`` of the chunk list over ``n_groups`` GPUs.
-    Used by ``fasta_index_object`` and by bench.py's multi-GPU line (one thread or rank per group)."""
+    """The multi-GPU split of one object's chunk plan when its chunks are kept whole: ``split_groups`` of the
+    chunk list over ``n_groups`` GPUs (tests/test_dist_gloo.py's reference split)."""
     out = []
     for i0, i1 in split_groups(len(plan), n_groups):
         if i1 <= i0:
@@ -173,39 +269,82 @@ def fasta_passes(plan: Sequence[Tuple[int, int]], g: FastaGroup, size: int, budg
     return out
 
 
-def _fasta_group(dev: int, co, plan: Sequence[Tuple[int, int]], g: FastaGroup, u64: bool) -> np.ndarray:
+def _fasta_group(dev: int, co, scan_plan: Sequence[Tuple[int, int]], pieces: Sequence[FastaPiece], g: FastaGroup,
+                 u64: bool):
+    """One GPU's group on the calling thread's context for ``dev``: (pairs of each piece, first '\\n' of each
+    piece cut inside its chunk, or None when it has none)."""
     ctx = get_context(dev)
     size = co.size
-    parts = []
-    for p_ in fasta_passes(plan, g, size, max_launch_bytes()):
+    per_piece, first_nl = [], {}
+    for p_ in fasta_passes(scan_plan, g, size, max_launch_bytes()):
         n = p_.buf_hi - p_.lo
         d = ctx.workspace("input", n + 64)
         fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, p_.lo, p_.buf_hi, d.ptr)
-        pairs, pending, _ = ctx.fasta_index(d.ptr, n, p_.lo, size, p_.chunks(plan), u64=u64)
+        pairs, pending, cend = ctx.fasta_index(d.ptr, n, p_.lo, size, p_.chunks(scan_plan), u64=u64)
         for p in pending[pending >= 0]:
             start = int(pairs[p, 0])
             end = resolve_line_end(ctx, co.storage, co.path.bucket, co.path.key, size, p_.buf_hi)
             if not u64 and end > 0xFFFFFFFF:
                 raise OverflowError(f"FASTA offset {end} does not fit the uint32 index (header at {start})")
             pairs[p, 1] = end
-        parts.append(pairs)
-    return parts[0] if len(parts) == 1 else np.concatenate(parts)
+        prev = 0
+        for k in range(p_.i0, p_.i1):
+            e = int(cend[k - p_.i0])
+            per_piece.append(pairs[prev:e])
+            prev = e
+            pc = pieces[k]
+            if not pc.first:                              # the first line segment of a cut piece
+                nl = ctx.find_delim(d.ptr, n, p_.lo, pc.a, 10)
+                first_nl[k] = nl if 0 <= nl < pc.end else None
+    return per_piece, first_nl
+
+
+def stitch_pieces(pieces: Sequence[FastaPiece], per_piece: Sequence[np.ndarray], first_nl: dict) -> np.ndarray:
+    """Pairs of cut chunks as the whole chunks give them (fasta.py:24-56).  Each piece was scanned with an
+    empty line state at its start; where the chunk's true state there says a header is open on the current
+    line (the previous piece ended inside a header line), the piece's headers in its first line segment —
+    before its first '\\n' — are not headers of the chunk: they are dropped.  The open header's end needs no
+    fix: ends are always the object's next '\\n' (resolved on the device or from later bytes).  The state
+    carried on is the piece's own at its end (a header pending there) once the piece holds a '\\n', or stays
+    open through a piece without one."""
+    out = []
+    S = False
+    for k, (pc, pairs) in enumerate(zip(pieces, per_piece)):
+        if pc.first:
+            S = False
+        pend = len(pairs) > 0 and int(pairs[-1, 1]) > pc.end
+        if pc.first:
+            keep = pairs
+        else:
+            nl = first_nl.get(k)
+            if S:
+                keep = pairs[:0] if nl is None else pairs[pairs[:, 0] > nl]
+            else:
+                keep = pairs
+            if nl is None:
+                pend = S or pend
+        S = pend
+        out.append(keep)
+    return np.concatenate(out) if out else np.zeros((0, 2), np.uint32)
 
 
 def fasta_index_object(co, plan: Sequence[Tuple[int, int]], u64: bool = False,
                        max_devices: Optional[int] = None) -> np.ndarray:
     """(n, 2) (start, end) pairs of every chunk of ``plan`` concatenated in chunk order — the index
-    ``merge_fasta_metadata`` (fasta.py:66-74) assembles from the per-chunk map outputs."""
+    ``merge_fasta_metadata`` (fasta.py:66-74) assembles from the per-chunk map outputs.  The plan's bytes are
+    cut into one byte-balanced group per GPU (``fasta_split``), each scanned by its device's persistent
+    worker, and the cut chunks are stitched (``stitch_pieces``)."""
+    dt = np.uint64 if u64 else np.uint32
     if not plan:
-        return np.zeros((0, 2), np.uint64 if u64 else np.uint32)
+        return np.zeros((0, 2), dt)
     devs = devices(max_devices, co)
-    groups = fasta_groups(plan, len(devs), co.size)
-    if len(groups) == 1:
-        return _fasta_group(devs[0], co, plan, groups[0], u64)
-    with cf.ThreadPoolExecutor(len(groups)) as ex:
-        futs = [ex.submit(_fasta_group, devs[k], co, plan, g, u64) for k, g in enumerate(groups)]
-        parts = [f.result() for f in futs]
-    return np.concatenate(parts)
+    pieces, scan_plan, groups = fasta_split(plan, len(devs), co.size)
+    jobs = [partial(_fasta_group, devs[k], co, scan_plan, pieces, g, u64) for k, g in enumerate(groups)]
+    per_piece, first_nl = [], {}
+    for pp, fn in run_on_devices(devs, jobs):
+        first_nl.update(fn)
+        per_piece.extend(pp)
+    return stitch_pieces(pieces, per_piece, first_nl).astype(dt, copy=False)
 
 
 def fasta_index_chunk(co, data, chunk_offset: int, job: int = 0, u64: bool = False) -> np.ndarray:
@@ -328,21 +467,18 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
         r = _delim_group(devs[k % len(devs)], co, lo, hi, delim, 1, 0, fmt=fmt)
         return r[0] if fmt == "u64" else r
 
-    if len(bounds) == 1:
-        out = [run(0)]
-    else:
-        # one worker per GPU; parts of the same GPU run in order on that GPU's thread
-        by_dev = {}
-        for k in range(len(bounds)):
-            by_dev.setdefault(k % len(devs), []).append(k)
-        out = [None] * len(bounds)
+    # parts of one device entry run in order on that entry's persistent worker (run_on_devices)
+    by_dev = {}
+    for k in range(len(bounds)):
+        by_dev.setdefault(k % len(devs), []).append(k)
+    out = [None] * len(bounds)
 
-        def worker(ks):
-            for k in ks:
-                out[k] = run(k)
+    def worker(ks):
+        for k in ks:
+            out[k] = run(k)
 
-        with cf.ThreadPoolExecutor(len(by_dev)) as ex:
-            list(ex.map(worker, by_dev.values()))
+    entries = sorted(by_dev)
+    run_on_devices([devs[e] for e in entries], [partial(worker, by_dev[e]) for e in entries])
     if fmt == "u64":
         return np.concatenate(out)
     low = np.concatenate([o[0] for o in out])

@@ -110,6 +110,18 @@ int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
  * (carry + n_delims) / every_k - carry / every_k.
  *   out_mode 0: uint32 (DP_ERR_OVERFLOW at >= 2^32), 1: uint64, 2: uint32 low words (a paged index: split the
  *   ranges at multiples of 2^32 and read each page's first entry from range_end).
+ *   out_mode 3: uint16 low words plus a 64 KiB block table -- the stored CSV/VCF index (<key>.lines and
+ *   <key>.lines.blocks), a quarter of the uint64 index's bytes:
+ *     - d_out[0 .. n_out) are uint16: entry i = (offset_i + emit_add) & 0xFFFF;
+ *     - the block table follows at byte offset (2 * cap + 15) & ~15 of d_out: uint64 tab[j] for
+ *       j = 0 .. J-1, J = ((last - 1) >> 16) - j0 + 1 (1 if last == first), j0 = first >> 16, where first =
+ *       ranges[0] and last = ranges[2 * nranges - 1]; tab[j] = entries (relative to this launch) before
+ *       object offset (j0 + j) << 16, so entry i's full offset is ((j0 + j) << 16) + low word for the j
+ *       with tab[j] <= i < tab[j + 1] (tab is non-decreasing).  When `first` is not a multiple of 64 KiB,
+ *       tab[0] stands for a boundary below the first byte and is not written: read it as 0.
+ *     - d_out must hold (2 * cap + 15) & ~15 + 8 * J bytes;
+ *     - ranges must be contiguous (range i + 1 starts where range i ends), and d_buf and buf_base must be
+ *       congruent mod 16 (the kernel's 16-byte lanes then sit on object-aligned 64 KiB boundaries).
  *   range_end (host array of nranges, may be NULL): delimiters up to and including range i.
  */
 int dp_delim_ranges_async(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base,

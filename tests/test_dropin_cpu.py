@@ -54,10 +54,11 @@ def stub_scan(monkeypatch, sample):
 
 def _upload(server, data, key="fasta_sample.fasta"):
     co = CloudObject.from_s3(ffa.FASTA, f"s3://genomics/{key}", fetch=False, s3_config=server.storage_config)
-    try:
-        co.storage.head_bucket(Bucket="genomics")
-    except Exception:
-        co.storage.create_bucket(Bucket="genomics")
+    for bucket in ("genomics", "genomics.meta"):     # the index bucket too: tests may run alone (-k)
+        try:
+            co.storage.head_bucket(Bucket=bucket)
+        except Exception:
+            co.storage.create_bucket(Bucket=bucket)
     co.storage.put_object(Body=data, Bucket="genomics", Key=key)
     return CloudObject.from_s3(ffa.FASTA, f"s3://genomics/{key}", s3_config=server.storage_config)
 
@@ -251,6 +252,45 @@ def test_fasta_get_slices_batched_over_http(server, fasta_cases):
         assert n_batched <= 2 and len(calls) >= len(slices)
         checked += 1
     assert checked == len(recs)
+
+
+def test_fasta_get_many_in_bounded_groups(server, monkeypatch):
+    """FASTASlice.get_many holds one bounded group of coalesced extents at a time: with a tiny
+    group size the slices come from several groups and still equal the reference-semantics get()."""
+    from dataplug_amd.entities import get_slices
+    from dataplug_amd.preprocessing.handler import upload_metadata
+    from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
+    from dataplug_amd import synth
+    from oracle import cpu_ref
+    data = bytes(synth.fasta(1 << 18, 11))
+    co = _upload(server, data, "slices_grouped.fasta")
+    idx, nseq = cpu_ref.fasta_index(data, len(data) // 3 + 1)
+    upload_metadata(co, PreprocessingMetadata(metadata=idx, attributes={"num_sequences": nseq}))
+    co.fetch()
+    slices = co.partition(ffa.partition_chunks_strategy, num_chunks=23)
+    monkeypatch.setattr(ffa, "GET_MANY_GROUP_BYTES", 20_000)
+    calls = _counting(co.storage)
+    got = get_slices(slices, threads=4)
+    n_batched = len(calls)
+    calls.clear()
+    assert got == [s.get() for s in slices]
+    assert 5 <= n_batched < len(calls)
+
+
+def test_force_refreshes_attributes(server, sample, stub_scan):
+    """Deliberate deviation: after preprocess(force=True) the in-memory attributes are the
+    ones just stored.  The reference's preprocess ends with self.fetch() (cloudobject.py:248), which skips
+    _fetch_metadata while _meta_headers is set (:176-178), so a forced re-index of an indexed object keeps
+    the previous namedtuple; the stored index and attrs are the same either way."""
+    data, exp = sample
+    co = _upload(server, data, "force_attrs.fasta")
+    co.preprocess(chunk_size=1500)                               # 1 chunk, the tail dropped (num_chunks = size // cs)
+    first = co.attributes.num_sequences
+    assert first == int(((exp[:, 0] < 1500)).sum()) < 9
+    co.preprocess(chunk_size=-(-len(data) // 4), force=True)     # every byte: all 9 headers
+    stored = pickle.loads(co.storage.get_object(Bucket="genomics.meta", Key="force_attrs.fasta.attrs")["Body"].read())
+    assert stored == {"num_sequences": 9}
+    assert co.attributes.num_sequences == 9                      # the reference would still report `first`
 
 
 def test_get_slices_first_error_in_slice_order():

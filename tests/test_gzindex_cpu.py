@@ -12,6 +12,7 @@ import pytest
 
 from dataplug_amd import gz, synth
 from dataplug_amd.scan import gzindex
+from dataplug_amd.scan._lib import DPCapacityError
 from oracle import cpu_ref
 
 
@@ -25,9 +26,11 @@ class _Buf:
 class OracleCtx:
     """The few ScanContext calls gzindex makes; the scan is cpu_ref.delim_index over the 'device' bytes."""
 
-    def __init__(self):
+    def __init__(self, enforce_cap=False):
         self.mem = {}
         self.out = None
+        self.enforce_cap = enforce_cap
+        self.cap = None
 
     def pinned(self, name, n):
         b = _Buf(n)
@@ -55,9 +58,17 @@ class OracleCtx:
         g = np.arange(len(pos), dtype=np.int64) + carry
         sel = pos[(g % k) == k - 1] + np.uint64(add)
         self.out = (sel, len(pos))
+        self.cap = cap
+        if self.enforce_cap:                      # the device writes at most cap entries (DP_ERR_CAPACITY)
+            d, j = self._at(d_out)
+            assert j + 8 * cap <= len(d), "output buffer smaller than its capacity"
 
     def delim_ranges_result(self, nranges):
         sel, nd = self.out
+        if self.enforce_cap and len(sel) > self.cap:
+            e = DPCapacityError(3, f"output capacity below {len(sel)} entries")
+            e.needed = len(sel)
+            raise e
         return len(sel), nd, np.array([nd], np.uint64)
 
     def d2h(self, out, src):
@@ -188,3 +199,49 @@ def test_preprocess_gzip_then_read_batches(monkeypatch, kind):
     for nb in (1, 7, 33):
         got = [ln for b in co.partition(ffq.partition_reads_batches, num_batches=nb) for ln in b.get()]
         assert got == lines
+
+
+@pytest.mark.parametrize("k", [1, 4])
+def test_piece_of_empty_lines_fits_the_read_end_capacity(k):
+    """A piece that is almost all newlines (FASTQ with empty sequence lines, or blank text lines) has one
+    read end per k bytes: the device output is sized for that bound, checked by a stand-in
+    that enforces the capacity the pipeline passes, as the device does."""
+    raw = (b"@\n\n+\n\n" * 3000) + b"\n" * 20000 + synth.fastq(200, seed=2).tobytes()
+    blob = gzip.compress(raw)
+    ctx = OracleCtx(enforce_cap=True)
+    ix = gzindex.index_stream(ctx, _reader(blob, 4096), record_lines=k, span=1 << 15, piece_bytes=1 << 14,
+                              threads=1)
+    _check(ix, raw, blob, k, 1 << 15, bgzf=False)
+
+
+def test_bgzf_long_zero_padding_does_not_spin():
+    """More than a batch of zero padding between BGZF members: the padding is dropped and the stream read
+    on (it used to rescan the same buffer forever)."""
+    raw = synth.fastq(2000, seed=5).tobytes()
+    half = len(raw) // 2
+    blob = synth.bgzf(raw[:half], block=65_280)
+    eof_marker = blob[-28:]                      # the empty BGZF member that ends a BGZF file
+    blob = blob[:-28] + bytes(gzindex.BGZF_BATCH + 12345) + synth.bgzf(raw[half:], block=65_280)
+    assert eof_marker == blob[-28:]
+    ix = gzindex.index_stream(OracleCtx(), _reader(blob, 1 << 20), span=1 << 18, piece_bytes=1 << 17, threads=2)
+    assert ix.bgzf
+    ends = np.frombuffer(ix.ends.read(), "<u8")
+    nl = np.flatnonzero(np.frombuffer(raw, np.uint8) == 10).astype(np.uint64)
+    assert np.array_equal(ends, nl[3::4] + np.uint64(1))
+
+
+def test_reader_error_surfaces_from_parallel_inflate():
+    """A GET body that fails mid-stream: the error reaches the caller (no hang in the reader thread)."""
+    raw = synth.fastq(20_000, seed=9).tobytes()
+    blob = gzip.compress(raw)
+    f = io.BytesIO(blob)
+    calls = [0]
+
+    def read(n):
+        calls[0] += 1
+        if calls[0] > 2:
+            raise ConnectionError("body reset")
+        return f.read(min(n, 50_000))
+
+    with pytest.raises(ConnectionError):
+        gzindex.index_stream(OracleCtx(), read, span=1 << 15, piece_bytes=1 << 16, threads=4, region_bytes=4096)

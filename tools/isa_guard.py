@@ -1,4 +1,4 @@
-"""ISA guard for the hand-waited input loads of scan_kernel (dataplug_amd/csrc/dpscan.hip).
+"""ISA guard for the hand-waited input loads of scan_kernel and fasta_map_kernel (dataplug_amd/csrc/dpscan.hip).
 
 The data waves issue their buffer loads as inline asm and wait with one explicit `s_waitcnt vmcnt(N)` per
 buffer, N = the loads of the buffers still in flight.  The compiler knows nothing about that contract, so
@@ -19,7 +19,7 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "dataplug_amd", "csrc", "dpscan.hip")
-KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_111scan_kernelILi[01]ELi[012]EE\w*):", re.M)
+KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1(?:11scan_kernelILi[01]ELi[012]EE|16fasta_map_kernel)\w*):", re.M)
 
 
 def compile_asm() -> str:
@@ -135,7 +135,7 @@ def check(asm_path: str):
     text = open(asm_path).read()
     problems = []
     kernels = KERNEL_RE.findall(text)
-    assert len(kernels) == 5, kernels
+    assert len(kernels) == 6, kernels
     for k in kernels:
         body = text[text.index(k + ":") + len(k) + 1:]
         body = body[:body.index(".Lfunc_end")]
@@ -163,7 +163,7 @@ def scratch(asm_path: str):
     text = open(asm_path).read()
     out = []
     for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, re.S):
-        if "scan_kernel" not in m.group(1):
+        if "scan_kernel" not in m.group(1) and "fasta_map_kernel" not in m.group(1):
             continue
         sz = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(2))
         if sz and int(sz.group(1)) > 0:
