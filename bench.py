@@ -374,18 +374,27 @@ def load_traffic(args, size, kernel):
 
 
 # ------------------------------------------------------------------------------------------ FASTA
+# The FASTA index is two kernels (libdpscan: the map over 16 KiB ranges, then the placement); their HIP-event
+# span is one "launch" (DP_FASTA_ONEPASS=1: round 2's one-pass look-back kernel, for A/B runs)
+_ONEPASS = os.environ.get("DP_FASTA_ONEPASS", "0") not in ("", "0")
+FASTA_KERNEL = "scan_kernel<FASTA>" if _ONEPASS else "fasta_map_kernel + fasta_place_kernel (one HIP-event span)"
+FASTA_PMC_KERNELS = "scan_kernel<0" if _ONEPASS else "fasta_map_kernel,fasta_place_kernel"
+
+
 class FastaSpec:
-    """One FASTA object and its chunk plan, split over n workers (scan.objects.fasta_groups)."""
+    """One FASTA object and its chunk plan, split over n workers by the product's split
+    (scan.objects.fasta_split: byte-balanced groups, chunks cut where a group boundary falls inside one).
+    ``scan_plan`` holds the launch chunks (whole chunks, or pieces of cut ones)."""
 
     def __init__(self, size: int, chunks_total: int, n_workers: int, seed: int = 1):
         from dataplug_amd import synth
-        from dataplug_amd.scan.objects import fasta_groups
+        from dataplug_amd.scan.objects import fasta_split
         self.size = size
         self.chunk_size = math.ceil(size / chunks_total)
         n = size // self.chunk_size
         self.plan = [(i * self.chunk_size, size if self.chunk_size == n - 1 else (i + 1) * self.chunk_size)
                      for i in range(n)]
-        self.groups = fasta_groups(self.plan, n_workers, size)
+        self.pieces, self.scan_plan, self.groups = fasta_split(self.plan, n_workers, size)
         self.obj = synth.TiledFasta(size, seed=seed)
         # the reference's uint32 index holds every offset < 2^32 (ends <= size; the synthetic object never
         # ends inside a header line); larger objects need the opt-in uint64 index (index_dtype="uint64")
@@ -397,14 +406,14 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
     out = {"worker": k, "device": dev}
     ctxs = (ScanContext(dev), ScanContext(dev))
 
-    def prepare(sp: FastaSpec, tag: str):
-        if k >= len(sp.groups):
+    def prepare(sp: FastaSpec, tag: str, gi: int):
+        if gi >= len(sp.groups):
             return None
-        g = sp.groups[k]
+        g = sp.groups[gi]
         host = sp.obj.bytes_range(g.lo, g.buf_hi)
         d_in = ctxs[0].workspace(f"in_{tag}", len(host) + 64)
         ctxs[0].h2d(d_in.ptr, host)
-        chunks = np.ascontiguousarray(np.asarray(g.chunks(sp.plan), np.uint64).reshape(-1))
+        chunks = np.ascontiguousarray(np.asarray(g.chunks(sp.scan_plan), np.uint64).reshape(-1))
         nch = len(chunks) // 2
         cap = (g.hi - g.lo) // 256 + 1024
         osz = 2 * cap * (8 if sp.u64 else 4)
@@ -417,7 +426,7 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
         def collect(i):
             return ctxs[i % 2].fasta_result(nch)
 
-        scanned = sum(c1 - c0 for c0, c1 in g.chunks(sp.plan))
+        scanned = sum(p.b - p.a for p in sp.pieces[g.i0:g.i1])         # the plan's bytes (not the overlap byte)
         return {"g": g, "host": host, "d_in": d_in, "d_outs": d_outs, "steps": Steps(team, ctxs, launch, collect),
                 "scanned": scanned, "chunks": chunks}
 
@@ -427,15 +436,15 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
             return None
         from oracle import dpref          # the checker (test infrastructure), outside every timed region
         g = st["g"]
-        rel = [(c0 - g.lo, c1 - g.lo) for c0, c1 in g.chunks(sp.plan)]
+        rel = [(c0 - g.lo, c1 - g.lo) for c0, c1 in g.chunks(sp.scan_plan)]
         exp = dpref.fasta_pairs(st["host"], rel)
         got = np.empty((n_pairs, 2), np.uint64 if sp.u64 else np.uint32)
         ctxs[0].d2h(got, st["d_outs"][i_last % 2].ptr)
         return bool((pending == -1).all() and np.array_equal(got.astype(np.uint64) - np.uint64(g.lo), exp))
 
     t0 = time.perf_counter()
-    st = prepare(spec, "main")
-    ss = prepare(strong, "strong") if strong is not None else None
+    st = prepare(spec, "main", 0)                     # weak: this worker's own configs[1] object
+    ss = prepare(strong, "strong", k) if strong is not None else None
     out["gen_s"] = time.perf_counter() - t0
     team.barrier()                    # every worker's uploads are done before any scan (shared-GPU rehearsals)
     S = st["steps"]
@@ -467,12 +476,14 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
 
 def main_fasta(args, world, rank, devs, team):
     per_gpu = args.size or (4 << 30)
-    size = per_gpu * world
-    spec = FastaSpec(size, args.chunks * world, world)
+    size = per_gpu
+    # weak: every GPU indexes its own configs[1] object (the reference's plan, chunk_size = size / 4, uint32
+    # index) -- N x the N = 1 workload; strong: ONE such object cut over the N GPUs by the product's split
+    spec = FastaSpec(size, args.chunks, 1)
     strong = None
     if world > 1 and not args.no_strong:
-        strong = FastaSpec(per_gpu, args.chunks * world, world)
-    log(f"{world} GPU(s): one {size / GiB:g} GiB FASTA, {len(spec.plan)} chunks of {spec.chunk_size} B, "
+        strong = FastaSpec(per_gpu, args.chunks, world)
+    log(f"{world} GPU(s): a {size / GiB:g} GiB FASTA per GPU, {len(spec.plan)} chunks of {spec.chunk_size} B, "
         f"{'uint64' if spec.u64 else 'uint32'} index, devices {devs} (rank {rank})")
     keep = world == 1 and not args.no_cpu_baseline
     res = run_workers(lambda k, d: fasta_worker(args, team, spec, strong, k, d, keep), devs, rank * len(devs), team)
@@ -492,7 +503,7 @@ def main_fasta(args, world, rank, devs, team):
     peak_meas = min(r["stream_peak"] for r in allres)
     verified = None if args.no_verify else all(r["verified"] for r in allres)
     cpu = cpu_baseline(host, spec.chunk_size) if host is not None else None
-    traffic, traffic_src = load_traffic(args, per_gpu, "scan_kernel<0") if world == 1 else (None, None)
+    traffic, traffic_src = load_traffic(args, per_gpu, FASTA_PMC_KERNELS) if world == 1 else (None, None)
     strong_out = None
     if strong is not None:
         sr = [r["strong"] for r in allres if "strong" in r]
@@ -502,8 +513,11 @@ def main_fasta(args, world, rank, devs, team):
                       "chunks": len(strong.plan), "gpus_used": len(sr),
                       "kernel_avg_us_max": round(max(r["kern_s"] for r in sr) * 1e6, 2),
                       "verified_bit_exact": None if args.no_verify else all(r["verified"] for r in sr),
-                      "note": "fixed total: the configs[1] 4 GiB object, chunk plan size/(4N), split over the "
-                              "same N GPUs (strong scaling point of SURVEY.md §8(e))"}
+                      "pieces": len(strong.pieces), "cut_chunks": sum(not p.first for p in strong.pieces),
+                      "note": "fixed total: ONE configs[1] 4 GiB object with the caller's plan (chunk_size = "
+                              "size/4) cut into byte-balanced groups over the same N GPUs by the product split "
+                              "(scan.objects.fasta_split; chunks cut where a group boundary falls inside one) "
+                              "-- the strong scaling point of SURVEY.md §8(e)"}
     r0 = allres[0]
     out = {
         "metric": "GiB/s scanned (device-resident) + offsets/s, FASTA index at 1/2/4/8 MI355X",
@@ -518,14 +532,14 @@ def main_fasta(args, world, rank, devs, team):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": f"FASTA '>' header index of ONE {size / GiB:g} GiB synthetic object "
-                               f"({per_gpu / GiB:g} GiB per GPU), chunk_size={spec.chunk_size} "
-                               f"(= size/{len(spec.plan)}; BASELINE configs[1] at N=1)",
-                   "object_bytes": size, "chunks": len(spec.plan), "pairs": int(pairs),
+        "config": {"workload": f"FASTA '>' header index of a {size / GiB:g} GiB synthetic object per GPU "
+                               f"(BASELINE configs[1]: chunk_size={spec.chunk_size} = size/{len(spec.plan)}), "
+                               f"{world} object(s)",
+                   "object_bytes": size, "objects": world, "chunks": len(spec.plan), "pairs": int(pairs),
                    "index_dtype": "uint64" if spec.u64 else "uint32",
-                   "parallelism": f"contiguous chunk groups x{world} (scan.objects.fasta_groups), "
+                   "parallelism": f"independent objects x{world}, "
                                   f"{'one rank per GPU (gloo for barriers)' if team.pg is not None else 'one host thread per GPU'}, "
-                                  f"no collective"},
+                                  f"no collective; one object over N GPUs: the `strong` point"},
         "offsets_per_s": round(2.0 * pairs * K / dt, 1),
         "timing": "pipelined" if pipelined else "serialized",
         "serialized": {"value": round(scanned * K / dt_ser / GiB, 3), "unit": "GiB/s",
@@ -536,8 +550,9 @@ def main_fasta(args, world, rank, devs, team):
         "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
                      "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
-                     "kernel": "scan_kernel<FASTA>", "kernel_avg_us": round(kern * 1e6, 2),
+                     "kernel": FASTA_KERNEL, "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(r0["alg_bytes"]),
+                     "alg_bytes_def": "N + 8 * H (N chunk bytes read once, H headers x two uint32 offsets)",
                      "measured_peak": round(peak_meas / 1e9, 1),
                      "frac_of_measured_peak": round(ach / peak_meas, 4),
                      "note": "per GPU (the slowest GPU's algorithmic bytes / its average scan launch); "

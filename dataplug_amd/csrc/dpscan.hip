@@ -33,6 +33,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -1958,15 +1959,16 @@ int fail(int code, const std::string& msg) {
 
 }  // namespace
 
-// One persistent scan grid at a time per device.  The look-back assumes every workgroup of a grid is
-// resident; two grids launched at the same moment from different streams (one process indexing several
-// objects or chunk groups on one GPU, e.g. DATAPLUG_AMD_DEVICES=0,0,0) could split the CUs between them and
-// wait on each other's unscheduled workgroups.  So a scan launch on a ctx stream first waits (on the device,
-// no host sync) for the last scan launched on that device from any other stream.
+// One scan stream per device, owned by the library.  Every scan launch of every context on a device goes
+// to it, in call order: one grid fills the chip, so two scans side by side would only split the CUs, and
+// a process then holds at most one scan stream per device (GPU_MAX_HW_QUEUES is 4 on the box; four or more
+// context streams each launching scans and waiting on one another's events were seen to stall a scan for
+// ~0.5 s).  A launch hands over with two events: the scan stream waits for the context
+// stream's earlier work (table upload, input copies), the context stream waits for the scan (resolve
+// kernel, read-back); the scan's HIP timing events sit on the scan stream around the kernels alone.
 struct DeviceSerial {
   std::mutex m;
-  hipEvent_t last = nullptr;          // completion of the device's last scan (owned by that ctx)
-  hipStream_t last_stream = nullptr;
+  hipStream_t scan = nullptr;         // created on the device's first scan, kept for the process
 };
 constexpr int kMaxDevices = 64;
 DeviceSerial g_serial[kMaxDevices];
@@ -2003,26 +2005,39 @@ struct dp_ctx {
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_order = nullptr;      // dp_ctx_wait: device-scope ordering event on this ctx's stream
-  hipEvent_t ev_scan = nullptr;       // end of this ctx's last scan launch (DeviceSerial)
+  hipEvent_t ev_in = nullptr;         // ctx stream -> device scan stream hand-over (DeviceSerial)
+  hipEvent_t ev_out = nullptr;        // device scan stream -> ctx stream
   size_t ev_used = 0;
   double ms_acc = 0.0;
   uint64_t launches = 0;
 };
 
+std::atomic<uint64_t> g_dev_allocs{0}, g_host_allocs{0};
+
 namespace {
+
+// Every device / pinned host allocation the library makes goes through these (dp_alloc_counts).
+hipError_t dev_alloc(void** p, uint64_t bytes) {
+  g_dev_allocs.fetch_add(1, std::memory_order_relaxed);
+  return hipMalloc(p, bytes);
+}
+hipError_t host_alloc(void** p, uint64_t bytes) {
+  g_host_allocs.fetch_add(1, std::memory_order_relaxed);
+  return hipHostMalloc(p, bytes, hipHostMallocDefault);
+}
 
 int ensure_tab(dp_ctx* c, uint64_t words) {
   if (words > c->tab_cap) {
     if (c->d_tab) HIPCHK(hipFree(c->d_tab));
     uint64_t cap = words + words / 2 + 64;
-    HIPCHK(hipMalloc(&c->d_tab, cap * 8));
+    HIPCHK(dev_alloc((void**)&c->d_tab, cap * 8));
     c->tab_cap = cap;
     c->last_tab.clear();   // forces a full upload (table + control words) before the next scan
   }
   if (words > c->h_cap) {
     if (c->h_tab) HIPCHK(hipHostFree(c->h_tab));
     uint64_t cap = words + words / 2 + 64;
-    HIPCHK(hipHostMalloc(&c->h_tab, cap * 8, hipHostMallocDefault));
+    HIPCHK(host_alloc((void**)&c->h_tab, cap * 8));
     c->h_cap = cap;
   }
   return DP_OK;
@@ -2031,13 +2046,13 @@ int ensure_desc(dp_ctx* c, uint64_t n) {
   if (n > c->desc_cap) {
     if (c->d_desc) HIPCHK(hipFree(c->d_desc));
     uint64_t cap = ((n + n / 4 + 1023) / 1024) * 1024;
-    HIPCHK(hipMalloc(&c->d_desc, cap * 8));
+    HIPCHK(dev_alloc((void**)&c->d_desc, cap * 8));
     c->desc_cap = cap;
     c->desc_epoch = 0;
   }
   return DP_OK;
 }
-int ev_begin(dp_ctx* c, hipEvent_t* e0) {
+int ev_begin(dp_ctx* c, hipEvent_t* e0, hipStream_t s) {
   if (!c->timing) return DP_OK;
   while (c->ev_pool.size() < c->ev_used + 2) {
     hipEvent_t e;
@@ -2047,12 +2062,12 @@ int ev_begin(dp_ctx* c, hipEvent_t* e0) {
     c->ev_pool.push_back(e);
   }
   *e0 = c->ev_pool[c->ev_used];
-  HIPCHK(hipEventRecord(*e0, c->stream));
+  HIPCHK(hipEventRecord(*e0, s));
   return DP_OK;
 }
-int ev_end(dp_ctx* c) {
+int ev_end(dp_ctx* c, hipStream_t s) {
   if (!c->timing) return DP_OK;
-  HIPCHK(hipEventRecord(c->ev_pool[c->ev_used + 1], c->stream));
+  HIPCHK(hipEventRecord(c->ev_pool[c->ev_used + 1], s));
   c->ev_used += 2;
   return DP_OK;
 }
@@ -2110,6 +2125,24 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
   return DP_OK;
 }
 
+// Hand a scan over to the device's scan stream (caller holds ds.m): the scan stream waits for everything
+// enqueued on the ctx stream so far.  scan_leave: the ctx stream waits for the scan.  Both events keep the
+// default system-scope release: the input arrives by DMA and the read-back leaves by DMA.
+int scan_enter(dp_ctx* c, DeviceSerial& ds, hipStream_t* ss) {
+  if (!ds.scan) HIPCHK(hipStreamCreateWithFlags(&ds.scan, hipStreamNonBlocking));
+  if (!c->ev_in) HIPCHK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+  if (!c->ev_out) HIPCHK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(c->ev_in, c->stream));
+  HIPCHK(hipStreamWaitEvent(ds.scan, c->ev_in, 0));
+  *ss = ds.scan;
+  return DP_OK;
+}
+int scan_leave(dp_ctx* c, hipStream_t ss) {
+  HIPCHK(hipEventRecord(c->ev_out, ss));
+  HIPCHK(hipStreamWaitEvent(c->stream, c->ev_out, 0));
+  return DP_OK;
+}
+
 int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t units,
                 void* d_out, int out_u64, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add,
                 uint64_t carry = 0, uint32_t wrap32 = 0, unsigned long long* blocktab = nullptr, uint64_t tab_j0 = 0,
@@ -2155,31 +2188,29 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
   DeviceSerial& ds = g_serial[c->device];
   std::lock_guard<std::mutex> lock(ds.m);
-  if (ds.last && ds.last_stream != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, ds.last, 0));
-  if (!c->ev_scan) HIPCHK(hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming | hipEventReleaseToDevice));
+  hipStream_t ss = nullptr;
+  rc = scan_enter(c, ds, &ss);
+  if (rc) return rc;
   hipEvent_t e0;
-  rc = ev_begin(c, &e0);
+  rc = ev_begin(c, &e0, ss);
   if (rc) return rc;
   const uint64_t* tlo = c->d_tab;
   const uint64_t* thi = c->d_tab + n;
   const uint64_t* tu0 = c->d_tab + 2 * n;
   if (mode == kFasta && !out_u64)
-    hipLaunchKernelGGL((scan_kernel<kFasta, 0>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+    hipLaunchKernelGGL((scan_kernel<kFasta, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else if (mode == kFasta)
-    hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+    hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else if (out_u64 == 2)
-    hipLaunchKernelGGL((scan_kernel<kDelim, 2>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+    hipLaunchKernelGGL((scan_kernel<kDelim, 2>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else if (!out_u64)
-    hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+    hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else
-    hipLaunchKernelGGL((scan_kernel<kDelim, 1>), dim3(grid), dim3(kThreads), 0, c->stream, a, tlo, thi, tu0);
+    hipLaunchKernelGGL((scan_kernel<kDelim, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   HIPCHK(hipGetLastError());
-  rc = ev_end(c);
+  rc = ev_end(c, ss);
   if (rc) return rc;
-  HIPCHK(hipEventRecord(c->ev_scan, c->stream));
-  ds.last = c->ev_scan;
-  ds.last_stream = c->stream;
-  return DP_OK;
+  return scan_leave(c, ss);
 }
 
 // The two-kernel FASTA index (fasta_map_kernel + fasta_place_kernel) over a chunk table staged with
@@ -2196,8 +2227,8 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
     c->d_spill = nullptr;
     c->rec_cap = 0;
     const uint64_t cap_r = nranges + nranges / 8 + 64;
-    HIPCHK(hipMalloc(&c->d_rec, cap_r * sizeof(uint4)));
-    HIPCHK(hipMalloc(&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t)));
+    HIPCHK(dev_alloc((void**)&c->d_rec, cap_r * sizeof(uint4)));
+    HIPCHK(dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t)));
     c->rec_cap = cap_r;
   }
   const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
@@ -2249,26 +2280,24 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   const uint64_t* tr0 = c->d_tab + 2 * n;
   DeviceSerial& ds = g_serial[c->device];
   std::lock_guard<std::mutex> lock(ds.m);
-  if (ds.last && ds.last_stream != c->stream) HIPCHK(hipStreamWaitEvent(c->stream, ds.last, 0));
-  if (!c->ev_scan) HIPCHK(hipEventCreateWithFlags(&c->ev_scan, hipEventDisableTiming | hipEventReleaseToDevice));
-  hipEvent_t e0;
-  rc = ev_begin(c, &e0);
+  hipStream_t ss = nullptr;
+  rc = scan_enter(c, ds, &ss);
   if (rc) return rc;
-  hipLaunchKernelGGL(fasta_map_kernel, dim3(grid), dim3(kWave * kMapWaves), 0, c->stream, m, tlo, thi, tr0);
+  hipEvent_t e0;
+  rc = ev_begin(c, &e0, ss);
+  if (rc) return rc;
+  hipLaunchKernelGGL(fasta_map_kernel, dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   if (out_u64)
-    hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, c->stream, pa, a, tlo,
+    hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
                        thi, tr0);
   else
-    hipLaunchKernelGGL((fasta_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, c->stream, pa, a, tlo,
+    hipLaunchKernelGGL((fasta_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
                        thi, tr0);
   HIPCHK(hipGetLastError());
-  rc = ev_end(c);
+  rc = ev_end(c, ss);
   if (rc) return rc;
-  HIPCHK(hipEventRecord(c->ev_scan, c->stream));
-  ds.last = c->ev_scan;
-  ds.last_stream = c->stream;
-  return DP_OK;
+  return scan_leave(c, ss);
 }
 
 int check_ctx(dp_ctx* c) {
@@ -2351,14 +2380,8 @@ int dp_ctx_destroy(dp_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_order) (void)hipEventDestroy(c->ev_order);
-  if (c->ev_scan) {
-    std::lock_guard<std::mutex> lock(g_serial[c->device].m);
-    if (g_serial[c->device].last == c->ev_scan) {
-      g_serial[c->device].last = nullptr;
-      g_serial[c->device].last_stream = nullptr;
-    }
-    (void)hipEventDestroy(c->ev_scan);
-  }
+  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->d_rec) (void)hipFree(c->d_rec);
   if (c->d_spill) (void)hipFree(c->d_spill);
@@ -2403,7 +2426,7 @@ int dp_malloc(dp_ctx* c, uint64_t bytes, void** p) {
   int rc = check_ctx(c);
   if (rc) return rc;
   if (!p) return fail(DP_ERR_INVALID, "null");
-  HIPCHK(hipMalloc(p, bytes ? bytes : 16));
+  HIPCHK(dev_alloc(p, bytes ? bytes : 16));
   return DP_OK;
 }
 
@@ -2416,7 +2439,7 @@ int dp_free(dp_ctx* c, void* p) {
 
 int dp_host_alloc(uint64_t bytes, void** p) {
   if (!p) return fail(DP_ERR_INVALID, "null");
-  HIPCHK(hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocDefault));
+  HIPCHK(host_alloc(p, bytes ? bytes : 16));
   return DP_OK;
 }
 
@@ -2674,13 +2697,13 @@ int dp_stream_rw(dp_ctx* c, const void* d_in, uint64_t bytes, void* d_out, uint3
   const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 1;
   c->last_tab.clear();   // the table area is the (practically never written) sink
   hipEvent_t e0;
-  rc = ev_begin(c, &e0);
+  rc = ev_begin(c, &e0, c->stream);
   if (rc) return rc;
   hipLaunchKernelGGL(stream_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, c->stream,
                      reinterpret_cast<const uint4*>(d_in), bytes / 16, write_q16 ? reinterpret_cast<uint4*>(d_out) : nullptr,
                      (uint64_t)write_q16, reinterpret_cast<unsigned*>(c->d_tab));
   HIPCHK(hipGetLastError());
-  return ev_end(c);
+  return ev_end(c, c->stream);
 }
 
 int dp_stream_read(dp_ctx* c, const void* d_buf, uint64_t bytes, int blocks_per_cu) {
@@ -2721,6 +2744,12 @@ int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slo
   (void)c; (void)host_words; (void)n_words; (void)slots; (void)waves;
   return fail(DP_ERR_INVALID, "dp_debug_profile: library built without -DDP_PROF");
 #endif
+}
+
+int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs) {
+  if (device_allocs) *device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
+  if (host_allocs) *host_allocs = g_host_allocs.load(std::memory_order_relaxed);
+  return DP_OK;
 }
 
 int dp_scan_geometry(dp_ctx* c, int* grid, int* unit_bytes) {

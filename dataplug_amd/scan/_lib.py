@@ -59,6 +59,7 @@ SIGNATURES = [
     ("dp_timing_enable", _c.c_int, [_p, _c.c_int]),
     ("dp_timing_read", _c.c_int, [_p, _c.POINTER(_c.c_double), _u64p]),
     ("dp_debug_profile", _c.c_int, [_p, _u64p, _u64, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
+    ("dp_alloc_counts", _c.c_int, [_u64p, _u64p]),
     ("dp_scan_geometry", _c.c_int, [_p, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
 ]
 
@@ -109,6 +110,13 @@ def check(rc: int) -> None:
     if rc == DP_ERR_CAPACITY:
         raise DPCapacityError(rc, msg)
     raise DPScanError(rc, msg)
+
+
+def alloc_counts():
+    """(device allocations, pinned host allocations) libdpscan has made in this process (dp_alloc_counts)."""
+    d, h = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(load().dp_alloc_counts(ctypes.byref(d), ctypes.byref(h)))
+    return int(d.value), int(h.value)
 
 
 def device_count() -> int:

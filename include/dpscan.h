@@ -6,10 +6,11 @@
  * the message of the last failure on the calling thread is available from dp_last_error().  No C++
  * exception crosses this boundary.  A dp_ctx is bound to one device and owns one stream plus the
  * scan workspace; use one ctx per host thread (calls on distinct ctx are thread-safe, and ctypes
- * releases the GIL around them).  Scan kernels of different ctx on one device (in one process) run one
- * after another (each launch waits on the device for the previous one: one grid fills the chip).  The
- * persistent grid's workgroups claim their units from a ticket at run time, so a grid never waits on a
- * workgroup that has not started: grids of different processes may share a GPU.
+ * releases the GIL around them).  Scan kernels of every ctx on one device (in one process) run one after
+ * another on one library-owned scan stream per device (one grid fills the chip); each scan call hands
+ * over from the ctx stream to that stream and back with an event, so the ctx stream sees the results in
+ * order.  Workgroups that depend on one another claim their work from a ticket at run time, so a grid
+ * never waits on a workgroup that has not started: grids of different processes may share a GPU.
  *
  * Reference interfaces each entry point replaces (CLOUDLAB-URV/dataplug @ 2025-07-11):
  *   dp_fasta_index  <- dataplug/formats/genomics/fasta.py:24-63 (preprocess_fasta: the per-chunk
@@ -140,7 +141,9 @@ int dp_find_delim(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t 
 int dp_stream_read(dp_ctx* ctx, const void* d_buf, uint64_t bytes, int blocks_per_cu);
 int dp_stream_rw(dp_ctx* ctx, const void* d_in, uint64_t bytes, void* d_out, uint32_t write_q16, int blocks_per_cu);
 
-/* Kernel timing: HIP events around every scan-kernel launch on the ctx stream (off by default). */
+/* Kernel timing (off by default): HIP events around every scan launch -- on the device's scan stream,
+ * around the scan's kernels alone (FASTA: the map and placement kernels as one span) -- and around the
+ * calibration kernels on the ctx stream. */
 int dp_timing_enable(dp_ctx* ctx, int enable);
 int dp_timing_read(dp_ctx* ctx, double* total_ms, uint64_t* launches);   /* syncs; then resets */
 
@@ -148,6 +151,11 @@ int dp_timing_read(dp_ctx* ctx, double* total_ms, uint64_t* launches);   /* sync
  * `slots` words per wave, `waves` waves per workgroup).  Only a library built with -DDP_PROF
  * (lib/libdpscan_prof.so) records them; the production build returns DP_ERR_INVALID. */
 int dp_debug_profile(dp_ctx* ctx, uint64_t* host_words, uint64_t n_words, int* slots, int* waves);
+
+/* Device (hipMalloc) and pinned host (hipHostMalloc) allocations the library has made in this process so
+ * far: dp_malloc / dp_host_alloc and every context's own workspace (chunk table, look-back descriptors,
+ * FASTA range summaries and spill).  Steady-state calls on warm contexts allocate nothing. */
+int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
 
 /* Launch geometry (for tests/tuning): workgroups of the persistent scan grid, and unit size in bytes. */
 int dp_scan_geometry(dp_ctx* ctx, int* grid, int* unit_bytes);

@@ -1,6 +1,7 @@
 """N>1 path on CPU: two ranks over gloo (127.0.0.1), driven through bench.py's own Team / FastaSpec.  Ranks
-get disjoint contiguous chunk groups of one object from the product split (scan.objects.fasta_groups), the
-per-rank outputs gathered in rank order equal the single-process index."""
+get disjoint byte-balanced groups of one object from the product split (scan.objects.fasta_split, a chunk
+cut where the group boundary falls inside it); the per-rank outputs gathered in rank order and stitched
+(scan.objects.stitch_pieces) equal the single-process index."""
 import os
 import socket
 import subprocess
@@ -63,19 +64,25 @@ WORKER = textwrap.dedent("""
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     team = bench.Team(1, dist)                      # what bench.py builds under torch.distributed.run
-    # bench.py's FASTA workload: one object, chunk plan size/(4N), the product's group split
-    # (scan.objects.fasta_groups); this rank materializes only its group + halo, as a bench rank does
-    spec = bench.FastaSpec({size}, 4 * world, world, seed=3)
+    # bench.py's strong point: ONE object with the caller's plan (chunk_size = size/4) over the ranks by the
+    # product split (scan.objects.fasta_split); this rank materializes only its group + halo, as a bench
+    # rank does.  The GPU scan of each launch chunk stands in as the oracle over the same bytes (no GPU here)
+    spec = bench.FastaSpec({size}, 4, world, seed=3)
     g = spec.groups[rank]
     host = spec.obj.bytes_range(g.lo, g.buf_hi)
-    rel = [(c0 - g.lo, c1 - g.lo) for c0, c1 in g.chunks(spec.plan)]
-    # the GPU scan of the group stands in as the oracle over the same bytes (no GPU here)
-    mine = (dpref.fasta_pairs(host, rel) + np.uint64(g.lo)).tolist()
+    mine, first_nl = [], {{}}
+    for k in range(g.i0, g.i1):
+        p = spec.pieces[k]
+        mine.append((dpref.fasta_pairs(host, [(p.a - g.lo, p.end - g.lo)]) + np.uint64(g.lo)).tolist())
+        if not p.first:
+            nl = np.flatnonzero(host[p.a - g.lo:p.end - g.lo] == 10)
+            first_nl[k] = int(p.a + nl[0]) if len(nl) else None
     team.barrier()
     tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
     lo, hi = rank_byte_range(len(tv.head), tv.size, rank, world)
     nl = np.concatenate(list(tv.delims_range(lo, hi))).tolist()
-    allres = team.gather([{{"rank": rank, "group": [g.i0, g.i1, g.lo, g.hi, g.buf_hi], "pairs": mine, "nl": nl}}])
+    allres = team.gather([{{"rank": rank, "group": [g.i0, g.i1, g.lo, g.hi, g.buf_hi], "pairs": mine,
+                            "first_nl": first_nl, "nl": nl}}])
     if allres is not None:
         with open(os.path.join({tmp!r}, "gathered.json"), "w") as f:
             json.dump(allres, f)
@@ -84,9 +91,9 @@ WORKER = textwrap.dedent("""
 
 
 def test_two_rank_gloo(tmp_path):
-    """Two ranks over gloo, as bench.py runs under torch.distributed.run: each takes its chunk group of ONE
-    object from the product's split, the gather reaches rank 0 in rank order, and the groups' pairs
-    concatenate to the whole object's index."""
+    """Two ranks over gloo, as bench.py runs under torch.distributed.run: each takes its group of ONE object
+    from the product's split (the caller's 3-chunk plan over 2 ranks: the middle chunk is cut), the gather
+    reaches rank 0 in rank order, and the groups' pieces stitch to the whole object's index."""
     import json
     from oracle import cpu_ref, dpref
     from dataplug_amd import synth
@@ -101,14 +108,19 @@ def test_two_rank_gloo(tmp_path):
         procs.append(subprocess.Popen([sys.executable, str(script)], env=env, cwd=REPO))
     for p in procs:
         assert p.wait(timeout=240) == 0
+    from dataplug_amd.scan.objects import fasta_split, stitch_pieces
     res = json.load(open(tmp_path / "gathered.json"))
     assert [r["rank"] for r in res] == [0, 1]
     g0, g1 = res[0]["group"], res[1]["group"]
     obj = synth.TiledFasta(size, seed=3).bytes_range(0, size)
-    plan = cpu_ref.chunk_plan(size, -(-size // 8))         # 7 chunks: the tail past 7 * cs is never scanned
-    assert g0[0] == 0 and g0[1] == g1[0] and g1[1] == len(plan) and g0[3] == g1[2]
-    whole = dpref.fasta_pairs(obj, plan).tolist()
-    assert res[0]["pairs"] + res[1]["pairs"] == whole
+    plan = cpu_ref.chunk_plan(size, -(-size // 4))         # 3 chunks: the tail past 3 * cs is never scanned
+    pieces, _, _ = fasta_split(plan, 2, size)
+    assert len(pieces) == 4 and sum(not p.first for p in pieces) == 1
+    assert g0[0] == 0 and g0[1] == g1[0] and g1[1] == len(pieces) and g0[3] in (g1[2], g1[2] + 1)
+    per_piece = [np.asarray(x, np.uint64).reshape(-1, 2) for r in res for x in r["pairs"]]
+    first_nl = {int(k): v for r in res for k, v in r["first_nl"].items()}
+    whole = dpref.fasta_pairs(obj, plan)
+    assert np.array_equal(stitch_pieces(pieces, per_piece, first_nl), whole)
     tv = synth.tiled_vcf(1_000_003, seed=4, block=200_003)
     body_nl = cpu_ref.delim_index(tv.bytes_range(0, tv.size), len(tv.head), tv.size).tolist()
     assert res[0]["nl"] + res[1]["nl"] == body_nl

@@ -298,9 +298,10 @@ def test_fastq_gz_parallel_inflate_on_gpu(threads, region):
 
 # ------------------------------------------------------------------------------------------ multi-GPU split
 def test_bench_thread_mode_split_on_one_gpu(tmp_path):
-    """bench.py --gpus 4 --devices 0,0,0,0: the multi-GPU line's own code (one host thread per GPU, the
-    product's chunk-group split of ONE object, per-group halo) rehearsed on one GPU; every group's index is
-    bit-exact against the oracle (verified_bit_exact) and the strong-scaling point too."""
+    """bench.py --gpus 4 --devices 0,0,0,0: the multi-GPU line's own code (one host thread per GPU, one
+    configs[1]-shaped object per worker; the strong point cuts ONE object's 4-chunk plan over the 4 workers
+    by the product split, per-group halo) rehearsed on one GPU; every launch is bit-exact against the oracle
+    (verified_bit_exact) in both."""
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -310,8 +311,10 @@ def test_bench_thread_mode_split_on_one_gpu(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 4 and line["verified_bit_exact"] is True
-    assert line["config"]["chunks"] == 16 and line["config"]["index_dtype"] == "uint32"
+    assert line["config"]["chunks"] == 4 and line["config"]["objects"] == 4
+    assert line["config"]["index_dtype"] == "uint32"
     assert line["strong"]["verified_bit_exact"] is True and line["strong"]["gpus_used"] == 4
+    assert line["strong"]["chunks"] == 4 and line["strong"]["pieces"] == 4
     assert line["ms_per_step"] * 1e3 >= line["roofline"]["kernel_avg_us"]
 
 

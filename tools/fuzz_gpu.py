@@ -99,22 +99,28 @@ def chunk_size(rng, size):
 
 
 def object_mode(args, rng):
-    """co.preprocess() end to end through storage: random chunk plans split into 1-6 groups on this GPU
-    (dataplug_devices=[0]*g: the multi-GPU split with its 64 KiB halos, header ends past a group's halo
-    resolved from later bytes), sometimes a launch byte budget far below a group (passes of whole chunks),
-    sometimes the per-chunk joblib route; the stored index against the oracle."""
+    """co.preprocess() end to end through storage: random chunk plans (30 % the canonical 1-4 chunk plans)
+    split into 1-9 byte-balanced groups on this GPU (dataplug_devices=[0]*g: the multi-GPU split, chunks cut
+    at group boundaries and stitched, 64 KiB halos, header ends past a group's halo resolved from later
+    bytes), sometimes a launch byte budget far below a group (passes), sometimes the per-chunk joblib route;
+    the stored index against the oracle."""
     from dataplug_amd.cloudobject import CloudObject
     from dataplug_amd.formats.genomics.fasta import FASTA
     from dataplug_amd.storage import MemoryStore
-    stats = {"object_cases": 0, "pairs": 0, "bytes": 0, "groups": {}, "budget_cases": 0, "joblib_cases": 0}
+    stats = {"object_cases": 0, "pairs": 0, "bytes": 0, "groups": {}, "budget_cases": 0, "joblib_cases": 0,
+             "cut_cases": 0, "cuts": 0}
     t0 = last = time.time()
     i = 0
     while time.time() - t0 < args.seconds:
         size = int(math.exp(rng.uniform(math.log(64), math.log(getattr(args, "max_size", 12 << 20)))))
         a = records(rng, size) if rng.random() < 0.7 else runs(rng, size)
         cs = chunk_size(rng, size)
+        if rng.random() < 0.3:                         # the reference's canonical few-chunk plans (fasta_example.py:23)
+            cs = max(1, math.ceil(size / int(rng.integers(1, 5))))
         plan = cpu_ref.chunk_plan(size, cs)
-        groups = int(rng.integers(1, 7))
+        groups = int(rng.integers(1, 10))
+        from dataplug_amd.scan.objects import fasta_split
+        ncut = sum(not p.first for p in fasta_split(plan, groups, size)[0]) if plan else 0
         pc = {"dataplug_devices": [0] * groups}
         if rng.random() < 0.15:
             pc.update({"backend": "threading", "n_jobs": int(rng.integers(1, 5))})
@@ -154,6 +160,9 @@ def object_mode(args, rng):
         stats["pairs"] += len(exp) // 2
         stats["bytes"] += size
         stats["groups"][groups] = stats["groups"].get(groups, 0) + 1
+        if ncut and "backend" not in pc:
+            stats["cut_cases"] += 1
+            stats["cuts"] += ncut
         i += 1
         if time.time() - last > 20:
             last = time.time()

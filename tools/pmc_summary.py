@@ -1,6 +1,6 @@
 """Summarise a tools/profile.sh run into per-launch numbers for one kernel (profiles/<tag>/pmc_summary.json).
 
-    python tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<tag> [--kernel scan_kernel<0>]
+    python tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<tag> [--kernel scan_kernel<0>|fasta_map_kernel,fasta_place_kernel]
 
 Counters are averaged over the kernel's dispatches, summed over the per-XCD/SE rows rocprofv3 reports per
 dispatch.  FETCH_SIZE/WRITE_SIZE are in KB (1024 B); on gfx950 FETCH_SIZE counts half of the wide
@@ -18,12 +18,19 @@ from collections import defaultdict
 
 
 def counters(path: str, kernel: str):
-    per = defaultdict(lambda: defaultdict(float))
-    for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
-        for row in csv.DictReader(open(f)):
-            if kernel in row["Kernel_Name"]:
-                per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
-    return {c: sum(d.values()) / len(d) for c, d in per.items() if d}
+    """Per-dispatch averages of each counter for one kernel name, or the SUM of those averages over a
+    comma-separated list of kernels that make up one launch (the FASTA map + placement kernels)."""
+    out = defaultdict(float)
+    for k in kernel.split(","):
+        per = defaultdict(lambda: defaultdict(float))
+        for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                if k in row["Kernel_Name"]:
+                    per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
+        for c, d in per.items():
+            if d:
+                out[c] += sum(d.values()) / len(d)
+    return dict(out)
 
 
 def main():
