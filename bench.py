@@ -377,8 +377,8 @@ def load_traffic(args, size, kernel):
 # The FASTA index is two kernels (libdpscan: the map over 16 KiB ranges, then the placement); their HIP-event
 # span is one "launch" (DP_FASTA_ONEPASS=1: round 2's one-pass look-back kernel, for A/B runs)
 _ONEPASS = os.environ.get("DP_FASTA_ONEPASS", "0") not in ("", "0")
-FASTA_KERNEL = "scan_kernel<FASTA>" if _ONEPASS else "fasta_map_kernel + fasta_place_kernel (one HIP-event span)"
-FASTA_PMC_KERNELS = "scan_kernel<0" if _ONEPASS else "fasta_map_kernel,fasta_place_kernel"
+FASTA_KERNEL = "scan_kernel<FASTA>" if _ONEPASS else "map_kernel<FASTA> + fasta_place_kernel (one HIP-event span)"
+FASTA_PMC_KERNELS = "scan_kernel<0" if _ONEPASS else "map_kernel<0>,fasta_place_kernel"
 
 
 class FastaSpec:
@@ -613,6 +613,9 @@ def delim_worker(args, team, k, world, dev, keep_host):
     def collect(i):
         return ctxs[i % 2].delim_ranges_result(nr)
 
+    two_max = ctxs[0].forms()[1]
+    kernel = ("map_kernel<DELIM> + delim_place_kernel (one HIP-event span)" if nbytes <= two_max
+              else "scan_kernel<DELIM> (one-pass)")
     S = Steps(team, ctxs, launch, collect)
     team.barrier()
     S.warm(args.warmup)
@@ -646,6 +649,7 @@ def delim_worker(args, team, k, world, dev, keep_host):
     wpr = item * n_out / nbytes
     d_mix = ctxs[0].workspace("bench_mix", int(wpr * nbytes) + (1 << 20))
     out = {"dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn), "scanned": nbytes, "offsets": n_out,
+           "kernel": kernel,
            "alg_bytes": nbytes + item * n_out + (8 * ScanContext.block_table_size(rg)[1] if fmt == "u16b" else 0),
            "verified": verified, "gen_s": gen_s, "size": size,
            "stream_peak": stream_peak(ctxs[0], d_buf.ptr, nbytes),
@@ -709,7 +713,7 @@ def main_delim(args, world, rank, devs, team):
         "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
                      "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
-                     "kernel": "scan_kernel<DELIM>", "kernel_avg_us": round(kern * 1e6, 2),
+                     "kernel": allres[0]["kernel"], "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(allres[0]["alg_bytes"]),
                      "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)%s" % (
                          {"u16b": 2, "u32p": 4, "u64": 8}[args.index_dtype],

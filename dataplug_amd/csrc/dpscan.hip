@@ -1548,15 +1548,41 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
 // every unit to the grid's slowest); here the map streams like the calibration kernel and the placement
 // only touches the summaries (16 B per 16 KiB) and the events.
 constexpr uint32_t kSpillCap = 512;                 // events kept per range (1 KiB slot); more = dense
+// The spill is word-major: 16-byte word j (events 8j .. 8j + 7) of range r at word index j * nranges + r, so
+// the placement's threads (one per range) read word j of consecutive ranges from consecutive addresses, and
+// the map's 16 waves of a workgroup (on 16 consecutive ranges in the same step) write adjacent words.
+__device__ __forceinline__ uint64_t spill_word(uint32_t j, uint64_t r, uint64_t nranges) { return j * nranges + r; }
 constexpr uint32_t kPlaceBlock = 1024;              // range summaries per placement workgroup (one per thread)
+constexpr uint32_t kStageBytes = 128u << 10;        // LDS staging of a placement block's output run
 constexpr uint32_t kMapWaves = 16;                  // map kernel: 16 data waves per workgroup, no coordinator
 constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 0-3: sF, sT, fV, dense)
+#ifndef DP_MAP_SYNC        // map kernel: a workgroup barrier per step (its waves on adjacent ranges)
+#define DP_MAP_SYNC 1
+#endif
+#ifndef DP_PLACE_TICKET    // placement blocks in ticket order (0: in blockIdx order, A/B only)
+#define DP_PLACE_TICKET 1
+#endif
+#ifndef DP_MAP_LEAD        // DP_MAP_SYNC 2: steps a wave may lead its workgroup's slowest wave by
+#define DP_MAP_LEAD 1
+#endif
+#ifndef DP_MAP_DYN         // map kernel: groups of 16 ranges claimed from a ticket (0: static striding)
+#define DP_MAP_DYN 1
+#endif
+#ifndef DP_MAP_RUN         // groups per claim ...
+#define DP_MAP_RUN 2
+#endif
+#ifndef DP_MAP_TAIL        // ... and one group per claim once within DP_MAP_TAIL x G groups of the end
+#define DP_MAP_TAIL 3
+#endif
 
 struct MapArgs {
   const uint8_t* base;         // 16-byte aligned; coordinates relative to it
   uint64_t nchunks, nranges;
-  uint4* rec;                  // [nranges] range summaries
-  uint16_t* spill;             // [nranges][kSpillCap] event positions relative to the range
+  uint4* rec;                  // [2 * nranges]: range r's summary at 2r, its geometry at 2r + 1 (range_geo_rec)
+  uint16_t* spill;             // event positions relative to the range, word-major (spill_word)
+  unsigned int* ticket;        // (DP_MAP_DYN) next group to claim; zeroed by the placement kernel
+  unsigned int* place_ticket;  // [2] the placement kernel's block ticket, zeroed here
+  uint32_t delim;              // DELIM: the delimiter byte x4
 };
 
 // Range r of the chunk table (ranges of kWaveBytes in each chunk's aligned coordinates): the Geo of a
@@ -1590,62 +1616,226 @@ __device__ __forceinline__ Geo range_geo(const Tab& T, uint32_t nchunks, uint32_
   return g;
 }
 
-__global__ void __launch_bounds__(kWave * kMapWaves) fasta_map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
-                                                                      const uint64_t* __restrict__ tab_hi,
-                                                                      const uint64_t* __restrict__ tab_r0) {
+// One 16-byte-group returning atomic add, hand-waited like the input loads (inline asm: the compiler adds no
+// vmcnt wait for it): issued right after a wait_buf, its result is read after the next one (tools/isa_guard.py
+// tracks returning atomics with sc0 as hand-waited destinations).
+// Called by every lane of the wave (no divergent branch around it, so the compiler sees the destination
+// defined in all lanes and merges nothing into it while the atomic is in flight); only lane 0 executes the
+// atomic (exec narrowed inside the asm and restored), and only its value is meaningful: read it with
+// readfirstlane once the wait has covered it.
+__device__ __forceinline__ uint32_t atomic_add_nowait(unsigned int* p, uint32_t v) {
+  uint32_t old;
+  uint64_t save;
+  asm volatile("s_mov_b64 %1, exec\n\t"
+               "s_mov_b64 exec, 1\n\t"
+               "global_atomic_add %0, %2, %3, off sc0\n\t"
+               "s_mov_b64 exec, %1"
+               : "=&v"(old), "=&s"(save) : "v"(p), "v"(v) : "memory");
+  return old;
+}
+
+// The second half of a range record: where the range lies (aligned coordinates) and its chunk bounds relative to
+// it, so the placement needs no chunk-table lookup: {wbase lo, wbase hi, lo_w | hi_w << 16, 0}.
+__device__ __forceinline__ uint4 range_geo_rec(const Geo& g) {
+  return uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32), g.lo_u | (g.hi_u << 16), 0u};
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
+                                                                const uint64_t* __restrict__ tab_hi,
+                                                                const uint64_t* __restrict__ tab_r0) {
   __shared__ __attribute__((aligned(16))) uint16_t sev[kMapWaves][kSpillCap];
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   const uint32_t nranges = (uint32_t)M.nranges, nchunks = (uint32_t)M.nchunks;
   const uint32_t NW = gridDim.x * kMapWaves;
+  uint16_t* evw = sev[wave];
+  // the placement kernel that follows claims its blocks from this ticket: it starts from zero (no memset
+  // launch, no end-of-kernel counter; the placement kernel zeroes this kernel's own ticket in turn)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    M.place_ticket[0] = 0u;
+    M.place_ticket[1] = 0u;
+  }
+#ifdef DP_PROF
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  uint32_t n_done = 0;
+#endif
+#if DP_MAP_DYN
+  // Groups of 16 consecutive ranges (one per wave), the first one blockIdx.x, then claimed in runs from a
+  // ticket by wave 0 (so faster CUs and XCDs take more groups); s_grp[k % kGrpQ] = the group of step k.
+  constexpr uint32_t kGrpQ = 8;
+  __shared__ uint32_t s_grp[kGrpQ];
+  const uint32_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
+  const uint32_t G = gridDim.x;
+  uint32_t claimed = 0, run = 0, pend = 0;           // wave 0: steps with a group; the pending claim's size
+  uint32_t claim_res = 0;
+  if (wave == 0) {                                    // before any load: the claim is waited for at once
+    uint32_t u = atomic_add_nowait(M.ticket, (uint32_t)DP_MAP_RUN);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(u) :: "memory");
+    u = G + rfl(u);
+    if (lane == 0) {
+      s_grp[0] = blockIdx.x;
+      for (uint32_t i = 0; i < (uint32_t)DP_MAP_RUN; ++i) s_grp[1 + i] = u + i;
+    }
+  }
+  claimed = 1 + DP_MAP_RUN;
+  __syncthreads();
+  // (the host launches at most one workgroup per group, so s_grp[0] = blockIdx.x < ngroups)
+  uint32_t r = s_grp[0] * kMapWaves + (uint32_t)wave;
+#elif DP_MAP_SYNC
+  // every wave of the workgroup runs the workgroup's step count (wave 0 has the most), so the per-step
+  // barrier keeps its 16 waves on adjacent ranges; a wave past the end scans nothing and stores nothing
+  uint32_t r = blockIdx.x * kMapWaves + (uint32_t)wave;
+  const uint32_t r0w = blockIdx.x * kMapWaves;
+  if (r0w >= nranges) return;
+  const uint32_t steps = (nranges - r0w + NW - 1) / NW;
+#else
   uint32_t r = blockIdx.x * kMapWaves + (uint32_t)wave;
   if (r >= nranges) return;
-  uint16_t* evw = sev[wave];
+#endif
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
   Buf b[kBufs];
 #pragma unroll
   for (int h = 0; h < kBufs; ++h) load_buf(b[h], ScanArgs{M.base}, g, 0, lane, h);
+#if DP_MAP_SYNC == 2 && !DP_MAP_DYN
+  // soft lockstep: a wave starts step it only once every wave of the workgroup has finished step
+  // it - DP_MAP_LEAD - 1 (monotonic per-slot completion counts, no reset), and trails-the-front issue priority
+  __shared__ uint32_t s_done[8];
+  __shared__ uint32_t s_front;
+  if (threadIdx.x < 8) s_done[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_front = 0;
+  __syncthreads();
+#endif
+#if DP_MAP_SYNC || DP_MAP_DYN
+  for (uint32_t it = 0;; ++it) {
+#if DP_MAP_SYNC == 2 && !DP_MAP_DYN
+    if (it > (uint32_t)DP_MAP_LEAD) {
+      const uint32_t j = it - DP_MAP_LEAD - 1u;
+      const uint32_t target = kMapWaves * (j / 8u + 1u);
+      uint64_t t0 = 0;
+      for (uint32_t spins = 0; lds_ld(&s_done[j % 8u]) < target; ++spins) {
+        if (wait_expired(spins, t0)) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    {
+      uint32_t front = 0;
+      if (lane == 0) front = __hip_atomic_fetch_max(&s_front, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      front = rfl(front);
+      const uint32_t lag = front > it ? front - it : 0u;
+      set_prio(lag < 3u ? lag : 3u);
+    }
+#else
+    __syncthreads();
+#endif
+#else
   for (;;) {
+#endif
+#if DP_MAP_DYN
+    const uint32_t gnext = s_grp[(it + 1) % kGrpQ];
+    const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
+    // wave 0 keeps two steps claimed ahead: step it + 2 needs its group by the barrier of step it + 1
+    const bool do_claim = wave == 0 && claimed < it + 3u && s_grp[(claimed - 1) % kGrpQ] < ngroups;
+    if (do_claim) run = s_grp[(claimed - 1) % kGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
+#else
     const uint32_t rn = r + NW;
+#endif
     const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
     FState st{0u, 0u, 0u, -1, 0u, 0u};
     const int lo = (int)g.lo_u, hi = (int)g.hi_u;
     const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
     auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kSpillCap - 1u ? rk : kSpillCap - 1u] = (uint16_t)pos; };
+    const uint32_t key = M.delim ^ kSel12;
 #pragma unroll
     for (int h = 0; h < kBufs; ++h) {
       wait_buf(b[h]);                                 // this buffer landed; the other stays in flight
+#if DP_MAP_DYN
+      if (h == 0 && do_claim) {                       // the youngest vector-memory operation until the next wait
+        claim_res = atomic_add_nowait(M.ticket, run);
+        pend = run;
+      }
+      if (h == 1 && pend) {                           // the wait above covered the claim: its value is back
+        asm volatile("" : "+v"(claim_res) :: "memory");
+        const uint32_t u = G + rfl(claim_res);
+        if (lane == 0)
+          for (uint32_t i = 0; i < pend; ++i) s_grp[(claimed + i) % kGrpQ] = u + i;
+        claimed += pend;
+        pend = 0;
+      }
+#endif
       v4u x[kRows];
 #pragma unroll
       for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
-      if (interior) fasta_rows<true>(x, b[h].la, h, lo, hi, lane, st, keep);
-      else fasta_rows<false>(x, b[h].la, h, lo, hi, lane, st, keep);
+      if constexpr (MODE == kFasta) {
+        if (interior) fasta_rows<true>(x, b[h].la, h, lo, hi, lane, st, keep);
+        else fasta_rows<false>(x, b[h].la, h, lo, hi, lane, st, keep);
+      } else {
+        if (interior) delim_rows<true>(x, h, lo, hi, key, lane, st.nev, keep);
+        else delim_rows<false>(x, h, lo, hi, key, lane, st.nev, keep);
+      }
       if (h + 1 < kBufs) load_buf(b[h], ScanArgs{M.base}, gn, 0, lane, h);
     }
-    // the range's summary (phase_a_rec of a one-range unit) and its events
-    if (!st.nlseen) st.fV = st.S;
-    uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
-    if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
     const bool dense = st.nev > kSpillCap;
     const uint32_t n = dense ? 0u : st.nev;
     cbar();
-    if ((uint32_t)lane * 8u < n) {
-      const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
-      __builtin_nontemporal_store(v, reinterpret_cast<v4u*>(M.spill + (uint64_t)r * kSpillCap) + lane);
-    }
-    if (lane == 0) {
-      const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
-                          ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
-      M.rec[r] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+    if constexpr (MODE == kFasta) {
+      // the range's summary (phase_a_rec of a one-range unit) and its events, word-major
+      if (!st.nlseen) st.fV = st.S;
+      uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
+      if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
+      if ((uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
+        const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
+        reinterpret_cast<v4u*>(M.spill)[spill_word((uint32_t)lane, r, M.nranges)] = v;   // re-read soon: cacheable
+      }
+      if (lane == 0 && (g.fl & kGeoValid)) {
+        const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
+                            ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
+        M.rec[2 * (uint64_t)r] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+        M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
+      }
+    } else {
+      // the range's delimiter count and positions, range-major (the placement gathers consecutive events)
+      if ((uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
+        const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
+        reinterpret_cast<v4u*>(M.spill)[(uint64_t)r * (kSpillCap / 8u) + (uint32_t)lane] = v;
+      }
+      if (lane == 0 && (g.fl & kGeoValid)) {
+        const uint32_t fl = (dense ? kFlDense : 0u) | ((g.fl & kGeoFirst) ? kRecFirst : 0u) |
+                            ((g.fl & kGeoLast) ? kRecLast : 0u);
+        M.rec[2 * (uint64_t)r] = uint4{st.nev, 0u, fl, g.c};
+        M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
+      }
     }
     load_buf(b[kBufs - 1], ScanArgs{M.base}, gn, 0, lane, kBufs - 1);
+#ifdef DP_PROF
+    n_done += (g.fl & kGeoValid) ? 1u : 0u;
+#endif
+#if DP_MAP_SYNC == 2 && !DP_MAP_DYN
+    if (lane == 0) lds_add(&s_done[it % 8u], 1u);
+#endif
+#if DP_MAP_DYN
+    if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
+#elif DP_MAP_SYNC
+    if (it + 1 >= steps) break;
+#else
     if (rn >= nranges) break;
+#endif
     r = rn;
     g = gn;
   }
   drain_bufs(b);
+#ifdef DP_PROF
+  // per wave: start and end (100 MHz realtime clock), ranges scanned, the XCC it ran on
+  if (lane == 0 && blockIdx.x < kProfMaxGrid) {
+    unsigned long long* w = g_prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
+    w[0] = t_start;
+    w[1] = __builtin_amdgcn_s_memrealtime();
+    w[2] = n_done;
+    w[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 0xFu;   // HW_REG_XCC_ID
+  }
+#endif
 }
 
 // Wave-wide (64-lane) inclusive scan of range functions, lane 0 farthest.
@@ -1664,6 +1854,7 @@ struct PlaceArgs {
   const uint16_t* spill;
   uint64_t nranges, nblocks;
   int count_only;              // no output buffer: counts, chunk ends and pending only
+  unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
 };
 
 template <int OUT64>
@@ -1682,25 +1873,58 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
   __shared__ uint32_t s_dense[kPlaceBlock];
   __shared__ uint64_t s_dP[kPlaceBlock];
   __shared__ uint32_t s_dS[kPlaceBlock];
+  // the block's output slots are one contiguous run: staged here, then written with coalesced 16-byte stores
+  __shared__ __attribute__((aligned(16))) OutT s_stage[kStageBytes / sizeof(OutT)];
+  __shared__ unsigned long long s_lo, s_hi;          // the block's output run
+  __shared__ uint32_t s_anydense;
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   if (threadIdx.x == 0) {
-    s_blk = atomicAdd(&A.ticket[0], 1u);             // blocks in claim order: a block only waits on lower,
+    if (blockIdx.x == 0) PA.map_ticket[0] = 0u;       // the map kernel is done with it: ready for the next launch
+    s_blk = DP_PLACE_TICKET ? atomicAdd(&A.ticket[0], 1u) : blockIdx.x;   // claim order: a block only waits on lower,
     s_ndense = 0;                                     // already running or finished, blocks
+    s_lo = 0;
+    s_hi = 0;
+    s_anydense = 0;
   }
   __syncthreads();
   const uint32_t b = s_blk;
+#ifdef DP_PROF
+  // per block (profiling build): realtime stamps at its sections, in g_prof past the map kernel's words
+  unsigned long long* pst = g_prof + ((uint64_t)(512u + (b & 511u)) * kProfWaves) * kProfSlots;
+#define PLACE_STAMP(i) do { if (threadIdx.x == 0 && b < 512u) pst[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PLACE_STAMP(i) do {} while (0)
+#endif
+  PLACE_STAMP(0);
   const uint64_t r = (uint64_t)b * kPlaceBlock + threadIdx.x;
   const bool valid = r < PA.nranges;
   uint4 rc = uint4{0u, 0u, 2u, 0u};                   // identity: no count, state kept
-  if (valid) rc = PA.rec[r];
+  uint4 rg = uint4{0u, 0u, 0u, 0u};
+  if (valid) {
+    rc = PA.rec[2 * r];
+    rg = PA.rec[2 * r + 1];
+  }
   const uint32_t cF = rc.x & 0xFFFFu, cT = rc.x >> 16, fl = rc.z;
+  // what the placement needs besides the prefix is loaded now, under the scan and the look-back: the
+  // range's first two spill words (16 events; most ranges have no more)
+  const uint32_t nev = rc.y >> 16;
+  const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
+  uint4 sw0 = uint4{0u, 0u, 0u, 0u}, sw1 = uint4{0u, 0u, 0u, 0u};
+  const uint4* sp = reinterpret_cast<const uint4*>(PA.spill);
+  if (valid && !PA.count_only) {
+    if (!(fl & kFlDense)) {
+      if (nev > 0u) sw0 = sp[spill_word(0u, r, PA.nranges)];
+      if (nev > 8u) sw1 = sp[spill_word(1u, r, PA.nranges)];
+    }
+  }
   const Func32 f{cF, cT, fl & 1u, (fl >> 1) & 1u};
   const Func32 inc = f32_wave_scan(f);
   const Func32 ex = Func32{dpp32<kWaveShr1, 0xF>(inc.cF, 0u), dpp32<kWaveShr1, 0xF>(inc.cT, 0u),
                            dpp32<kWaveShr1, 0xF>(inc.sF, 0u), dpp32<kWaveShr1, 0xF>(inc.sT, 1u)};
   if (lane == kWave - 1) s_wagg[wave] = inc;
+  PLACE_STAMP(1);
   __syncthreads();
   if (wave == 0) {
     Func32 w = lane < kPW ? s_wagg[lane] : Func32{0, 0, 0, 1};
@@ -1718,6 +1942,7 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
     // the block's exclusive prefix: a decoupled look-back over the block descriptors
     uint64_t P = 0;
     uint32_t S = 0;
+    PLACE_STAMP(2);
     if (b > 0) {
       if (lane == 0) st_desc(&A.desc[b], pack_agg(agg) | A.epoch);
       const uint32_t W = lb_span(b, kNoUnit);
@@ -1740,6 +1965,7 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
       s_P = P;
       s_S = S;
     }
+    PLACE_STAMP(3);
   }
   __syncthreads();
   const uint64_t Pb = s_P;
@@ -1751,40 +1977,47 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
   uint64_t P = Pw + (Sw ? ex.cT : ex.cF);
   uint32_t S = (Sw ? ex.sT : ex.sF) & 1u;
   if (fl & kRecFirst) S = 0u;                         // chunk start: no header pending
-  if (valid) {
-    const uint64_t P_incl = P + (S ? cT : cF);
-    const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
-    if (fl & kRecLast) {
-      A.chunk_end[rc.w] = P_incl;
-      A.pending[rc.w] = S_out ? (long long)P_incl - 1 : -1ll;
-    }
-    if (r + 1 == PA.nranges) A.total[0] = P_incl;
-  }
+  // this range's output run: slots [b0, b0 + n) (the fix-up of phase_b: drop a start pending from the
+  // previous range, prepend the end of the header pending into it)
+  const uint32_t fn = rc.y & 0xFFFFu;
+  const uint32_t fV = (fl >> 2) & 1u;
+  const uint32_t skip = S & fV;
+  const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
+  const uint64_t b0 = 2 * P - S;
+  // the ranges' runs follow one another in range order: the block's run is [b0 of its first range, end of its
+  // last); a dense range (its count of slots is not in the record) means no staging
   if (valid && !PA.count_only) {
-    const uint32_t c = rc.w;
-    const uint64_t lo = T.lo[c];
-    const uint64_t wbase = (lo & ~15ull) + (r - (uint64_t)T.u0[c]) * (uint64_t)kWaveBytes;
+    if (fl & kFlDense) s_anydense = 1u;
+    if (threadIdx.x == 0) s_lo = b0;
+    if (r + 1 == PA.nranges || threadIdx.x == kPlaceBlock - 1) s_hi = b0 + nev - skip + pre;
+  }
+  __syncthreads();
+  const uint64_t last = 2 * A.cap - 1;
+  const uint64_t run_lo = s_lo, run_hi = s_hi < last + 1 ? s_hi : last + 1;
+  constexpr uint32_t kVec = 16u / sizeof(OutT);
+  const uint64_t stage0 = run_lo & ~(uint64_t)(kVec - 1u);
+  const bool stage = !PA.count_only && !s_anydense && run_lo < run_hi &&
+                     (run_hi - stage0) * sizeof(OutT) <= kStageBytes;
+  if (valid && !PA.count_only) {
     if (fl & kFlDense) {
       s_dense[atomicAdd(&s_ndense, 1u)] = threadIdx.x;
     } else {
       const uint64_t obj_off = A.obj_base - A.shift + wbase;
       const bool near4g = OUT64 == 0 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
-      const uint32_t fn = rc.y & 0xFFFFu, nev = rc.y >> 16;
-      const uint32_t fV = (fl >> 2) & 1u;
-      const uint32_t skip = S & fV;
-      const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
-      const uint64_t b0 = 2 * P - S, last = 2 * A.cap - 1;
       bool ovf = false;
       auto emit = [&](uint64_t slot, uint32_t e) {
         const uint64_t val = obj_off + e + (slot & 1u);
         if (near4g) ovf |= val > 0xFFFFFFFFull;
-        put<OutT>(A.out, slot < last ? slot : last, val);
+        if (stage) {
+          if (slot <= last) s_stage[slot - stage0] = (OutT)val;
+        } else {
+          put<OutT>(A.out, slot < last ? slot : last, val);
+        }
       };
       if (pre) emit(b0, fn - 1u);
-      const uint4* sp = reinterpret_cast<const uint4*>(PA.spill + r * kSpillCap);
       const uint64_t base_slot = b0 + pre - skip;     // event k goes to base_slot + k (k >= skip)
       for (uint32_t k0 = 0; k0 < nev; k0 += 8u) {
-        const uint4 v = sp[k0 >> 3];
+        const uint4 v = k0 == 0u ? sw0 : (k0 == 8u ? sw1 : sp[spill_word(k0 >> 3, r, PA.nranges)]);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (uint32_t e = 0; e < 8u; ++e) {
@@ -1795,8 +2028,36 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
       if (ovf) atomicOr(A.err, kErrOverflow);
     }
   }
-  // dense ranges: one wave each, rescanned from the input with the now known state
   __syncthreads();
+  PLACE_STAMP(4);
+  if (stage) {
+    // coalesced copy of the run; its first and last partial 16-byte groups element by element, so that the
+    // neighbouring blocks' slots are never written.  (A header still pending at a chunk end leaves its end
+    // slot unwritten here: the resolve kernel, or the host, writes it afterwards.)
+    OutT* o = reinterpret_cast<OutT*>(A.out);
+    const uint64_t v0 = (run_lo + kVec - 1u) & ~(uint64_t)(kVec - 1u), v1 = run_hi & ~(uint64_t)(kVec - 1u);
+    if (v0 <= v1) {
+      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+      const v4u* src = reinterpret_cast<const v4u*>(s_stage + (v0 - stage0));
+      v4u* dst = reinterpret_cast<v4u*>(o + v0);
+      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[g];
+    } else {                                          // the run lies inside one 16-byte group
+      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+    }
+  }
+  PLACE_STAMP(5);
+  // per-chunk results, after the output stores (a store here would make the loops above wait for it)
+  if (valid) {
+    const uint64_t P_incl = P + (S ? cT : cF);
+    const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
+    if (fl & kRecLast) {
+      A.chunk_end[rc.w] = P_incl;
+      A.pending[rc.w] = S_out ? (long long)P_incl - 1 : -1ll;
+    }
+    if (r + 1 == PA.nranges) A.total[0] = P_incl;
+  }
+  // dense ranges: one wave each, rescanned from the input with the now known state
   const uint32_t nd = s_ndense;
   if (nd) {
     // every thread keeps its own (P, S); a wave fetches a dense range's through LDS
@@ -1806,23 +2067,241 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
     for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
       const uint32_t t = s_dense[i];
       const uint64_t rr = (uint64_t)b * kPlaceBlock + t;
-      const uint4 rq = PA.rec[rr];
-      const uint32_t c = rq.w;
-      const uint64_t lo = T.lo[c], hi = T.hi[c];
-      const uint64_t wbase = (lo & ~15ull) + (rr - (uint64_t)T.u0[c]) * (uint64_t)kWaveBytes;
-      const uint32_t lo_w = lo > wbase ? (uint32_t)(lo - wbase) : 0u;
-      const uint64_t hw = hi - wbase;
-      const uint32_t hi_w = hw < (uint64_t)(kWaveBytes + 16) ? (uint32_t)hw : (uint32_t)(kWaveBytes + 16);
-      dense_b<kFasta, OUT64>(A, wbase, lo_w | (hi_w << 16), s_dP[t], s_dS[t], lane);
+      const uint4 rq = PA.rec[2 * rr + 1];
+      dense_b<kFasta, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, s_dP[t], s_dS[t], lane);
     }
   }
-  // every block is done with the ticket: the last one resets it for the next launch on this table
-  __syncthreads();
+  PLACE_STAMP(6);
+#undef PLACE_STAMP
+}
+
+// ------------------------------------------------------------------------------------------ DELIM, two kernels
+// The newline index as map_kernel<kDelim> (per 16 KiB range: the delimiter count, and the positions in the
+// range's spill slot, range-major) followed by delim_place_kernel: one workgroup per block of 1024 ranges
+// scans the counts, resolves the block's prefix by a decoupled look-back over block descriptors (counts: an
+// AGG or PREFIX descriptor holds a 48-bit count), and then writes the block's output entries by output
+// index: thread t fills groups of 8 consecutive entries, finding each entry's range by a binary search over
+// the block's prefix counts in LDS and gathering its position from that range's spill slot, so the stores
+// are coalesced 16-byte groups.  Ranges with more than kSpillCap delimiters ("dense") are rescanned from the
+// input by dense_b.  every_k / emit_add / carry and the four output forms are those of the one-pass kernel.
+__device__ __forceinline__ uint64_t pack_count(uint64_t st, uint64_t count) { return st | (count & 0xFFFFFFFFFFFFull); }
+__device__ __forceinline__ bool lb_reduce_count(uint64_t (&d)[kLbPer], uint32_t W, uint64_t basedesc, int lane, uint64_t& P) {
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+  uint32_t seen = 0, bad = 0;
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) {                // nearest first
+    if (kLbPer * rl + j == W) d[j] = basedesc;
+    const uint64_t st = d[j] & kStatMask;
+    if (!seen && st == 0ull) bad = 1;
+    if (st == kStatPrefix) seen = 1;
+  }
+  const uint64_t PB = __ballot(seen);
+  const uint64_t BB = __ballot(bad);
+  if (PB == 0ull) return false;
+  const int Lp = 63 - __builtin_clzll(PB);            // nearest lane holding a prefix
+  const uint64_t need = ~((1ull << Lp) - 1ull);
+  if (BB & need) return false;
+  uint32_t jp = kLbPer;
+#pragma unroll
+  for (int j = kLbPer - 1; j >= 0; --j)
+    if ((d[j] & kStatMask) == kStatPrefix) jp = (uint32_t)j;
+  const uint32_t kP = (uint32_t)kLbPer * (uint32_t)(63 - Lp) + (uint32_t)__builtin_amdgcn_readlane((int)jp, Lp);
+  uint64_t sum = 0, pv = 0;
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) {
+    const uint32_t k = kLbPer * rl + j;
+    if (k < kP) sum += d[j] & 0xFFFFFFFFFFFFull;
+    if (k == kP) pv = d[j] & 0xFFFFFFFFFFFFull;
+  }
+  // wave sum (64-bit, two 32-bit halves through DPP)
+  uint32_t lo = (uint32_t)sum, hi = (uint32_t)(sum >> 32);
+  sum = ((uint64_t)hi << 32) | lo;
+  sum += dpp64<kRowShr1, 0xF>(sum, 0ull);
+  sum += dpp64<kRowShr2, 0xF>(sum, 0ull);
+  sum += dpp64<kRowShr4, 0xF>(sum, 0ull);
+  sum += dpp64<kRowShr8, 0xF>(sum, 0ull);
+  sum += dpp64<kRowBcast15, 0xA>(sum, 0ull);
+  sum += dpp64<kRowBcast31, 0xC>(sum, 0ull);
+  P = readlane64(pv, Lp) + readlane64(sum, kWave - 1);
+  return true;
+}
+
+struct DPlaceArgs {
+  const uint4* rec;
+  const uint16_t* spill;       // range-major: range r's positions at spill[r * kSpillCap + e]
+  uint64_t nranges;
+  unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
+};
+
+template <int OUT64>
+__global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA, ScanArgs A,
+                                                                 const uint64_t* __restrict__ tab_lo,
+                                                                 const uint64_t* __restrict__ tab_hi,
+                                                                 const uint64_t* __restrict__ tab_r0) {
+  typedef typename std::conditional<OUT64 == 1, uint64_t,
+                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
+  constexpr int kPW = kPlaceBlock / kWave;
+  constexpr uint32_t kDenseBit = 0x80000000u;
+  __shared__ uint32_t s_blk, s_ndense;
+  __shared__ uint32_t s_wsum[kPW];
+  __shared__ uint64_t s_P, s_total;
+  __shared__ uint32_t s_ex[kPlaceBlock];             // delimiters of the block before range t
+  __shared__ uint32_t s_cnt[kPlaceBlock];            // range t's delimiters (| kDenseBit: not spilled)
+  __shared__ uint64_t s_off[kPlaceBlock];            // object offset of range t's first byte + emit_add
+  __shared__ uint32_t s_dense[kPlaceBlock];
+  const int lane = __lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   if (threadIdx.x == 0) {
-    if (atomicAdd(&A.ticket[1], 1u) == gridDim.x - 1u) {
-      atomicExch(&A.ticket[0], 0u);
-      atomicExch(&A.ticket[1], 0u);
+    if (blockIdx.x == 0) PA.map_ticket[0] = 0u;
+    s_blk = atomicAdd(&A.ticket[0], 1u);             // claim order: a block only waits on lower blocks
+    s_ndense = 0;
+  }
+  __syncthreads();
+  const uint32_t b = s_blk;
+  const uint32_t t = threadIdx.x;
+  const uint64_t r = (uint64_t)b * kPlaceBlock + t;
+  const bool valid = r < PA.nranges;
+  uint4 rc = uint4{0u, 0u, 0u, 0u}, rg = uint4{0u, 0u, 0u, 0u};
+  if (valid) {
+    rc = PA.rec[2 * r];
+    rg = PA.rec[2 * r + 1];
+  }
+  const uint32_t cnt = rc.x, fl = rc.z;
+  const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
+  // block scan of the counts
+  uint32_t inc = cnt;
+  inc += dpp32<kRowShr1, 0xF>(inc, 0u);
+  inc += dpp32<kRowShr2, 0xF>(inc, 0u);
+  inc += dpp32<kRowShr4, 0xF>(inc, 0u);
+  inc += dpp32<kRowShr8, 0xF>(inc, 0u);
+  inc += dpp32<kRowBcast15, 0xA>(inc, 0u);
+  inc += dpp32<kRowBcast31, 0xC>(inc, 0u);
+  if (lane == kWave - 1) s_wsum[wave] = inc;
+  __syncthreads();
+  if (wave == 0) {
+    uint32_t w = lane < kPW ? s_wsum[lane] : 0u;
+    uint32_t wi = w;
+    wi += dpp32<kRowShr1, 0xF>(wi, 0u);
+    wi += dpp32<kRowShr2, 0xF>(wi, 0u);
+    wi += dpp32<kRowShr4, 0xF>(wi, 0u);
+    wi += dpp32<kRowShr8, 0xF>(wi, 0u);
+    if (lane < kPW) s_wsum[lane] = wi - w;            // exclusive per wave
+    const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)wi, kPW - 1);
+    uint64_t P = 0;
+    if (b > 0) {
+      if (lane == 0) st_desc(&A.desc[b], pack_count(kStatAgg, total) | A.epoch);
+      const uint32_t W = lb_span(b, kNoUnit);
+      uint64_t t0 = 0;
+      for (uint32_t spins = 0;; ++spins) {
+        uint64_t d[kLbPer];
+        lb_load(A, b, W, lane, d);
+        if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P)) break;
+        if (wait_expired(spins, t0)) {
+          if (lane == 0) atomicOr(A.err, kErrTimeout);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
     }
+    if (lane == 0) {
+      st_desc(&A.desc[b], pack_count(kStatPrefix, P + total) | A.epoch);
+      s_P = P;
+      s_total = total;
+    }
+  }
+  __syncthreads();
+  const uint64_t Pb = s_P, total = s_total;
+  const uint32_t ex = s_wsum[wave] + inc - cnt;
+  const uint64_t P = Pb + ex;                         // delimiters of the launch before this range
+  const bool dense = (fl & kFlDense) != 0u;
+  s_ex[t] = ex;
+  s_cnt[t] = valid ? (cnt | (dense ? kDenseBit : 0u)) : 0u;
+  s_off[t] = A.obj_base - A.shift + wbase + A.emit_add;
+  if (valid && dense) s_dense[atomicAdd(&s_ndense, 1u)] = t;
+  __syncthreads();
+  // output entries of the block: the selected delimiters (global ordinal G = launch ordinal + carry with
+  // G % k == k - 1) go to index G / k - carry / k
+  const uint64_t k = A.every_k, carry = A.carry;
+  const uint64_t Ga = Pb + carry, Gb = Ga + total;
+  const uint64_t q_lo = Ga / k - carry / k, q_hi = Gb / k - carry / k;
+  const uint64_t cap = A.cap;
+  const uint64_t q_end = q_hi < cap ? q_hi : cap;
+  OutT* out = reinterpret_cast<OutT*>(A.out);
+  const bool near4g = OUT64 == 0 && !A.wrap32;
+  bool ovf = false;
+  const uint16_t* spb = PA.spill + (uint64_t)b * kPlaceBlock * kSpillCap;
+  for (uint64_t g0 = (q_lo & ~7ull) + 8ull * t; g0 < q_end; g0 += 8ull * kPlaceBlock) {
+    // entry q of the group: launch ordinal o = (q + carry / k) * k + k - 1 - carry, block ordinal o - Pb
+    const uint64_t qa = g0 > q_lo ? g0 : q_lo;
+    uint64_t ob = (qa + carry / k) * k + k - 1 - carry - Pb;
+    // the range holding block ordinal ob: the last t with s_ex[t] <= ob
+    uint32_t lo = 0, hi = kPlaceBlock;
+    while (hi - lo > 1) {
+      const uint32_t m = (lo + hi) >> 1;
+      if (s_ex[m] <= ob) lo = m; else hi = m;
+    }
+    uint32_t tr = lo;
+    OutT v[8];
+    uint32_t have = 0;                                // bit i: entry g0 + i written by this group
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i) {
+      const uint64_t q = g0 + i;
+      if (q < qa || q >= q_end) continue;
+      const uint64_t o = (q + carry / k) * k + k - 1 - carry - Pb;
+      while (tr + 1 < kPlaceBlock && s_ex[tr + 1] <= o) ++tr;   // walk on (zero-count ranges in between)
+      const uint32_t cw = s_cnt[tr];
+      if (cw & kDenseBit) continue;                  // written by the dense rescan
+      const uint32_t e = (uint32_t)(o - s_ex[tr]);
+      const uint64_t val = s_off[tr] + spb[(uint64_t)tr * kSpillCap + e];
+      if (near4g) ovf |= val > 0xFFFFFFFFull;
+      v[i] = (OutT)val;
+      have |= 1u << i;
+    }
+    if (have == 0xFFu) {
+      if constexpr (OUT64 == 2) {
+        v4u pk;
+        pk.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
+        pk.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
+        pk.z = (uint32_t)v[4] | ((uint32_t)v[5] << 16);
+        pk.w = (uint32_t)v[6] | ((uint32_t)v[7] << 16);
+        __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(out + g0));
+      } else if constexpr (OUT64 == 0) {
+        __builtin_nontemporal_store(v4u{(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]},
+                                    reinterpret_cast<v4u*>(out + g0));
+        __builtin_nontemporal_store(v4u{(uint32_t)v[4], (uint32_t)v[5], (uint32_t)v[6], (uint32_t)v[7]},
+                                    reinterpret_cast<v4u*>(out + g0 + 4));
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < 8u; i += 2)
+          __builtin_nontemporal_store(v2u64{(uint64_t)v[i], (uint64_t)v[i + 1]}, reinterpret_cast<v2u64*>(out + g0 + i));
+      }
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < 8u; ++i)
+        if (have & (1u << i)) out[g0 + i] = v[i];
+    }
+  }
+  if (ovf) atomicOr(A.err, kErrOverflow);
+  // per-chunk results and the 64 KiB block table, after the output stores
+  if (valid) {
+    if (fl & kRecLast) A.chunk_end[rc.w] = P + cnt;
+    if (r + 1 == PA.nranges) A.total[0] = P + cnt;
+    if constexpr (OUT64 == 2) {
+      // the entries before every 64 KiB boundary that starts a range of this chunk (see phase_b)
+      const uint64_t off0 = A.obj_base - A.shift + wbase;
+      const uint64_t j = (off0 >> 16) - A.tab_j0;
+      const bool holds = (rg.z & 0xFFFFu) == 0u && (rg.z >> 16) != 0u;
+      if ((off0 & 0xFFFFull) == 0 && holds && off0 >= (A.tab_j0 << 16) && j < A.tab_n) A.blocktab[j] = P;
+    }
+  }
+  __syncthreads();
+  const uint32_t nd = s_ndense;
+  for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
+    const uint32_t td = s_dense[i];
+    const uint64_t rr = (uint64_t)b * kPlaceBlock + td;
+    const uint4 rq = PA.rec[2 * rr + 1];
+    dense_b<kDelim, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, Pb + s_ex[td], 0u, lane);
   }
 }
 
@@ -1931,13 +2410,10 @@ __global__ void __launch_bounds__(1024) stream_kernel(const uint4* __restrict__ 
     for (int i = 0; i < kCalRange / 1024; ++i) x ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
     acc ^= x;
     if (out) {
+      // one non-temporal 16-byte store per element (the scan's own output stores are 16-byte groups too)
       const uint64_t e0 = (r * wq16) >> 6, e1 = ((r + 1) * wq16) >> 6;   // 16-byte elements of this range
-      for (uint64_t e = e0 + (uint64_t)lane; e < e1; e += 64) {
-        __builtin_nontemporal_store(x, &out[e].x);
-        __builtin_nontemporal_store((uint32_t)e, &out[e].y);
-        __builtin_nontemporal_store((uint32_t)r, &out[e].z);
-        __builtin_nontemporal_store(acc, &out[e].w);
-      }
+      for (uint64_t e = e0 + (uint64_t)lane; e < e1; e += 64)
+        __builtin_nontemporal_store(v4u{x, (uint32_t)e, (uint32_t)r, acc}, reinterpret_cast<v4u*>(out) + e);
     }
   }
   if (acc == 0x9E3779B9u) sink[0] = acc;   // keeps the loads alive; practically never stores
@@ -1945,6 +2421,12 @@ __global__ void __launch_bounds__(1024) stream_kernel(const uint4* __restrict__ 
 
 // ------------------------------------------------------------------------------------------ host side
 thread_local std::string g_err;
+
+// Newline launches up to this many bytes run as two kernels; larger ones as the one-pass look-back kernel.
+// Default 0: on the CSV/VCF shapes (a newline every 36-80 B) the two-kernel form was 7-25 % slower at 4 and
+// 16 GiB (its placement gathers every position from the spill), so the one-pass kernel stays the newline
+// index; DP_DELIM_TWOPASS_MAX enables the two-kernel form (it wins on sparse newlines: DESIGN.md §4).
+constexpr uint64_t kDelimTwoPassMax = 0;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -1993,6 +2475,7 @@ struct dp_ctx {
   uint16_t* d_spill = nullptr;
   uint64_t rec_cap = 0;               // ranges
   bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
+  uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
   uint64_t nchunks = 0, cap = 0;
@@ -2084,8 +2567,8 @@ int harvest_events(dp_ctx* c) {
 }
 
 // Lay out the chunk table in aligned coordinates and enqueue its upload when it changed.
-// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[5] (err | total | spare x2 |
-// unit ticket: next unit, workgroups finished; zero between launches).
+// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[6] (err | total | spare x2 |
+// unit ticket: next unit, workgroups finished | map-kernel group ticket: the same pair; zero between launches).
 // No per-launch reset: every launch rewrites pending / chunk_end of each non-empty chunk and total (when it
 // has units), so only the upload sets their defaults (-1, ~0, 0) and err = 0.  A launch that sets an err
 // bit drops last_tab, so the next one re-uploads (results of a failed launch are discarded anyway).
@@ -2107,7 +2590,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
   }
   tab[3 * n] = units;
   tab.push_back(unit_bytes);                          // (host-side only: a change of geometry re-uploads)
-  const uint64_t words = 5 * n + 1 + 5;
+  const uint64_t words = 5 * n + 1 + 6;
   int rc = ensure_tab(c, words);
   if (rc) return rc;
   c->pend_off = 3 * n + 1;
@@ -2117,7 +2600,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(c->h_tab, tab.data(), (3 * n + 1) * 8);
     memset(c->h_tab + c->pend_off, 0xFF, 2 * n * 8);
-    memset(c->h_tab + c->ctrl_off, 0, 5 * 8);
+    memset(c->h_tab + c->ctrl_off, 0, 6 * 8);
     HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, words * 8, hipMemcpyHostToDevice, c->stream));
     c->last_tab.swap(tab);
   }
@@ -2213,12 +2696,8 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   return scan_leave(c, ss);
 }
 
-// The two-kernel FASTA index (fasta_map_kernel + fasta_place_kernel) over a chunk table staged with
-// 16 KiB ranges.  Timed as one span: the HIP events bracket both kernels.
-int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
-                  int out_u64, uint64_t cap) {
-  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
-  if (nranges == 0) return DP_OK;
+// Range summaries and spill slots for a two-kernel launch (grow-only).
+int ensure_ranges(dp_ctx* c, uint64_t nranges) {
   if (nranges >= 0xFFFFFFFFull) return fail(DP_ERR_INVALID, "launch exceeds 2^32 ranges of 16 KiB");
   if (nranges > c->rec_cap) {
     if (c->d_rec) HIPCHK(hipFree(c->d_rec));
@@ -2227,10 +2706,21 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
     c->d_spill = nullptr;
     c->rec_cap = 0;
     const uint64_t cap_r = nranges + nranges / 8 + 64;
-    HIPCHK(dev_alloc((void**)&c->d_rec, cap_r * sizeof(uint4)));
+    HIPCHK(dev_alloc((void**)&c->d_rec, 2 * cap_r * sizeof(uint4)));
     HIPCHK(dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t)));
     c->rec_cap = cap_r;
   }
+  return DP_OK;
+}
+
+// The two-kernel FASTA index (map_kernel<kFasta> + fasta_place_kernel) over a chunk table staged with
+// 16 KiB ranges.  Timed as one span: the HIP events bracket both kernels.
+int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
+                  int out_u64, uint64_t cap) {
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  if (nranges == 0) return DP_OK;
+  int rc0 = ensure_ranges(c, nranges);
+  if (rc0) return rc0;
   const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
   int rc = ensure_desc(c, nblocks);
   if (rc) return rc;
@@ -2247,7 +2737,8 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   a.nunits = nranges;
   a.desc = c->d_desc;
   a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
-  const int count_only = (cap == 0 || d_out == nullptr);
+  static const bool probe_count_only = getenv("DP_PROBE_PLACE_COUNT_ONLY") != nullptr;   // perf probe only
+  const int count_only = (cap == 0 || d_out == nullptr || probe_count_only);
   if (count_only) {
     d_out = c->d_tab + c->ctrl_off + 2;
     cap = 1;
@@ -2267,7 +2758,11 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   m.nranges = nranges;
   m.rec = c->d_rec;
   m.spill = c->d_spill;
+  m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
+  m.place_ticket = a.ticket;
+  m.delim = 0;
   PlaceArgs pa;
+  pa.map_ticket = m.ticket;
   pa.rec = c->d_rec;
   pa.spill = c->d_spill;
   pa.nranges = nranges;
@@ -2286,7 +2781,7 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   hipEvent_t e0;
   rc = ev_begin(c, &e0, ss);
   if (rc) return rc;
-  hipLaunchKernelGGL(fasta_map_kernel, dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
+  hipLaunchKernelGGL((map_kernel<kFasta>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   if (out_u64)
     hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
@@ -2294,6 +2789,91 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   else
     hipLaunchKernelGGL((fasta_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
                        thi, tr0);
+  HIPCHK(hipGetLastError());
+  rc = ev_end(c, ss);
+  if (rc) return rc;
+  return scan_leave(c, ss);
+}
+
+// The two-kernel newline index (map_kernel<kDelim> + delim_place_kernel), same staging as launch_fasta2.
+int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
+                  int kind, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
+                  uint32_t wrap32, unsigned long long* blocktab, uint64_t tab_j0, uint64_t tab_n) {
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  if (nranges == 0) return DP_OK;
+  int rc = ensure_ranges(c, nranges);
+  if (rc) return rc;
+  const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
+  rc = ensure_desc(c, nblocks);
+  if (rc) return rc;
+  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
+    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
+    c->desc_epoch = 0;
+  }
+  ScanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = d_buf - shift;
+  a.shift = shift;
+  a.obj_base = buf_base;
+  a.nchunks = n;
+  a.nunits = nranges;
+  a.desc = c->d_desc;
+  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
+  if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
+    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
+    cap = 1;
+  }
+  a.out = d_out;
+  a.cap = cap;
+  a.out_u64 = kind;
+  a.wrap32 = wrap32;
+  a.blocktab = blocktab;
+  a.tab_j0 = tab_j0;
+  a.tab_n = tab_n;
+  a.carry = carry;
+  a.delim = delim * 0x01010101u;
+  a.every_k = every_k;
+  a.emit_add = emit_add;
+  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
+  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
+  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
+  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
+  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  MapArgs m;
+  m.base = a.base;
+  m.nchunks = n;
+  m.nranges = nranges;
+  m.rec = c->d_rec;
+  m.spill = c->d_spill;
+  m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
+  m.place_ticket = a.ticket;
+  m.delim = a.delim;
+  DPlaceArgs pa;
+  pa.rec = c->d_rec;
+  pa.spill = c->d_spill;
+  pa.nranges = nranges;
+  pa.map_ticket = m.ticket;
+  const uint64_t waves_needed = (nranges + kMapWaves - 1) / kMapWaves;
+  const unsigned grid = (unsigned)(waves_needed < (uint64_t)c->cus ? waves_needed : (uint64_t)c->cus);
+  const uint64_t* tlo = c->d_tab;
+  const uint64_t* thi = c->d_tab + n;
+  const uint64_t* tr0 = c->d_tab + 2 * n;
+  DeviceSerial& ds = g_serial[c->device];
+  std::lock_guard<std::mutex> lock(ds.m);
+  hipStream_t ss = nullptr;
+  rc = scan_enter(c, ds, &ss);
+  if (rc) return rc;
+  hipEvent_t e0;
+  rc = ev_begin(c, &e0, ss);
+  if (rc) return rc;
+  hipLaunchKernelGGL((map_kernel<kDelim>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
+  HIPCHK(hipGetLastError());
+  if (kind == 1)
+    hipLaunchKernelGGL((delim_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+  else if (kind == 2)
+    hipLaunchKernelGGL((delim_place_kernel<2>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+  else
+    hipLaunchKernelGGL((delim_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   rc = ev_end(c, ss);
   if (rc) return rc;
@@ -2370,6 +2950,9 @@ int dp_ctx_create(int device, dp_ctx** out) {
   if (c->grid > 256) c->grid = 256;   // one look-back window (G <= 256) per unit
   const char* onepass = getenv("DP_FASTA_ONEPASS");
   c->fasta_onepass = onepass && atoi(onepass) != 0;
+  // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
+  const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
+  c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
   *out = c;
   return DP_OK;
 }
@@ -2600,12 +3183,20 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
     if (!d_out) return fail(DP_ERR_INVALID, "out_mode 3 needs an output buffer (entries + block table)");
   }
   const uint64_t nr = rg.size() / 2;
-  uint64_t units = 0;
-  rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units);
-  if (rc) return rc;
+  uint64_t units = 0, span = 0;
+  for (uint64_t i = 0; i < nr; ++i) span += rg[2 * i + 1] - rg[2 * i];
   const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
-  rc = launch_scan(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
-                   out_mode == 2, tab, j0, ntab);
+  if (span <= c->delim_twopass_max) {                 // the two-kernel form
+    rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
+    if (rc) return rc;
+    rc = launch_delim2(c, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
+                       out_mode == 2, tab, j0, ntab);
+  } else {
+    rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units);
+    if (rc) return rc;
+    rc = launch_scan(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
+                     out_mode == 2, tab, j0, ntab);
+  }
   if (rc) return rc;
   c->inflight = kDelim;
   c->nchunks = nr;
@@ -2749,6 +3340,13 @@ int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slo
 int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs) {
   if (device_allocs) *device_allocs = g_dev_allocs.load(std::memory_order_relaxed);
   if (host_allocs) *host_allocs = g_host_allocs.load(std::memory_order_relaxed);
+  return DP_OK;
+}
+
+int dp_scan_forms(dp_ctx* c, int* fasta_two_kernel, uint64_t* delim_two_kernel_max) {
+  if (!c) return fail(DP_ERR_INVALID, "null");
+  if (fasta_two_kernel) *fasta_two_kernel = c->fasta_onepass ? 0 : 1;
+  if (delim_two_kernel_max) *delim_two_kernel_max = c->delim_twopass_max;
   return DP_OK;
 }
 

@@ -66,7 +66,8 @@ def test_canonical_plan_cut_over_groups(kind, groups):
     cs = math.ceil(n / 4)
     plan = cpu_ref.chunk_plan(n, cs)
     pieces, _, gs = fasta_split(plan, groups, n)
-    assert len(gs) == groups and any(not p.first for p in pieces)
+    assert len(gs) == groups
+    assert any(not p.first for p in pieces) == (groups % len(plan) != 0)     # 3 chunks (floor plan): 3 whole
     co = _co(FASTA, a.tobytes(), f"canon_{kind}_{groups}", _mem(f"canon_{kind}_{groups}"))
     co.preprocess(chunk_size=cs, parallel_config={"dataplug_devices": [0] * groups})
     exp = dpref.fasta_pairs(a, plan)

@@ -1,11 +1,13 @@
 """End-to-end (PCIe-inclusive) rate of the FASTA index build, for DESIGN.md §6 (never bench.py's value).
 
-    python tools/e2e_rate.py [--size BYTES] [--reps N]
+    python tools/e2e_rate.py [--size BYTES] [--reps N] [--devices 0,0] [--only memory,loopback_http]
 
 co.preprocess(chunk_size=size/4) on a synthetic FASTA held by (a) an in-process store (memory://), (b) the
 loopback HTTP S3 server in its own process, and (c) the same server as a thread of this process: ranged
 GETs into pinned host memory -> H2D -> scan -> D2H of the index -> PUT of index + attrs.  Also times the
-stages separately on the same object.
+stages separately on the same object.  ``--devices`` passes ``dataplug_devices`` to every preprocess (e.g.
+``0,0,0,0`` rehearses the multi-GPU split on one GPU: four groups, four persistent workers), and each rep
+reports the library's device / pinned allocations made during it (dp_alloc_counts: 0 once warm).
 """
 from __future__ import annotations
 
@@ -38,7 +40,12 @@ def main():
     ap.add_argument("--size", type=int, default=4 << 30)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--port", type=int, default=19001)
+    ap.add_argument("--devices", default=None, help="dataplug_devices for every preprocess, e.g. 0,0,0,0")
+    ap.add_argument("--only", default=None, help="comma-separated subset of the store configurations")
+    ap.add_argument("--no-stages", action="store_true")
     args = ap.parse_args()
+    from dataplug_amd.scan._lib import alloc_counts
+    pc = {"dataplug_devices": [int(x) for x in args.devices.split(",")]} if args.devices else {}
     size = args.size
     host = synth.tiled_fasta_host(size, seed=1)
     store = MemoryStore.named("e2e")
@@ -47,7 +54,7 @@ def main():
     store.put("genomics", "x.fasta", memoryview(host))
     del host
     cs = math.ceil(size / 4)
-    res = {"object_bytes": size, "chunk_size": cs}
+    res = {"object_bytes": size, "chunk_size": cs, "dataplug_devices": pc.get("dataplug_devices")}
     srv = LoopbackS3Server(store).start()
     # the loopback server in its own process, as MinIO serves the reference's examples (an in-process server
     # shares the GIL with the client's GET threads: tools/http_probe.py)
@@ -65,17 +72,29 @@ def main():
                ("loopback_http", {"endpoint_url": f"http://127.0.0.1:{port}"}),
                ("loopback_http_in_process", srv.storage_config))
     for name, cfg in configs:
+        if args.only and name not in args.only.split(","):
+            continue
         co = CloudObject.from_s3(FASTA, "s3://genomics/x.fasta", s3_config=cfg)
-        co.preprocess(chunk_size=cs, force=True)          # warm: context, pinned + device buffers
-        ts = []
+        co.preprocess(chunk_size=cs, force=True, parallel_config=pc)   # warm: contexts, pinned + device buffers
+        ts, allocs = [], []
         for _ in range(args.reps):
+            a0 = alloc_counts()
             t0 = time.perf_counter()
-            co.preprocess(chunk_size=cs, force=True)
+            co.preprocess(chunk_size=cs, force=True, parallel_config=pc)
             ts.append(time.perf_counter() - t0)
+            a1 = alloc_counts()
+            allocs.append([a1[0] - a0[0], a1[1] - a0[1]])
         t = min(ts)
         res[f"{name}_preprocess_s"] = round(t, 3)
         res[f"{name}_GiB_per_s"] = round(size / t / GiB, 2)
+        res[f"{name}_allocs_per_rep"] = allocs
         print(name, res, flush=True)
+    if args.no_stages:
+        srv.stop()
+        proc.terminate()
+        proc.wait(timeout=30)
+        print(json.dumps(res), flush=True)
+        return
     # stage breakdown (memory store)
     co = CloudObject.from_s3(FASTA, "s3://genomics/x.fasta", s3_config={"endpoint_url": "memory://e2e"})
     ctx = get_context(0)

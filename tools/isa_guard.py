@@ -1,4 +1,4 @@
-"""ISA guard for the hand-waited input loads of scan_kernel and fasta_map_kernel (dataplug_amd/csrc/dpscan.hip).
+"""ISA guard for the hand-waited input loads of scan_kernel and map_kernel (dataplug_amd/csrc/dpscan.hip).
 
 The data waves issue their buffer loads as inline asm and wait with one explicit `s_waitcnt vmcnt(N)` per
 buffer, N = the loads of the buffers still in flight.  The compiler knows nothing about that contract, so
@@ -19,7 +19,7 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "dataplug_amd", "csrc", "dpscan.hip")
-KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1(?:11scan_kernelILi[01]ELi[012]EE|16fasta_map_kernel)\w*):", re.M)
+KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1(?:11scan_kernelILi[01]ELi[012]EE|10map_kernelILi[01]EE)\w*):", re.M)
 
 
 def compile_asm() -> str:
@@ -104,7 +104,9 @@ def _scan(ins, q, problems, k):
         pending = frozenset().union(*q) if q else frozenset()
         if VMEM_RE.match(op):
             # hand-waited destinations: the input buffer loads and the returning (sc0) ticket atomic
-            if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]):
+            # (global atomics: only the map kernel's inline-asm claim is hand-waited; the compiler waits for its own)
+            if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]) or \
+                    (op.startswith("global_atomic") and "sc0" in toks[1:] and "map_kernel" in k):
                 dst = regs(toks[1])
                 srcs = set()
                 for t in toks[2:]:
@@ -135,7 +137,7 @@ def check(asm_path: str):
     text = open(asm_path).read()
     problems = []
     kernels = KERNEL_RE.findall(text)
-    assert len(kernels) == 6, kernels
+    assert len(kernels) == 7, kernels
     for k in kernels:
         body = text[text.index(k + ":") + len(k) + 1:]
         body = body[:body.index(".Lfunc_end")]
@@ -163,7 +165,7 @@ def scratch(asm_path: str):
     text = open(asm_path).read()
     out = []
     for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, re.S):
-        if "scan_kernel" not in m.group(1) and "fasta_map_kernel" not in m.group(1):
+        if "scan_kernel" not in m.group(1) and "map_kernel" not in m.group(1):
             continue
         sz = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(2))
         if sz and int(sz.group(1)) > 0:

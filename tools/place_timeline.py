@@ -1,0 +1,65 @@
+"""Section times of one fasta_place_kernel launch (profiling build: tools/build_variants.py prof=DP_PROF), next to
+the map kernel's wave end times, in microseconds from the map kernel's first wave start.
+
+    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof.so python tools/place_timeline.py [--size BYTES]
+
+Per placement block: 0 start (after its ticket), 1 range summaries loaded + wave scans, 2 block scan done,
+3 block prefix resolved (look-back), 4 events staged, 5 output written, 6 dense rescans done.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dataplug_amd import synth  # noqa: E402
+from dataplug_amd.scan import ScanContext, _lib  # noqa: E402
+from dataplug_amd.scan._lib import check  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=4 << 30)
+    args = ap.parse_args()
+    n = args.size
+    ctx = ScanContext(0)
+    host = synth.tiled_fasta_host(n, seed=1)
+    d = ctx.workspace("in", n + 64)
+    ctx.h2d(d.ptr, host)
+    cs = math.ceil(n / 4)
+    chunks = np.asarray([(i * cs, min(n, (i + 1) * cs)) for i in range(n // cs)], np.uint64).reshape(-1)
+    out = ctx.workspace("out", n // 64)
+    for _ in range(3):
+        ctx.fasta_index_async(d.ptr, n, 0, n, chunks, out.ptr, False, n // 256)
+        ctx.fasta_result(len(chunks) // 2)
+    words = 1024 * 16 * 8
+    buf = np.zeros(words, np.uint64)
+    sl, wv = ctypes.c_int(), ctypes.c_int()
+    check(_lib.load().dp_debug_profile(ctx.handle, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), words,
+                                       ctypes.byref(sl), ctypes.byref(wv)))
+    w = buf.reshape(1024, 16, 8).astype(np.int64)
+    mp = w[:256]
+    live = mp[:, :, 1] > 0
+    t0 = mp[:, :, 0][live].min()
+    map_end = (mp[:, :, 1][live].max() - t0) / 100.0
+    nb = -(-(n // (16 << 10)) // 1024)
+    pl = w[512:512 + min(nb, 512), 0, :7]
+    us = (pl - t0) / 100.0
+    q = lambda a: [round(float(x), 1) for x in np.percentile(a, [0, 50, 100])]
+    res = {"map_last_wave_end": round(map_end, 1), "blocks": int(len(pl))}
+    names = ["start", "loaded", "scanned", "prefix", "staged", "written", "end"]
+    for i, nm in enumerate(names):
+        res[nm] = q(us[:, i])
+    res["prefix_minus_scanned_med"] = round(float(np.median(us[:, 3] - us[:, 2])), 2)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
