@@ -67,6 +67,10 @@ constexpr int kBufBytes = kRowBytes * kRows;
 constexpr int kWaveBytes = kRowBytes * kRangeRows;   // 16 KiB wave range per unit
 constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 240 KiB look-back unit
 static_assert(kRows * kBufs == kRangeRows && kRows >= 2 && kRows <= 8, "buffers of 2, 4 or 8 rows");
+// In-flight load destinations live in VGPRs (4 per 16-byte row). 1024-lane workgroups have 128 VGPRs per
+// lane; past 64 of them in buffers the compiler spills live destinations to scratch, and a spilled
+// un-waited destination corrupts addresses (DP_RROWS=32 + DP_NBUF=4 = 128 VGPRs faulted the GPU in round 3).
+static_assert(kBufs * kRows * 4 <= 64, "input buffers must leave room in the 128-VGPR budget");
 #ifndef DP_RING
 #define DP_RING 16
 #endif
@@ -1756,7 +1760,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const
         claim_res = atomic_add_nowait(M.ticket, run);
         pend = run;
       }
-      if (h == 1 && pend) {                           // the wait above covered the claim: its value is back
+      if (h == kBufs - 1 && pend) {                   // the wait above covered the claim: its value is back
         asm volatile("" : "+v"(claim_res) :: "memory");
         const uint32_t u = G + rfl(claim_res);
         if (lane == 0)

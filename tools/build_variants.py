@@ -38,6 +38,17 @@ def main(specs):
     with ThreadPoolExecutor(4) as ex:
         for out in ex.map(lambda j: build(defines=j[0], prof=j[1], out=j[2], src=j[3]), jobs):
             print(out)
+    # a variant whose compiled code touches an in-flight load destination (or spills to scratch) can corrupt
+    # addresses and fault the GPU: it is deleted, never run (tools/isa_guard.py on the same defines)
+    guard = os.path.join(os.path.dirname(os.path.abspath(__file__)), "isa_guard.py")
+    for defines, prof, out, src in jobs:
+        if src != SRC:
+            continue
+        env = dict(os.environ, DP_DEFINES=",".join(defines + (["DP_PROF"] if prof else [])))
+        r = subprocess.run([sys.executable, guard], env=env, capture_output=True, text=True)
+        if r.returncode != 0:
+            os.remove(out)
+            print(f"REFUSED {out}: ISA guard failed ({r.stdout.strip().splitlines()[-1]})")
     for j in jobs:
         if j[3] != SRC:
             os.remove(j[3])
