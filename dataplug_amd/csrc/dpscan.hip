@@ -154,11 +154,19 @@ enum Mode { kFasta = 0, kDelim = 1 };
 
 // In-kernel section timers (diagnostics build only: -DDP_PROF).  Per workgroup and wave, kProfSlots
 // accumulated s_memtime deltas; read back with dp_debug_profile().
-#ifdef DP_PROF
+// -DDP_PROF2: only the two-kernel form's stamps (map_kernel / fasta_place_kernel), none in scan_kernel, whose
+// DP_PROF accumulators cost registers (its DP_PROF build spills and fails tools/isa_guard.py).
+#if defined(DP_PROF) && defined(DP_PROF2)
+#error "DP_PROF and DP_PROF2 are exclusive"
+#endif
+#if defined(DP_PROF) || defined(DP_PROF2)
+#define DP_STAMPS 1
 constexpr int kProfSlots = 8;
 constexpr int kProfWaves = 16;
 constexpr int kProfMaxGrid = 1024;
 __device__ unsigned long long g_prof[kProfMaxGrid * kProfWaves * kProfSlots];
+#endif
+#ifdef DP_PROF
 #define PROF_DECL uint64_t prof_acc[kProfSlots] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t prof_t = __builtin_amdgcn_s_memtime()
 #define PROF_MARK(slot) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[slot] += t_ - prof_t; prof_t = t_; } while (0)
 #define PROF_FLUSH(wave) do { if (__lane_id() == 0 && blockIdx.x < kProfMaxGrid) { for (int i_ = 0; i_ < kProfSlots; ++i_) \
@@ -446,17 +454,20 @@ __device__ __forceinline__ uint32_t lb_span(uint32_t u, uint32_t u_prev) {
   const uint32_t d = u_prev == kNoUnit ? u : u - u_prev - 1u;
   return d < kLbSlots ? d : kLbSlots;
 }
+// All kLbPer loads are issued before any is used (a lane outside the window loads desc[0] and discards it):
+// a load under its own branch got its own vmcnt(0) wait there, one round trip per slot.
 __device__ __forceinline__ void lb_load(const ScanArgs& A, uint32_t u, uint32_t W, int lane, uint64_t (&d)[kLbPer]) {
   const uint32_t rl = (uint32_t)(kWave - 1 - lane);
 #pragma unroll
   for (int j = 0; j < kLbPer; ++j) {
     const uint32_t k = kLbPer * rl + j;
-    if (k < W) {
-      const uint64_t v = ld_desc(&A.desc[u - 1 - k]);
-      d[j] = (v & kEpochMask) == A.epoch ? v : 0ull;   // an earlier launch's descriptor: not published yet
-    } else {
-      d[j] = kIdentDesc;
-    }
+    d[j] = ld_desc(&A.desc[k < W ? u - 1 - k : 0u]);
+  }
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) {
+    const uint32_t k = kLbPer * rl + j;
+    // an earlier launch's descriptor: not published yet
+    d[j] = k < W ? ((d[j] & kEpochMask) == A.epoch ? d[j] : 0ull) : kIdentDesc;
   }
 }
 
@@ -1558,7 +1569,12 @@ constexpr uint32_t kSpillCap = 512;                 // events kept per range (1 
 __device__ __forceinline__ uint64_t spill_word(uint32_t j, uint64_t r, uint64_t nranges) { return j * nranges + r; }
 constexpr uint32_t kPlaceBlock = 1024;              // range summaries per placement workgroup (one per thread)
 constexpr uint32_t kStageBytes = 128u << 10;        // LDS staging of a placement block's output run
-constexpr uint32_t kMapWaves = 16;                  // map kernel: 16 data waves per workgroup, no coordinator
+#ifndef DP_MAP_WAVES
+#define DP_MAP_WAVES 16
+#endif
+constexpr uint32_t kMapWaves = DP_MAP_WAVES;        // map kernel: 16 data waves per workgroup, no coordinator
+constexpr uint32_t kMapPerCU = 16u / kMapWaves;     // (A/B: 8-wave workgroups, two per CU)
+static_assert(kMapWaves * kMapPerCU == 16u, "map kernel: 16 waves per CU");
 constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 0-3: sF, sT, fV, dense)
 #ifndef DP_MAP_SYNC        // map kernel: a workgroup barrier per step (its waves on adjacent ranges)
 #define DP_MAP_SYNC 1
@@ -1645,7 +1661,7 @@ __device__ __forceinline__ uint4 range_geo_rec(const Geo& g) {
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
+__global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
                                                                 const uint64_t* __restrict__ tab_hi,
                                                                 const uint64_t* __restrict__ tab_r0) {
   __shared__ __attribute__((aligned(16))) uint16_t sev[kMapWaves][kSpillCap];
@@ -1653,7 +1669,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   const uint32_t nranges = (uint32_t)M.nranges, nchunks = (uint32_t)M.nchunks;
+#if !DP_MAP_DYN
   const uint32_t NW = gridDim.x * kMapWaves;
+#endif
   uint16_t* evw = sev[wave];
   // the placement kernel that follows claims its blocks from this ticket: it starts from zero (no memset
   // launch, no end-of-kernel counter; the placement kernel zeroes this kernel's own ticket in turn)
@@ -1661,7 +1679,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const
     M.place_ticket[0] = 0u;
     M.place_ticket[1] = 0u;
   }
-#ifdef DP_PROF
+#ifdef DP_STAMPS
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   uint32_t n_done = 0;
 #endif
@@ -1813,7 +1831,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const
       }
     }
     load_buf(b[kBufs - 1], ScanArgs{M.base}, gn, 0, lane, kBufs - 1);
-#ifdef DP_PROF
+#ifdef DP_STAMPS
     n_done += (g.fl & kGeoValid) ? 1u : 0u;
 #endif
 #if DP_MAP_SYNC == 2 && !DP_MAP_DYN
@@ -1830,7 +1848,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves) map_kernel(MapArgs M, const
     g = gn;
   }
   drain_bufs(b);
-#ifdef DP_PROF
+#ifdef DP_STAMPS
   // per wave: start and end (100 MHz realtime clock), ranges scanned, the XCC it ran on
   if (lane == 0 && blockIdx.x < kProfMaxGrid) {
     unsigned long long* w = g_prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
@@ -1883,7 +1901,6 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
   __shared__ uint32_t s_anydense;
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) PA.map_ticket[0] = 0u;       // the map kernel is done with it: ready for the next launch
     s_blk = DP_PLACE_TICKET ? atomicAdd(&A.ticket[0], 1u) : blockIdx.x;   // claim order: a block only waits on lower,
@@ -1894,7 +1911,7 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
   }
   __syncthreads();
   const uint32_t b = s_blk;
-#ifdef DP_PROF
+#ifdef DP_STAMPS
   // per block (profiling build): realtime stamps at its sections, in g_prof past the map kernel's words
   unsigned long long* pst = g_prof + ((uint64_t)(512u + (b & 511u)) * kProfWaves) * kProfSlots;
 #define PLACE_STAMP(i) do { if (threadIdx.x == 0 && b < 512u) pst[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -2020,15 +2037,19 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
       };
       if (pre) emit(b0, fn - 1u);
       const uint64_t base_slot = b0 + pre - skip;     // event k goes to base_slot + k (k >= skip)
-      for (uint32_t k0 = 0; k0 < nev; k0 += 8u) {
-        const uint4 v = k0 == 0u ? sw0 : (k0 == 8u ? sw1 : sp[spill_word(k0 >> 3, r, PA.nranges)]);
+      // (the prefetched words by name: selecting among them by index made the compiler keep them in a
+      // private array in scratch, waiting for their loads at once)
+      auto emit8 = [&](const uint4& v, uint32_t k0) {
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
         for (uint32_t e = 0; e < 8u; ++e) {
           const uint32_t k = k0 + e;
           if (k >= skip && k < nev) emit(base_slot + k, (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu);
         }
-      }
+      };
+      if (nev > 0u) emit8(sw0, 0u);
+      if (nev > 8u) emit8(sw1, 8u);
+      for (uint32_t k0 = 16u; k0 < nev; k0 += 8u) emit8(sp[spill_word(k0 >> 3, r, PA.nranges)], k0);
       if (ovf) atomicOr(A.err, kErrOverflow);
     }
   }
@@ -2148,14 +2169,13 @@ __global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA,
   constexpr uint32_t kDenseBit = 0x80000000u;
   __shared__ uint32_t s_blk, s_ndense;
   __shared__ uint32_t s_wsum[kPW];
-  __shared__ uint64_t s_P, s_total;
+  __shared__ uint64_t s_P;
   __shared__ uint32_t s_ex[kPlaceBlock];             // delimiters of the block before range t
   __shared__ uint32_t s_cnt[kPlaceBlock];            // range t's delimiters (| kDenseBit: not spilled)
   __shared__ uint64_t s_off[kPlaceBlock];            // object offset of range t's first byte + emit_add
   __shared__ uint32_t s_dense[kPlaceBlock];
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) PA.map_ticket[0] = 0u;
     s_blk = atomicAdd(&A.ticket[0], 1u);             // claim order: a block only waits on lower blocks
@@ -2211,11 +2231,10 @@ __global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA,
     if (lane == 0) {
       st_desc(&A.desc[b], pack_count(kStatPrefix, P + total) | A.epoch);
       s_P = P;
-      s_total = total;
     }
   }
   __syncthreads();
-  const uint64_t Pb = s_P, total = s_total;
+  const uint64_t Pb = s_P;
   const uint32_t ex = s_wsum[wave] + inc - cnt;
   const uint64_t P = Pb + ex;                         // delimiters of the launch before this range
   const bool dense = (fl & kFlDense) != 0u;
@@ -2226,64 +2245,38 @@ __global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA,
   __syncthreads();
   // output entries of the block: the selected delimiters (global ordinal G = launch ordinal + carry with
   // G % k == k - 1) go to index G / k - carry / k
-  const uint64_t k = A.every_k, carry = A.carry;
-  const uint64_t Ga = Pb + carry, Gb = Ga + total;
-  const uint64_t q_lo = Ga / k - carry / k, q_hi = Gb / k - carry / k;
+  // A wave copies one range's selected positions at a time: the range's launch ordinals are o0 + e for its
+  // spill entries e, the selected ones (G = o + carry with G % k == k - 1) are e0, e0 + k, ... and land at
+  // consecutive output indexes from q0 = G / k - carry / k. Lanes take consecutive entries, so the spill
+  // loads and the output stores are contiguous per wave instruction.
+  const uint64_t k = rfl64(A.every_k), carry = rfl64(A.carry);
   const uint64_t cap = A.cap;
-  const uint64_t q_end = q_hi < cap ? q_hi : cap;
   OutT* out = reinterpret_cast<OutT*>(A.out);
   const bool near4g = OUT64 == 0 && !A.wrap32;
   bool ovf = false;
   const uint16_t* spb = PA.spill + (uint64_t)b * kPlaceBlock * kSpillCap;
-  for (uint64_t g0 = (q_lo & ~7ull) + 8ull * t; g0 < q_end; g0 += 8ull * kPlaceBlock) {
-    // entry q of the group: launch ordinal o = (q + carry / k) * k + k - 1 - carry, block ordinal o - Pb
-    const uint64_t qa = g0 > q_lo ? g0 : q_lo;
-    uint64_t ob = (qa + carry / k) * k + k - 1 - carry - Pb;
-    // the range holding block ordinal ob: the last t with s_ex[t] <= ob
-    uint32_t lo = 0, hi = kPlaceBlock;
-    while (hi - lo > 1) {
-      const uint32_t m = (lo + hi) >> 1;
-      if (s_ex[m] <= ob) lo = m; else hi = m;
+  for (uint32_t tr = (uint32_t)wave; tr < (uint32_t)kPlaceBlock; tr += kPW) {
+    const uint32_t cw = rfl(s_cnt[tr]);
+    if (cw == 0u || (cw & kDenseBit)) continue;      // nothing, or written by the dense rescan
+    const uint64_t o0 = Pb + rfl(s_ex[tr]);
+    const uint64_t off = rfl64(s_off[tr]);
+    const uint16_t* sp = spb + (uint64_t)tr * kSpillCap;
+    uint32_t e0 = 0, n = cw, step = 1;
+    uint64_t q0 = o0;
+    if (k != 1ull) {
+      const uint64_t G0 = o0 + carry;
+      const uint64_t r0 = k - 1ull - G0 % k;
+      e0 = (uint32_t)(r0 < cw ? r0 : cw);
+      n = r0 < cw ? (uint32_t)((cw - r0 + k - 1ull) / k) : 0u;
+      q0 = (G0 + r0) / k - carry / k;
+      step = (uint32_t)k;
     }
-    uint32_t tr = lo;
-    OutT v[8];
-    uint32_t have = 0;                                // bit i: entry g0 + i written by this group
-#pragma unroll
-    for (uint32_t i = 0; i < 8u; ++i) {
-      const uint64_t q = g0 + i;
-      if (q < qa || q >= q_end) continue;
-      const uint64_t o = (q + carry / k) * k + k - 1 - carry - Pb;
-      while (tr + 1 < kPlaceBlock && s_ex[tr + 1] <= o) ++tr;   // walk on (zero-count ranges in between)
-      const uint32_t cw = s_cnt[tr];
-      if (cw & kDenseBit) continue;                  // written by the dense rescan
-      const uint32_t e = (uint32_t)(o - s_ex[tr]);
-      const uint64_t val = s_off[tr] + spb[(uint64_t)tr * kSpillCap + e];
+    if (q0 >= cap) continue;
+    if (q0 + n > cap) n = (uint32_t)(cap - q0);
+    for (uint32_t i = (uint32_t)lane; i < n; i += kWave) {
+      const uint64_t val = off + sp[e0 + i * step];
       if (near4g) ovf |= val > 0xFFFFFFFFull;
-      v[i] = (OutT)val;
-      have |= 1u << i;
-    }
-    if (have == 0xFFu) {
-      if constexpr (OUT64 == 2) {
-        v4u pk;
-        pk.x = (uint32_t)v[0] | ((uint32_t)v[1] << 16);
-        pk.y = (uint32_t)v[2] | ((uint32_t)v[3] << 16);
-        pk.z = (uint32_t)v[4] | ((uint32_t)v[5] << 16);
-        pk.w = (uint32_t)v[6] | ((uint32_t)v[7] << 16);
-        __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(out + g0));
-      } else if constexpr (OUT64 == 0) {
-        __builtin_nontemporal_store(v4u{(uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]},
-                                    reinterpret_cast<v4u*>(out + g0));
-        __builtin_nontemporal_store(v4u{(uint32_t)v[4], (uint32_t)v[5], (uint32_t)v[6], (uint32_t)v[7]},
-                                    reinterpret_cast<v4u*>(out + g0 + 4));
-      } else {
-#pragma unroll
-        for (uint32_t i = 0; i < 8u; i += 2)
-          __builtin_nontemporal_store(v2u64{(uint64_t)v[i], (uint64_t)v[i + 1]}, reinterpret_cast<v2u64*>(out + g0 + i));
-      }
-    } else {
-#pragma unroll
-      for (uint32_t i = 0; i < 8u; ++i)
-        if (have & (1u << i)) out[g0 + i] = v[i];
+      out[q0 + i] = (OutT)val;
     }
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
@@ -2773,7 +2766,8 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   pa.nblocks = nblocks;
   pa.count_only = count_only;
   const uint64_t waves_needed = (nranges + kMapWaves - 1) / kMapWaves;
-  const unsigned grid = (unsigned)(waves_needed < (uint64_t)c->cus ? waves_needed : (uint64_t)c->cus);
+  const uint64_t wgs = (uint64_t)c->cus * kMapPerCU;
+  const unsigned grid = (unsigned)(waves_needed < wgs ? waves_needed : wgs);
   const uint64_t* tlo = c->d_tab;
   const uint64_t* thi = c->d_tab + n;
   const uint64_t* tr0 = c->d_tab + 2 * n;
@@ -2858,7 +2852,8 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   pa.nranges = nranges;
   pa.map_ticket = m.ticket;
   const uint64_t waves_needed = (nranges + kMapWaves - 1) / kMapWaves;
-  const unsigned grid = (unsigned)(waves_needed < (uint64_t)c->cus ? waves_needed : (uint64_t)c->cus);
+  const uint64_t wgs = (uint64_t)c->cus * kMapPerCU;
+  const unsigned grid = (unsigned)(waves_needed < wgs ? waves_needed : wgs);
   const uint64_t* tlo = c->d_tab;
   const uint64_t* thi = c->d_tab + n;
   const uint64_t* tr0 = c->d_tab + 2 * n;
@@ -3325,7 +3320,7 @@ int dp_timing_read(dp_ctx* c, double* total_ms, uint64_t* launches) {
 }
 
 int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slots, int* waves) {
-#ifdef DP_PROF
+#ifdef DP_STAMPS
   if (!c || !host_words) return fail(DP_ERR_INVALID, "dp_debug_profile: null argument");
   const uint64_t n = n_words < (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots ? n_words
                                                                                  : (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;

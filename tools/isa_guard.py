@@ -7,7 +7,7 @@ returning `buffer_atomic_* … sc0`) into register(s) R until a wait that the lo
 vector-memory operations issued after it), no instruction may read or write R (dataflow over the
 kernel's basic blocks, tracking the ordered queue of outstanding vector-memory operations).  Usage: python tools/isa_guard.py [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
 (without an argument it compiles the kernel with -save-temps into a temp dir; DP_DEFINES=A=1,B adds -D's).
-It also fails if a scan kernel has a scratch segment (register spills to memory).
+It also fails if any kernel has a scratch segment (register spills or private arrays in memory).
 """
 from __future__ import annotations
 
@@ -160,13 +160,12 @@ def check(asm_path: str):
 
 
 def scratch(asm_path: str):
-    """Scan kernels with a private (scratch) segment: register spills to memory.  A spill reload in the
-    coordinator queues behind the CU's input stream (8 look-back windows did this: FASTA -2 %)."""
+    """Kernels with a private (scratch) segment: register spills or private arrays in memory.  A spill reload in
+    the coordinator queues behind the CU's input stream (8 look-back windows did this: FASTA -2 %); a private
+    array in the placement kernel forced a wait on its prefetched spill words (round 3)."""
     text = open(asm_path).read()
     out = []
     for m in re.finditer(r"\.amdhsa_kernel (\S+)(.*?)\.end_amdhsa_kernel", text, re.S):
-        if "scan_kernel" not in m.group(1) and "map_kernel" not in m.group(1):
-            continue
         sz = re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", m.group(2))
         if sz and int(sz.group(1)) > 0:
             out.append((m.group(1), int(sz.group(1))))

@@ -1,7 +1,7 @@
-"""Section times of one fasta_place_kernel launch (profiling build: tools/build_variants.py prof=DP_PROF), next to
+"""Section times of one fasta_place_kernel launch (profiling build: tools/build_variants.py prof2=DP_PROF2), next to
 the map kernel's wave end times, in microseconds from the map kernel's first wave start.
 
-    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof.so python tools/place_timeline.py [--size BYTES]
+    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof2.so python tools/place_timeline.py [--size BYTES]
 
 Per placement block: 0 start (after its ticket), 1 range summaries loaded + wave scans, 2 block scan done,
 3 block prefix resolved (look-back), 4 events staged, 5 output written, 6 dense rescans done.
