@@ -1690,18 +1690,14 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
   __shared__ uint32_t s_grp[kGrpQ];
   const uint32_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
   const uint32_t G = gridDim.x;
-  uint32_t claimed = 0, run = 0, pend = 0;           // wave 0: steps with a group; the pending claim's size
+  // The first two steps are static (groups blockIdx.x and G + blockIdx.x), so the first loads go out at once;
+  // the ticket hands out groups from 2G on, its first claim issued in step 0 like every later one.
+  uint32_t claimed = 2, run = 0, pend = 0;           // wave 0: steps with a group; the pending claim's size
   uint32_t claim_res = 0;
-  if (wave == 0) {                                    // before any load: the claim is waited for at once
-    uint32_t u = atomic_add_nowait(M.ticket, (uint32_t)DP_MAP_RUN);
-    asm volatile("s_waitcnt vmcnt(0)" : "+v"(u) :: "memory");
-    u = G + rfl(u);
-    if (lane == 0) {
-      s_grp[0] = blockIdx.x;
-      for (uint32_t i = 0; i < (uint32_t)DP_MAP_RUN; ++i) s_grp[1 + i] = u + i;
-    }
+  if (threadIdx.x == 0) {
+    s_grp[0] = blockIdx.x;
+    s_grp[1] = G + blockIdx.x;
   }
-  claimed = 1 + DP_MAP_RUN;
   __syncthreads();
   // (the host launches at most one workgroup per group, so s_grp[0] = blockIdx.x < ngroups)
   uint32_t r = s_grp[0] * kMapWaves + (uint32_t)wave;
@@ -1780,7 +1776,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
       }
       if (h == kBufs - 1 && pend) {                   // the wait above covered the claim: its value is back
         asm volatile("" : "+v"(claim_res) :: "memory");
-        const uint32_t u = G + rfl(claim_res);
+        const uint32_t u = 2u * G + rfl(claim_res);
         if (lane == 0)
           for (uint32_t i = 0; i < pend; ++i) s_grp[(claimed + i) % kGrpQ] = u + i;
         claimed += pend;
