@@ -320,12 +320,13 @@ class ScanContext:
         check(self.lib.dp_timing_read(self.handle, ctypes.byref(ms), ctypes.byref(n)))
         return float(ms.value), int(n.value)
 
-    def forms(self) -> Tuple[bool, int]:
-        """(FASTA index as two kernels, largest newline launch in bytes that runs as two kernels)."""
+    def forms(self) -> Tuple[int, int]:
+        """(FASTA index form: 2 fused map + placement, 1 two kernels, 0 one-pass; largest newline launch in
+        bytes that runs as two kernels)."""
         f = ctypes.c_int(0)
         d = ctypes.c_uint64(0)
         check(self.lib.dp_scan_forms(self.handle, ctypes.byref(f), ctypes.byref(d)))
-        return bool(f.value), int(d.value)
+        return int(f.value), int(d.value)
 
     def geometry(self) -> Tuple[int, int]:
         g = ctypes.c_int(0)

@@ -429,3 +429,59 @@ def test_delim_u16_blocks(ctx, base):
         bounds = np.arange(j0, ((base + n - 1) >> 16) + 1, dtype=np.uint64) << np.uint64(16)
         assert np.array_equal(tab[1:], np.searchsorted(exp, bounds[1:]).astype(np.uint64))
         assert ends[-1] == nd
+
+
+def _form_ctx(form):
+    from dataplug_amd.scan import ScanContext
+    os.environ["DP_FASTA_FORM"] = str(form)
+    try:
+        c = ScanContext(0)
+    finally:
+        del os.environ["DP_FASTA_FORM"]
+    assert c.forms()[0] == form, c.forms()
+    return c
+
+
+# sizes around the fused form's geometry: 1 group (16 ranges of 16 KiB), fewer groups than workgroups,
+# one placement block (64 groups) +- a range, several blocks, a partial last group
+_FORM_SIZES = [1, 5_000, 16 * 16384 - 7, 16 * 16384 + 1, 64 * 16 * 16384 - 1, 64 * 16 * 16384 + 16385,
+               (9 << 20) + 333, (300 << 20) + 17]
+
+
+@pytest.mark.parametrize("size", _FORM_SIZES)
+def test_fasta_forms_equal(size):
+    """The fused map + placement kernel (the default), the two-kernel form and the one-pass kernel give the
+    oracle's pairs and chunk ends, on plans that cut ranges, groups and blocks, also through a capacity retry."""
+    ctxs = [_form_ctx(f) for f in (2, 1, 0)]
+    try:
+        rng = np.random.default_rng(size)
+        a = synth.fasta(size, size % 97) if size > 4096 else _adversarial("dense", size, 3)
+        for div in (1, 3, 64):
+            plan = cpu_ref.chunk_plan(len(a), max(1, math.ceil(len(a) / div)))
+            exp = dpref.fasta_pairs(a, plan)
+            off = int(rng.integers(0, 16))
+            for c in ctxs:
+                pairs, cend = _gpu_pairs(c, a, plan, u64=bool(div == 3), offset=off)
+                np.testing.assert_array_equal(pairs.astype(np.uint64), exp)
+                # a capacity below the count: the kernel clamps its stores, reports the count, and the retry fits
+                buf = c.workspace("t_in", len(a) + 64)
+                p2, _, cend2 = c.fasta_index(buf.ptr + off, len(a), 0, len(a), plan, cap=max(1, len(exp) // 3))
+                np.testing.assert_array_equal(p2.astype(np.uint64), exp)
+                assert np.array_equal(cend2, cend)
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_fused_form_repeated_launches_and_sizes():
+    """Back-to-back fused launches of different sizes on one context: the block counters and both tickets are
+    put back for the next launch by the kernel itself (no per-launch memset)."""
+    c = _form_ctx(2)
+    try:
+        for i, size in enumerate([(40 << 20) + 1, 70_000, (40 << 20) + 1, 16 * 16384, (17 << 20) + 5] * 3):
+            a = synth.fasta(size, i)
+            plan = cpu_ref.chunk_plan(len(a), math.ceil(len(a) / (1 + i % 5)))
+            pairs, _ = _gpu_pairs(c, a, plan, offset=i % 16)
+            np.testing.assert_array_equal(pairs.astype(np.uint64), dpref.fasta_pairs(a, plan))
+    finally:
+        c.close()

@@ -19,7 +19,7 @@ import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "dataplug_amd", "csrc", "dpscan.hip")
-KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1(?:11scan_kernelILi[01]ELi[012]EE|10map_kernelILi[01]EE)\w*):", re.M)
+KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1(?:11scan_kernelILi[01]ELi[012]EE|10map_kernelILi[01]ELi(?:n1|[01])EE)\w*):", re.M)
 
 
 def compile_asm() -> str:
@@ -45,10 +45,17 @@ BRANCH_RE = re.compile(r"^s_(cbranch_\w+|branch)\s+(\.?\w+)")
 def _blocks(body: str):
     """Split a kernel body into basic blocks: (label, [instructions], successors)."""
     blocks, cur, label = [], [], "<entry>"
+    in_asm = False
     for line in body.splitlines():
+        if "#ASMSTART" in line:
+            in_asm = True
+        elif "#ASMEND" in line:
+            in_asm = False
         s = line.split(";")[0].strip()
         if not s:
             continue
+        if in_asm and not s.endswith(":"):
+            s += " @asm"                          # written by hand (inline asm), not by the compiler
         if s.endswith(":"):
             blocks.append([label, cur])
             label, cur = s[:-1], []
@@ -104,9 +111,9 @@ def _scan(ins, q, problems, k):
         pending = frozenset().union(*q) if q else frozenset()
         if VMEM_RE.match(op):
             # hand-waited destinations: the input buffer loads and the returning (sc0) ticket atomic
-            # (global atomics: only the map kernel's inline-asm claim is hand-waited; the compiler waits for its own)
+            # (global atomics: only the inline-asm claims are hand-waited; the compiler waits for its own)
             if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]) or \
-                    (op.startswith("global_atomic") and "sc0" in toks[1:] and "map_kernel" in k):
+                    (op.startswith("global_atomic") and "sc0" in toks[1:] and "@asm" in toks[1:]):
                 dst = regs(toks[1])
                 srcs = set()
                 for t in toks[2:]:
@@ -137,7 +144,7 @@ def check(asm_path: str):
     text = open(asm_path).read()
     problems = []
     kernels = KERNEL_RE.findall(text)
-    assert len(kernels) == 7, kernels
+    assert len(kernels) == 9, kernels
     for k in kernels:
         body = text[text.index(k + ":") + len(k) + 1:]
         body = body[:body.index(".Lfunc_end")]

@@ -14,7 +14,7 @@ python3 -c "
 import json,sys
 for f in sys.argv[1:]:
     d=json.load(open(f)); r=d['roofline']
-    print(f.split('/')[-1], d['value'], r['kernel_avg_us'], r['frac'], r.get('frac_of_measured_peak'), r.get('frac_of_mixed_peak'), d['verified_bit_exact'], d.get('cpu_baseline',{}).get('value'))
+    print(f.split('/')[-1], d['value'], r['kernel_avg_us'], r['frac'], r.get('frac_of_measured_peak'), r.get('frac_of_mixed_ref'), d['verified_bit_exact'], (d.get('cpu_baseline') or {}).get('value'))
 " $O/bench_fasta.json $O/bench_csv.json $O/bench_vcf.json
 step size-sweep
 timeout -k 10 300 python -u tools/size_sweep.py --sizes-gib 0.0625,0.25,0.5,1,2,4,8 > $O/size_sweep.log 2>&1 || { tail -20 $O/size_sweep.log; exit 1; }

@@ -7,6 +7,8 @@
 //      workgroup's 16 ranges) goes out as one contiguous run, all 16 waves storing it together after a
 //      workgroup barrier (the scan's output of one unit is one contiguous run too)
 //   D  like C, with the run's stores issued before the next step's loads are waited on
+//   E  like D, storing every 4th step the last 4 steps' runs (bigger write bursts)
+//   F  like D, storing the previous step's run (writes one step behind the reads)
 // Total (read + write) bytes / kernel time, best of `reps`, HIP events.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_mix tools/ubench_mix.hip && ./tools/ubench_mix [GiB]
 #include <hip/hip_runtime.h>
@@ -110,17 +112,24 @@ __global__ void __launch_bounds__(1024) mix_kernel(const uint4* __restrict__ in,
 #pragma unroll
       for (int i = 0; i < kHalf; ++i) x ^= b[i].x ^ b[i].y ^ b[i].z ^ b[i].w;
       acc ^= x;
-      if constexpr (V == 3) {
+      if constexpr (V >= 3) {
 #pragma unroll
         for (int i = 0; i < kHalf; ++i) b[i] = ld(pn + (kHalf + i) * 64);
       }
       if (lane == 0) s_x[wave] = x;
       __syncthreads();
-      if (out) {
-        // the group's run [e(16g), e(16g + 16)) stored by all 1024 threads together
-        const uint64_t e0 = e_of(g * 16, wq16), e1 = e_of(g * 16 + 16 < nranges ? g * 16 + 16 : nranges, wq16);
-        const uint32_t xx = s_x[threadIdx.x & 15];
-        for (uint64_t e = e0 + threadIdx.x; e < e1; e += 1024) st(out + e, uint4{xx, (uint32_t)e, (uint32_t)g, acc});
+      // V 2/3: this step's group; V 4: every 4th step, the last 4 steps' groups (one run of 4 groups, strided
+      // by the grid: 4 separate runs); V 5: the previous step's group (stores one step behind the reads)
+      const bool go = V == 4 ? (((g - blockIdx.x) / gridDim.x) % 4 == 3 || gn >= ngroups) : (V == 5 ? g >= gridDim.x + blockIdx.x || gn >= ngroups : true);
+      if (out && go) {
+        const int nb = V == 4 ? 4 : (V == 5 && gn >= ngroups && g >= gridDim.x ? 2 : 1);
+        for (int k = 0; k < nb; ++k) {
+          const uint64_t gg = V == 5 ? (gn >= ngroups && k == 1 ? g : g - gridDim.x) : g - (uint64_t)k * gridDim.x;
+          if (gg > g || (V == 5 && gg >= ngroups)) continue;
+          const uint64_t e0 = e_of(gg * 16, wq16), e1 = e_of(gg * 16 + 16 < nranges ? gg * 16 + 16 : nranges, wq16);
+          const uint32_t xx = s_x[threadIdx.x & 15];
+          for (uint64_t e = e0 + threadIdx.x; e < e1; e += 1024) st(out + e, uint4{xx, (uint32_t)e, (uint32_t)gg, acc});
+        }
       }
       if constexpr (V == 2) {
 #pragma unroll
@@ -178,12 +187,14 @@ int main(int argc, char** argv) {
   for (double w : ws) {
     const uint64_t wq16 = (uint64_t)(w * 65536.0 * 1024.0);   // 16-byte elements per range x 65536
     const uint64_t wbytes = (nranges * wq16 >> 16) * 16;
-    float t[4];
+    float t[6];
     t[0] = run<0>(in, nranges, w > 0 ? out : nullptr, wq16, sink, grid, 8);
     t[1] = run<1>(in, nranges, w > 0 ? out : nullptr, wq16, sink, grid, 8);
     t[2] = run<2>(in, nranges, w > 0 ? out : nullptr, wq16, sink, grid, 8);
     t[3] = run<3>(in, nranges, w > 0 ? out : nullptr, wq16, sink, grid, 8);
-    for (int v = 0; v < 4; ++v)
+    t[4] = run<4>(in, nranges, w > 0 ? out : nullptr, wq16, sink, grid, 8);
+    t[5] = run<5>(in, nranges, w > 0 ? out : nullptr, wq16, sink, grid, 8);
+    for (int v = 0; v < 6; ++v)
       printf("{\"variant\": \"%c\", \"write_per_read\": %.3f, \"us\": %.1f, \"read_TBps\": %.3f, \"total_TBps\": %.3f}\n",
              'A' + v, w, t[v] * 1e3, bytes / (t[v] * 1e-3) / 1e12, (bytes + wbytes) / (t[v] * 1e-3) / 1e12);
   }
