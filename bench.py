@@ -374,15 +374,11 @@ def load_traffic(args, size, kernel):
 
 
 # ------------------------------------------------------------------------------------------ FASTA
-# The FASTA index is the map kernel and the placement kernel (libdpscan), timed as one span by
-# HIP events around both.  A/B forms: DP_FASTA_FORM=2 (the fused map + placement kernel, one launch) and
-# DP_FASTA_FORM=0 or DP_FASTA_ONEPASS=1 (round 2's one-pass look-back kernel).
+# The FASTA index is two kernels (libdpscan: the map over 16 KiB ranges, then the placement); their HIP-event
+# span is one "launch" (DP_FASTA_ONEPASS=1: round 2's one-pass look-back kernel, for A/B runs)
 _ONEPASS = os.environ.get("DP_FASTA_ONEPASS", "0") not in ("", "0")
-_FORM = 0 if _ONEPASS else {"0": 0, "2": 2}.get(os.environ.get("DP_FASTA_FORM", "1"), 1)
-FASTA_KERNEL = {0: "scan_kernel<FASTA>",
-                1: "map_kernel<FASTA> + fasta_place_kernel (one HIP-event span)",
-                2: "map_kernel<FASTA, fused placement> (one launch)"}[_FORM]
-FASTA_PMC_KERNELS = {0: "scan_kernel<0", 1: "map_kernel<0, -1>,fasta_place_kernel", 2: "map_kernel<0, 0>"}[_FORM]
+FASTA_KERNEL = "scan_kernel<FASTA>" if _ONEPASS else "map_kernel<FASTA> + fasta_place_kernel (one HIP-event span)"
+FASTA_PMC_KERNELS = "scan_kernel<0" if _ONEPASS else "map_kernel<0>,fasta_place_kernel"
 
 
 class FastaSpec:

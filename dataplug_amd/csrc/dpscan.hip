@@ -1594,12 +1594,6 @@ constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 
 #ifndef DP_MAP_TAIL        // ... and one group per claim once within DP_MAP_TAIL x G groups of the end
 #define DP_MAP_TAIL 3
 #endif
-#ifndef DP_FUSED_STATIC    // fused form, A/B only: static first two groups (a placement may then wait on a
-#define DP_FUSED_STATIC 0  // workgroup not yet started: not deadlock-free with other grids on the GPU)
-#endif
-#ifndef DP_FUSED_FENCE     // fused form: acquire fence (L2 invalidate) before a block's placement reads
-#define DP_FUSED_FENCE 1
-#endif
 
 struct MapArgs {
   const uint8_t* base;         // 16-byte aligned; coordinates relative to it
@@ -1609,7 +1603,6 @@ struct MapArgs {
   unsigned int* ticket;        // (DP_MAP_DYN) next group to claim; zeroed by the placement kernel
   unsigned int* place_ticket;  // [2] the placement kernel's block ticket, zeroed here
   uint32_t delim;              // DELIM: the delimiter byte x4
-  unsigned int* blk_done;      // (fused) per placement block: its groups whose records and spill are out
 };
 
 // Range r of the chunk table (ranges of kWaveBytes in each chunk's aligned coordinates): the Geo of a
@@ -1661,293 +1654,17 @@ __device__ __forceinline__ uint32_t atomic_add_nowait(unsigned int* p, uint32_t 
   return old;
 }
 
-// One lane-0 atomic add whose result is not needed, issued like atomic_add_nowait (exec narrowed inside the asm,
-// no compiler-inserted wait; counted by vmcnt like a store).
-__device__ __forceinline__ void atomic_add_noret(unsigned int* p, uint32_t v) {
-  uint64_t save;
-  asm volatile("s_mov_b64 %0, exec\n\t"
-               "s_mov_b64 exec, 1\n\t"
-               "global_atomic_add %1, %2, off\n\t"
-               "s_mov_b64 exec, %0"
-               : "=&s"(save) : "v"(p), "v"(v) : "memory");
-}
-// A 16-byte store made visible device-wide when it completes (two agent-scope relaxed atomic stores: written
-// through the XCD's L2), for the fused kernel, whose placement reads records and spill words written by
-// workgroups on other XCDs in the same launch.
-__device__ __forceinline__ void st_agent16(void* p, const uint4& v) {
-  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
-  __hip_atomic_store(q, (unsigned long long)v.x | ((unsigned long long)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(q + 1, (unsigned long long)v.z | ((unsigned long long)v.w << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // The second half of a range record: where the range lies (aligned coordinates) and its chunk bounds relative to
 // it, so the placement needs no chunk-table lookup: {wbase lo, wbase hi, lo_w | hi_w << 16, 0}.
 __device__ __forceinline__ uint4 range_geo_rec(const Geo& g) {
   return uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32), g.lo_u | (g.hi_u << 16), 0u};
 }
 
-// Wave-wide (64-lane) inclusive scan of range functions, lane 0 farthest.
-__device__ __forceinline__ Func32 f32_wave_scan(Func32 f) {
-  f = f32_then(f32_dpp<kRowShr1, 0xF>(f), f);
-  f = f32_then(f32_dpp<kRowShr2, 0xF>(f), f);
-  f = f32_then(f32_dpp<kRowShr4, 0xF>(f), f);
-  f = f32_then(f32_dpp<kRowShr8, 0xF>(f), f);
-  f = f32_then(f32_dpp<kRowBcast15, 0xA>(f), f);
-  f = f32_then(f32_dpp<kRowBcast31, 0xC>(f), f);
-  return f;
-}
-
-struct PlaceArgs {
-  const uint4* rec;
-  const uint16_t* spill;
-  uint64_t nranges, nblocks;
-  int count_only;              // no output buffer: counts, chunk ends and pending only
-  unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
-};
-
-// LDS of one placement block (the fused kernel overlays it on the map's event lists)
-struct PlaceShared {
-  Func32 wagg[kPlaceBlock / kWave];
-  Func32 wex[kPlaceBlock / kWave];
-  uint64_t P;
-  uint32_t S, ndense, anydense, blk;
-  unsigned long long lo, hi;                          // the block's output run
-  uint32_t dense[kPlaceBlock];
-  uint64_t dP[kPlaceBlock];
-  uint32_t dS[kPlaceBlock];
-  // the block's output slots are one contiguous run: staged here, then written with coalesced 16-byte stores
-  uint4 stage[kStageBytes / 16];
-};
-
-// One placement block b (1024 range records): every thread of the workgroup takes part; ends with a barrier,
-// so the caller may reuse `ps` at once.
-template <int OUT64>
-__device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const ScanArgs& A, uint32_t b, PlaceShared& ps) {
-  typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
-  constexpr int kPW = kPlaceBlock / kWave;           // 16 waves
-  const int lane = __lane_id();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  OutT* s_stage = reinterpret_cast<OutT*>(ps.stage);
-  if (threadIdx.x == 0) {
-    ps.ndense = 0;
-    ps.lo = 0;
-    ps.hi = 0;
-    ps.anydense = 0;
-  }
-  __syncthreads();
-#ifdef DP_STAMPS
-  // per block (profiling build): realtime stamps at its sections, in g_prof past the map kernel's words
-  unsigned long long* pst = g_prof + ((uint64_t)(512u + (b & 511u)) * kProfWaves) * kProfSlots;
-#define PLACE_STAMP(i) do { if (threadIdx.x == 0 && b < 512u) pst[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define PLACE_STAMP(i) do {} while (0)
-#endif
-  PLACE_STAMP(0);
-  const uint64_t r = (uint64_t)b * kPlaceBlock + threadIdx.x;
-  const bool valid = r < PA.nranges;
-  uint4 rc = uint4{0u, 0u, 2u, 0u};                   // identity: no count, state kept
-  uint4 rg = uint4{0u, 0u, 0u, 0u};
-  if (valid) {
-    rc = PA.rec[2 * r];
-    rg = PA.rec[2 * r + 1];
-  }
-  const uint32_t cF = rc.x & 0xFFFFu, cT = rc.x >> 16, fl = rc.z;
-  // what the placement needs besides the prefix is loaded now, under the scan and the look-back: the
-  // range's first two spill words (16 events; most ranges have no more)
-  const uint32_t nev = rc.y >> 16;
-  const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
-  uint4 sw0 = uint4{0u, 0u, 0u, 0u}, sw1 = uint4{0u, 0u, 0u, 0u};
-  const uint4* sp = reinterpret_cast<const uint4*>(PA.spill);
-  if (valid && !PA.count_only) {
-    if (!(fl & kFlDense)) {
-      if (nev > 0u) sw0 = sp[spill_word(0u, r, PA.nranges)];
-      if (nev > 8u) sw1 = sp[spill_word(1u, r, PA.nranges)];
-    }
-  }
-  const Func32 f{cF, cT, fl & 1u, (fl >> 1) & 1u};
-  const Func32 inc = f32_wave_scan(f);
-  const Func32 ex = Func32{dpp32<kWaveShr1, 0xF>(inc.cF, 0u), dpp32<kWaveShr1, 0xF>(inc.cT, 0u),
-                           dpp32<kWaveShr1, 0xF>(inc.sF, 0u), dpp32<kWaveShr1, 0xF>(inc.sT, 1u)};
-  if (lane == kWave - 1) ps.wagg[wave] = inc;
-  PLACE_STAMP(1);
-  __syncthreads();
-  if (wave == 0) {
-    Func32 w = lane < kPW ? ps.wagg[lane] : Func32{0, 0, 0, 1};
-    Func32 wi = w;
-    wi = f32_then(f32_dpp<kRowShr1, 0xF>(wi), wi);
-    wi = f32_then(f32_dpp<kRowShr2, 0xF>(wi), wi);
-    wi = f32_then(f32_dpp<kRowShr4, 0xF>(wi), wi);
-    wi = f32_then(f32_dpp<kRowShr8, 0xF>(wi), wi);
-    const Func32 we = f32_dpp<kRowShr1, 0xF>(wi);
-    if (lane < kPW) ps.wex[lane] = we;
-    const Func agg{(uint32_t)__builtin_amdgcn_readlane((int)wi.cF, kPW - 1),
-                   (uint32_t)__builtin_amdgcn_readlane((int)wi.cT, kPW - 1),
-                   (uint32_t)__builtin_amdgcn_readlane((int)wi.sF, kPW - 1) & 1u,
-                   (uint32_t)__builtin_amdgcn_readlane((int)wi.sT, kPW - 1) & 1u};
-    // the block's exclusive prefix: a decoupled look-back over the block descriptors
-    uint64_t P = 0;
-    uint32_t S = 0;
-    PLACE_STAMP(2);
-    if (b > 0) {
-      if (lane == 0) st_desc(&A.desc[b], pack_agg(agg) | A.epoch);
-      const uint32_t W = lb_span(b, kNoUnit);
-      uint64_t t0 = 0;
-      for (uint32_t spins = 0;; ++spins) {
-        uint64_t d[kLbPer];
-        lb_load(A, b, W, lane, d);
-        if (lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S)) break;
-        if (wait_expired(spins, t0)) {
-          if (lane == 0) atomicOr(A.err, kErrTimeout);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    const uint64_t P_incl = P + (S ? agg.cT : agg.cF);
-    const uint32_t S_out = S ? agg.sT : agg.sF;
-    if (lane == 0) {
-      st_desc(&A.desc[b], pack_prefix(P_incl, S_out) | A.epoch);
-      ps.P = P;
-      ps.S = S;
-    }
-    PLACE_STAMP(3);
-  }
-  __syncthreads();
-  const uint64_t Pb = ps.P;
-  const uint32_t Sb = ps.S;
-  // this range's incoming state: the block prefix, then the waves before it, then the lanes before it
-  const Func32 wx = ps.wex[wave];
-  const uint64_t Pw = Pb + (Sb ? wx.cT : wx.cF);
-  const uint32_t Sw = Sb ? wx.sT : wx.sF;
-  uint64_t P = Pw + (Sw ? ex.cT : ex.cF);
-  uint32_t S = (Sw ? ex.sT : ex.sF) & 1u;
-  if (fl & kRecFirst) S = 0u;                         // chunk start: no header pending
-  // this range's output run: slots [b0, b0 + n) (the fix-up of phase_b: drop a start pending from the
-  // previous range, prepend the end of the header pending into it)
-  const uint32_t fn = rc.y & 0xFFFFu;
-  const uint32_t fV = (fl >> 2) & 1u;
-  const uint32_t skip = S & fV;
-  const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
-  const uint64_t b0 = 2 * P - S;
-  // the ranges' runs follow one another in range order: the block's run is [b0 of its first range, end of its
-  // last); a dense range (its count of slots is not in the record) means no staging
-  if (valid && !PA.count_only) {
-    if (fl & kFlDense) ps.anydense = 1u;
-    if (threadIdx.x == 0) ps.lo = b0;
-    if (r + 1 == PA.nranges || threadIdx.x == kPlaceBlock - 1) ps.hi = b0 + nev - skip + pre;
-  }
-  __syncthreads();
-  const uint64_t last = 2 * A.cap - 1;
-  const uint64_t run_lo = ps.lo, run_hi = ps.hi < last + 1 ? ps.hi : last + 1;
-  constexpr uint32_t kVec = 16u / sizeof(OutT);
-  const uint64_t stage0 = run_lo & ~(uint64_t)(kVec - 1u);
-  const bool stage = !PA.count_only && !ps.anydense && run_lo < run_hi &&
-                     (run_hi - stage0) * sizeof(OutT) <= kStageBytes;
-  if (valid && !PA.count_only) {
-    if (fl & kFlDense) {
-      ps.dense[atomicAdd(&ps.ndense, 1u)] = threadIdx.x;
-    } else {
-      const uint64_t obj_off = A.obj_base - A.shift + wbase;
-      const bool near4g = OUT64 == 0 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
-      bool ovf = false;
-      auto emit = [&](uint64_t slot, uint32_t e) {
-        const uint64_t val = obj_off + e + (slot & 1u);
-        if (near4g) ovf |= val > 0xFFFFFFFFull;
-        if (stage) {
-          if (slot <= last) s_stage[slot - stage0] = (OutT)val;
-        } else {
-          put<OutT>(A.out, slot < last ? slot : last, val);
-        }
-      };
-      if (pre) emit(b0, fn - 1u);
-      const uint64_t base_slot = b0 + pre - skip;     // event k goes to base_slot + k (k >= skip)
-      // (the prefetched words by name: selecting among them by index made the compiler keep them in a
-      // private array in scratch, waiting for their loads at once)
-      auto emit8 = [&](const uint4& v, uint32_t k0) {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (uint32_t e = 0; e < 8u; ++e) {
-          const uint32_t k = k0 + e;
-          if (k >= skip && k < nev) emit(base_slot + k, (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu);
-        }
-      };
-      if (nev > 0u) emit8(sw0, 0u);
-      if (nev > 8u) emit8(sw1, 8u);
-      for (uint32_t k0 = 16u; k0 < nev; k0 += 8u) emit8(sp[spill_word(k0 >> 3, r, PA.nranges)], k0);
-      if (ovf) atomicOr(A.err, kErrOverflow);
-    }
-  }
-  __syncthreads();
-  PLACE_STAMP(4);
-  if (stage) {
-    // coalesced copy of the run; its first and last partial 16-byte groups element by element, so that the
-    // neighbouring blocks' slots are never written.  (A header still pending at a chunk end leaves its end
-    // slot unwritten here: the resolve kernel, or the host, writes it afterwards.)
-    OutT* o = reinterpret_cast<OutT*>(A.out);
-    const uint64_t v0 = (run_lo + kVec - 1u) & ~(uint64_t)(kVec - 1u), v1 = run_hi & ~(uint64_t)(kVec - 1u);
-    if (v0 <= v1) {
-      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[q - stage0];
-      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
-      const v4u* src = reinterpret_cast<const v4u*>(s_stage + (v0 - stage0));
-      v4u* dst = reinterpret_cast<v4u*>(o + v0);
-      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[g];
-    } else {                                          // the run lies inside one 16-byte group
-      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
-    }
-  }
-  PLACE_STAMP(5);
-  // per-chunk results, after the output stores (a store here would make the loops above wait for it)
-  if (valid) {
-    const uint64_t P_incl = P + (S ? cT : cF);
-    const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
-    if (fl & kRecLast) {
-      A.chunk_end[rc.w] = P_incl;
-      A.pending[rc.w] = S_out ? (long long)P_incl - 1 : -1ll;
-    }
-    if (r + 1 == PA.nranges) A.total[0] = P_incl;
-  }
-  // dense ranges: one wave each, rescanned from the input with the now known state
-  const uint32_t nd = ps.ndense;
-  if (nd) {
-    // every thread keeps its own (P, S); a wave fetches a dense range's through LDS
-    ps.dP[threadIdx.x] = P;
-    ps.dS[threadIdx.x] = S;
-    __syncthreads();
-    for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
-      const uint32_t t = ps.dense[i];
-      const uint64_t rr = (uint64_t)b * kPlaceBlock + t;
-      const uint4 rq = PA.rec[2 * rr + 1];
-      dense_b<kFasta, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, ps.dP[t], ps.dS[t], lane);
-    }
-  }
-  PLACE_STAMP(6);
-#undef PLACE_STAMP
-  __syncthreads();
-}
-
-constexpr uint32_t kGroupsPerBlock = kPlaceBlock / kMapWaves;   // map groups (16 ranges) per placement block
-struct MapLds {
-  uint16_t sev[kMapWaves][kSpillCap];
-};
-struct FusedLds {                     // the placement phase reuses the event lists' LDS
-  union {
-    uint16_t sev[kMapWaves][kSpillCap];
-    PlaceShared ps;
-  };
-};
-
-// FUSED < 0: the map kernel of the two-kernel form.  FUSED = 0 / 1 (FASTA, uint32 / uint64 pairs): the fused
-// form: the same map, then every workgroup places blocks of 1024 ranges, claimed in order from
-// a ticket once their 64 groups have been counted in (blk_done): no second launch, and the placement of the
-// early blocks overlaps the map's tail.
-template <int MODE, int FUSED = -1>
+template <int MODE>
 __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
                                                                 const uint64_t* __restrict__ tab_hi,
-                                                                const uint64_t* __restrict__ tab_r0,
-                                                                PlaceArgs PA, ScanArgs A) {
-  static_assert(FUSED < 0 || (MODE == kFasta && DP_MAP_DYN), "fused form: FASTA with claimed groups");
-  __shared__ __attribute__((aligned(16))) typename std::conditional<(FUSED >= 0), FusedLds, MapLds>::type lds;
-  auto& sev = lds.sev;
+                                                                const uint64_t* __restrict__ tab_r0) {
+  __shared__ __attribute__((aligned(16))) uint16_t sev[kMapWaves][kSpillCap];
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
@@ -1958,7 +1675,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
   uint16_t* evw = sev[wave];
   // the placement kernel that follows claims its blocks from this ticket: it starts from zero (no memset
   // launch, no end-of-kernel counter; the placement kernel zeroes this kernel's own ticket in turn)
-  if (FUSED < 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     M.place_ticket[0] = 0u;
     M.place_ticket[1] = 0u;
   }
@@ -1975,23 +1692,13 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
   const uint32_t G = gridDim.x;
   // The first two steps are static (groups blockIdx.x and G + blockIdx.x), so the first loads go out at once;
   // the ticket hands out groups from 2G on, its first claim issued in step 0 like every later one.
-  // Fused form: the first two groups are claimed too (one waited claim), so every group belongs to a running
-  // workgroup and a placement that waits for a block's groups never waits on a workgroup not yet started.
   uint32_t claimed = 2, run = 0, pend = 0;           // wave 0: steps with a group; the pending claim's size
   uint32_t claim_res = 0;
-  const uint32_t claim_base = FUSED >= 0 && !DP_FUSED_STATIC ? 0u : 2u * G;   // first group the ticket hands out
   if (threadIdx.x == 0) {
-    if constexpr (FUSED >= 0 && !DP_FUSED_STATIC) {
-      const uint32_t u = atomicAdd(M.ticket, 2u);
-      s_grp[0] = u;
-      s_grp[1] = u + 1u;
-    } else {
-      s_grp[0] = blockIdx.x;
-      s_grp[1] = G + blockIdx.x;
-    }
+    s_grp[0] = blockIdx.x;
+    s_grp[1] = G + blockIdx.x;
   }
   __syncthreads();
-  uint32_t steps = 0;                                // steps run (fused: the last two are counted in after the loop)
   // (the host launches at most one workgroup per group, so s_grp[0] = blockIdx.x < ngroups)
   uint32_t r = s_grp[0] * kMapWaves + (uint32_t)wave;
 #elif DP_MAP_SYNC
@@ -2067,17 +1774,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         claim_res = atomic_add_nowait(M.ticket, run);
         pend = run;
       }
-      if constexpr (FUSED >= 0) {
-        // count in the group of step it - 2: every wave's records and spill stores of that step are older than
-        // a buffer wait it passed in step it - 1 (all waves did, by this step's barrier), so they are out
-        if (h == 0 && wave == 0 && it >= 2u) {
-          const uint32_t gs = s_grp[(it - 2u) % kGrpQ];
-          if (gs < ngroups) atomic_add_noret(&M.blk_done[gs / kGroupsPerBlock], 1u);
-        }
-      }
       if (h == kBufs - 1 && pend) {                   // the wait above covered the claim: its value is back
         asm volatile("" : "+v"(claim_res) :: "memory");
-        const uint32_t u = claim_base + rfl(claim_res);
+        const uint32_t u = 2u * G + rfl(claim_res);
         if (lane == 0)
           for (uint32_t i = 0; i < pend; ++i) s_grp[(claimed + i) % kGrpQ] = u + i;
         claimed += pend;
@@ -2088,8 +1787,16 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
 #pragma unroll
       for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
       if constexpr (MODE == kFasta) {
+#ifndef DP_MAP_NOSCAN
         if (interior) fasta_rows<true>(x, b[h].la, h, lo, hi, lane, st, keep);
         else fasta_rows<false>(x, b[h].la, h, lo, hi, lane, st, keep);
+#else
+        // timing probe (wrong results): the map's loads, barriers, claims and stores without the row scan
+        uint32_t xs = 0;
+#pragma unroll
+        for (int i = 0; i < kRows; ++i) xs ^= x[i].x ^ x[i].y ^ x[i].z ^ x[i].w;
+        st.cnt += __builtin_amdgcn_readfirstlane((int)xs) == 0x12345 ? 1u : 0u;
+#endif
       } else {
         if (interior) delim_rows<true>(x, h, lo, hi, key, lane, st.nev, keep);
         else delim_rows<false>(x, h, lo, hi, key, lane, st.nev, keep);
@@ -2106,20 +1813,13 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
       if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
       if ((uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
         const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
-        if constexpr (FUSED >= 0) st_agent16(reinterpret_cast<v4u*>(M.spill) + spill_word((uint32_t)lane, r, M.nranges), uint4{v.x, v.y, v.z, v.w});
-        else reinterpret_cast<v4u*>(M.spill)[spill_word((uint32_t)lane, r, M.nranges)] = v;   // re-read soon: cacheable
+        reinterpret_cast<v4u*>(M.spill)[spill_word((uint32_t)lane, r, M.nranges)] = v;   // re-read soon: cacheable
       }
       if (lane == 0 && (g.fl & kGeoValid)) {
         const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
                             ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
-        const uint4 r0 = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
-        if constexpr (FUSED >= 0) {
-          st_agent16(&M.rec[2 * (uint64_t)r], r0);
-          st_agent16(&M.rec[2 * (uint64_t)r + 1], range_geo_rec(g));
-        } else {
-          M.rec[2 * (uint64_t)r] = r0;
-          M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
-        }
+        M.rec[2 * (uint64_t)r] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+        M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
       }
     } else {
       // the range's delimiter count and positions, range-major (the placement gathers consecutive events)
@@ -2142,10 +1842,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     if (lane == 0) lds_add(&s_done[it % 8u], 1u);
 #endif
 #if DP_MAP_DYN
-    if (gnext >= ngroups) {                           // uniform (LDS value read after the barrier)
-      steps = it + 1u;
-      break;
-    }
+    if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
 #elif DP_MAP_SYNC
     if (it + 1 >= steps) break;
 #else
@@ -2156,64 +1853,286 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
   }
   drain_bufs(b);
 #ifdef DP_STAMPS
-  const uint64_t t_map_end = __builtin_amdgcn_s_memrealtime();
-#endif
-#if DP_MAP_DYN
-  if constexpr (FUSED >= 0) {
-    // every wave has waited for all its stores: count in the last two steps' groups, then place blocks
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      for (uint32_t k = steps >= 2u ? steps - 2u : 0u; k < steps; ++k) {
-        const uint32_t gs = s_grp[k % kGrpQ];
-        if (gs < ngroups) atomicAdd(&M.blk_done[gs / kGroupsPerBlock], 1u);
-      }
-    }
-    const uint32_t nblocks = (nranges + kPlaceBlock - 1u) / kPlaceBlock;
-    for (;;) {
-      __syncthreads();                                // the event lists (or the last block's LDS) are free
-      if (threadIdx.x == 0) {
-        uint32_t bk = atomicAdd(&A.ticket[0], 1u);    // blocks in order: a block only waits on lower ones
-        if (bk < nblocks) {
-          // its groups: claimed by running workgroups, which wait on nothing while they map
-          const uint32_t left = ngroups - bk * kGroupsPerBlock;
-          const uint32_t target = left < kGroupsPerBlock ? left : kGroupsPerBlock;
-          uint64_t t0 = 0;
-          for (uint32_t spins = 0; __hip_atomic_load(&M.blk_done[bk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target; ++spins) {
-            if (wait_expired(spins, t0)) {
-              atomicOr(A.err, kErrTimeout);
-              bk = ~0u - 1u;                          // skip it (its records may be incomplete); the host reports
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-          }
-          if (bk < nblocks) __hip_atomic_store(&M.blk_done[bk], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (bk == nblocks + G - 1u) {
-          // the last claim of the launch: every workgroup is past its map claims and its block claims
-          atomicExch(&A.ticket[0], 0u);
-          atomicExch(M.ticket, 0u);
-        }
-        lds.ps.blk = bk;
-      }
-      // records and spill words of other XCDs: drop this XCD's (L2) and this CU's stale lines
-      if (DP_FUSED_FENCE && wave == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      __syncthreads();
-      const uint32_t bk = lds.ps.blk;
-      if (bk == ~0u - 1u) continue;
-      if (bk >= nblocks) break;
-      fasta_place_block<FUSED < 0 ? 0 : FUSED>(PA, A, bk, lds.ps);
-    }
-  }
-#endif
-#ifdef DP_STAMPS
   // per wave: start and end (100 MHz realtime clock), ranges scanned, the XCC it ran on
   if (lane == 0 && blockIdx.x < kProfMaxGrid) {
     unsigned long long* w = g_prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
     w[0] = t_start;
-    w[1] = t_map_end;                                 // the map loop's end (fused: before the placement phase)
+    w[1] = __builtin_amdgcn_s_memrealtime();
     w[2] = n_done;
     w[3] = __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) & 0xFu;   // HW_REG_XCC_ID
   }
 #endif
+}
+
+// Wave-wide (64-lane) inclusive scan of range functions, lane 0 farthest.
+__device__ __forceinline__ Func32 f32_wave_scan(Func32 f) {
+  f = f32_then(f32_dpp<kRowShr1, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowShr2, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowShr4, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowShr8, 0xF>(f), f);
+  f = f32_then(f32_dpp<kRowBcast15, 0xA>(f), f);
+  f = f32_then(f32_dpp<kRowBcast31, 0xC>(f), f);
+  return f;
+}
+
+struct PlaceArgs {
+  const uint4* rec;
+  const uint16_t* spill;
+  uint64_t nranges, nblocks;
+  int count_only;              // no output buffer: counts, chunk ends and pending only
+  unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
+};
+
+// LDS of one placement block
+struct PlaceShared {
+  Func32 wagg[kPlaceBlock / kWave];
+  Func32 wex[kPlaceBlock / kWave];
+  uint64_t P;
+  uint32_t S, ndense, anydense, blk;
+  unsigned long long lo, hi;                          // the block's output run
+  uint32_t dense[kPlaceBlock];
+  uint64_t dP[kPlaceBlock];
+  uint32_t dS[kPlaceBlock];
+  // the block's output slots are one contiguous run: staged here, then written with coalesced 16-byte stores
+  uint4 stage[kStageBytes / 16];
+};
+
+// One placement block b (1024 range records): every thread of the workgroup takes part; ends with a barrier,
+// so the caller may reuse `ps` at once.
+template <int OUT64>
+__device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const ScanArgs& A, uint32_t b, PlaceShared& ps) {
+  typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
+  constexpr int kPW = kPlaceBlock / kWave;           // 16 waves
+  const int lane = __lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  OutT* s_stage = reinterpret_cast<OutT*>(ps.stage);
+  if (threadIdx.x == 0) {
+    ps.ndense = 0;
+    ps.lo = 0;
+    ps.hi = 0;
+    ps.anydense = 0;
+  }
+  __syncthreads();
+#ifdef DP_STAMPS
+  // per block (profiling build): realtime stamps at its sections, in g_prof past the map kernel's words
+  unsigned long long* pst = g_prof + ((uint64_t)(512u + (b & 511u)) * kProfWaves) * kProfSlots;
+#define PLACE_STAMP(i) do { if (threadIdx.x == 0 && b < 512u) pst[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PLACE_STAMP(i) do {} while (0)
+#endif
+  PLACE_STAMP(0);
+  const uint64_t r = (uint64_t)b * kPlaceBlock + threadIdx.x;
+  const bool valid = r < PA.nranges;
+  uint4 rc = uint4{0u, 0u, 2u, 0u};                   // identity: no count, state kept
+  uint4 rg = uint4{0u, 0u, 0u, 0u};
+  if (valid) {
+    rc = PA.rec[2 * r];
+    rg = PA.rec[2 * r + 1];
+  }
+  const uint32_t cF = rc.x & 0xFFFFu, cT = rc.x >> 16, fl = rc.z;
+  // what the placement needs besides the prefix is loaded now, under the scan and the look-back: the
+  // range's first four spill words (32 events).  With two (16 events), a quarter of the configs[1] ranges
+  // (8 headers per 16 KiB, up to 11) needed a third word after the prefix, i.e. one more dependent load in
+  // every block.
+  const uint32_t nev = rc.y >> 16;
+  const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
+  uint4 sw0 = uint4{0u, 0u, 0u, 0u}, sw1 = sw0, sw2 = sw0, sw3 = sw0;
+  const uint4* sp = reinterpret_cast<const uint4*>(PA.spill);
+  if (valid && !PA.count_only) {
+    if (!(fl & kFlDense)) {
+      if (nev > 0u) sw0 = sp[spill_word(0u, r, PA.nranges)];
+      if (nev > 8u) sw1 = sp[spill_word(1u, r, PA.nranges)];
+      if (nev > 16u) sw2 = sp[spill_word(2u, r, PA.nranges)];
+      if (nev > 24u) sw3 = sp[spill_word(3u, r, PA.nranges)];
+    }
+  }
+  const Func32 f{cF, cT, fl & 1u, (fl >> 1) & 1u};
+  const Func32 inc = f32_wave_scan(f);
+  const Func32 ex = Func32{dpp32<kWaveShr1, 0xF>(inc.cF, 0u), dpp32<kWaveShr1, 0xF>(inc.cT, 0u),
+                           dpp32<kWaveShr1, 0xF>(inc.sF, 0u), dpp32<kWaveShr1, 0xF>(inc.sT, 1u)};
+  if (lane == kWave - 1) ps.wagg[wave] = inc;
+  PLACE_STAMP(1);
+  __syncthreads();
+  if (wave == 0) {
+    Func32 w = lane < kPW ? ps.wagg[lane] : Func32{0, 0, 0, 1};
+    Func32 wi = w;
+    wi = f32_then(f32_dpp<kRowShr1, 0xF>(wi), wi);
+    wi = f32_then(f32_dpp<kRowShr2, 0xF>(wi), wi);
+    wi = f32_then(f32_dpp<kRowShr4, 0xF>(wi), wi);
+    wi = f32_then(f32_dpp<kRowShr8, 0xF>(wi), wi);
+    const Func32 we = f32_dpp<kRowShr1, 0xF>(wi);
+    if (lane < kPW) ps.wex[lane] = we;
+    const Func agg{(uint32_t)__builtin_amdgcn_readlane((int)wi.cF, kPW - 1),
+                   (uint32_t)__builtin_amdgcn_readlane((int)wi.cT, kPW - 1),
+                   (uint32_t)__builtin_amdgcn_readlane((int)wi.sF, kPW - 1) & 1u,
+                   (uint32_t)__builtin_amdgcn_readlane((int)wi.sT, kPW - 1) & 1u};
+    // the block's exclusive prefix: a decoupled look-back over the block descriptors
+    uint64_t P = 0;
+    uint32_t S = 0;
+    PLACE_STAMP(2);
+    if (b > 0) {
+      if (lane == 0) st_desc(&A.desc[b], pack_agg(agg) | A.epoch);
+      const uint32_t W = lb_span(b, kNoUnit);
+      uint64_t t0 = 0;
+      for (uint32_t spins = 0;; ++spins) {
+        uint64_t d[kLbPer];
+        lb_load(A, b, W, lane, d);
+        if (lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S)) break;
+        if (wait_expired(spins, t0)) {
+          if (lane == 0) atomicOr(A.err, kErrTimeout);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const uint64_t P_incl = P + (S ? agg.cT : agg.cF);
+    const uint32_t S_out = S ? agg.sT : agg.sF;
+    if (lane == 0) {
+      st_desc(&A.desc[b], pack_prefix(P_incl, S_out) | A.epoch);
+      ps.P = P;
+      ps.S = S;
+    }
+    PLACE_STAMP(3);
+  }
+  __syncthreads();
+  const uint64_t Pb = ps.P;
+  const uint32_t Sb = ps.S;
+  // this range's incoming state: the block prefix, then the waves before it, then the lanes before it
+  const Func32 wx = ps.wex[wave];
+  const uint64_t Pw = Pb + (Sb ? wx.cT : wx.cF);
+  const uint32_t Sw = Sb ? wx.sT : wx.sF;
+  uint64_t P = Pw + (Sw ? ex.cT : ex.cF);
+  uint32_t S = (Sw ? ex.sT : ex.sF) & 1u;
+  if (fl & kRecFirst) S = 0u;                         // chunk start: no header pending
+  // this range's output run: slots [b0, b0 + n) (the fix-up of phase_b: drop a start pending from the
+  // previous range, prepend the end of the header pending into it)
+  const uint32_t fn = rc.y & 0xFFFFu;
+  const uint32_t fV = (fl >> 2) & 1u;
+  const uint32_t skip = S & fV;
+  const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
+  const uint64_t b0 = 2 * P - S;
+  // the ranges' runs follow one another in range order: the block's run is [b0 of its first range, end of its
+  // last); a dense range (its count of slots is not in the record) means no staging
+  if (valid && !PA.count_only) {
+    if (fl & kFlDense) ps.anydense = 1u;
+    if (threadIdx.x == 0) ps.lo = b0;
+    if (r + 1 == PA.nranges || threadIdx.x == kPlaceBlock - 1) ps.hi = b0 + nev - skip + pre;
+  }
+  __syncthreads();
+  PLACE_STAMP(7);
+  const uint64_t last = 2 * A.cap - 1;
+  const uint64_t run_lo = ps.lo, run_hi = ps.hi < last + 1 ? ps.hi : last + 1;
+  constexpr uint32_t kVec = 16u / sizeof(OutT);
+  const uint64_t stage0 = run_lo & ~(uint64_t)(kVec - 1u);
+  const bool stage = !PA.count_only && !ps.anydense && run_lo < run_hi &&
+                     (run_hi - stage0) * sizeof(OutT) <= kStageBytes;
+  if (valid && !PA.count_only) {
+    if (fl & kFlDense) {
+      ps.dense[atomicAdd(&ps.ndense, 1u)] = threadIdx.x;
+    } else {
+      const uint64_t obj_off = A.obj_base - A.shift + wbase;
+      const bool near4g = OUT64 == 0 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+      bool ovf = false;
+      auto emit = [&](uint64_t slot, uint32_t e) {
+        const uint64_t val = obj_off + e + (slot & 1u);
+        if (near4g) ovf |= val > 0xFFFFFFFFull;
+        if (stage) {
+          if (slot <= last) s_stage[slot - stage0] = (OutT)val;
+        } else {
+          put<OutT>(A.out, slot < last ? slot : last, val);
+        }
+      };
+      if (pre) emit(b0, fn - 1u);
+      const uint64_t base_slot = b0 + pre - skip;     // event k goes to base_slot + k (k >= skip)
+      // (the prefetched words by name: selecting among them by index made the compiler keep them in a
+      // private array in scratch, waiting for their loads at once)
+      if (stage && !near4g) {
+        // the common case in 32-bit index arithmetic: event k -> s_stage[sb + k] (sb wraps to -1 when the
+        // run starts with a skipped event: k >= skip keeps the index in range), its value obj_off + e + the
+        // parity of its slot (start or end), slots past the capacity dropped by one bound on k
+        const uint32_t sb = (uint32_t)(base_slot - stage0);
+        const uint64_t room = last + 1u > base_slot ? last + 1u - base_slot : 0u;
+        const uint32_t lim = room < (uint64_t)nev ? (uint32_t)room : nev;
+        const OutT o0 = (OutT)obj_off;
+        const uint32_t par = (uint32_t)base_slot & 1u;
+        auto emit8s = [&](const uint4& v, uint32_t k0) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t e = 0; e < 8u; ++e) {
+            const uint32_t k = k0 + e;
+            const uint32_t ev = (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu;
+            if (k >= skip && k < lim) s_stage[sb + k] = o0 + (OutT)(ev + (par ^ (e & 1u)));
+          }
+        };
+        if (nev > 0u) emit8s(sw0, 0u);
+        if (nev > 8u) emit8s(sw1, 8u);
+        if (nev > 16u) emit8s(sw2, 16u);
+        if (nev > 24u) emit8s(sw3, 24u);
+        for (uint32_t k0 = 32u; k0 < nev; k0 += 8u) emit8s(sp[spill_word(k0 >> 3, r, PA.nranges)], k0);
+      } else {
+        auto emit8 = [&](const uint4& v, uint32_t k0) {
+          const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (uint32_t e = 0; e < 8u; ++e) {
+            const uint32_t k = k0 + e;
+            if (k >= skip && k < nev) emit(base_slot + k, (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu);
+          }
+        };
+        if (nev > 0u) emit8(sw0, 0u);
+        if (nev > 8u) emit8(sw1, 8u);
+        if (nev > 16u) emit8(sw2, 16u);
+        if (nev > 24u) emit8(sw3, 24u);
+        for (uint32_t k0 = 32u; k0 < nev; k0 += 8u) emit8(sp[spill_word(k0 >> 3, r, PA.nranges)], k0);
+      }
+      if (ovf) atomicOr(A.err, kErrOverflow);
+    }
+  }
+  __syncthreads();
+  PLACE_STAMP(4);
+  if (stage) {
+    // coalesced copy of the run; its first and last partial 16-byte groups element by element, so that the
+    // neighbouring blocks' slots are never written.  (A header still pending at a chunk end leaves its end
+    // slot unwritten here: the resolve kernel, or the host, writes it afterwards.)
+    OutT* o = reinterpret_cast<OutT*>(A.out);
+    const uint64_t v0 = (run_lo + kVec - 1u) & ~(uint64_t)(kVec - 1u), v1 = run_hi & ~(uint64_t)(kVec - 1u);
+    if (v0 <= v1) {
+      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+      const v4u* src = reinterpret_cast<const v4u*>(s_stage + (v0 - stage0));
+      v4u* dst = reinterpret_cast<v4u*>(o + v0);
+      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[g];
+    } else {                                          // the run lies inside one 16-byte group
+      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+    }
+  }
+  PLACE_STAMP(5);
+  // per-chunk results, after the output stores (a store here would make the loops above wait for it)
+  if (valid) {
+    const uint64_t P_incl = P + (S ? cT : cF);
+    const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
+    if (fl & kRecLast) {
+      A.chunk_end[rc.w] = P_incl;
+      A.pending[rc.w] = S_out ? (long long)P_incl - 1 : -1ll;
+    }
+    if (r + 1 == PA.nranges) A.total[0] = P_incl;
+  }
+  // dense ranges: one wave each, rescanned from the input with the now known state
+  const uint32_t nd = ps.ndense;
+  if (nd) {
+    // every thread keeps its own (P, S); a wave fetches a dense range's through LDS
+    ps.dP[threadIdx.x] = P;
+    ps.dS[threadIdx.x] = S;
+    __syncthreads();
+    for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
+      const uint32_t t = ps.dense[i];
+      const uint64_t rr = (uint64_t)b * kPlaceBlock + t;
+      const uint4 rq = PA.rec[2 * rr + 1];
+      dense_b<kFasta, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, ps.dP[t], ps.dS[t], lane);
+    }
+  }
+  PLACE_STAMP(6);
+#undef PLACE_STAMP
+  __syncthreads();
 }
 
 template <int OUT64>
@@ -2660,13 +2579,8 @@ struct dp_ctx {
   // two-kernel FASTA workspace: range summaries and event spill slots (grow-only)
   uint4* d_rec = nullptr;
   uint16_t* d_spill = nullptr;
-  unsigned int* d_blk = nullptr;      // fused FASTA form: per placement block, its groups counted in
   uint64_t rec_cap = 0;               // ranges
-  bool blk_dirty = true;              // d_blk must be zeroed before the next fused launch (fresh, or an error)
-  // FASTA form: 1 = map + placement as two kernels (default), 2 = the fused map + placement kernel
-  // (DP_FASTA_FORM=2), 0 = one-pass look-back kernel (DP_FASTA_FORM=0 or DP_FASTA_ONEPASS=1)
-  int fasta_form = 1;
-  bool fasta_onepass = false;
+  bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
   uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
@@ -2894,17 +2808,13 @@ int ensure_ranges(dp_ctx* c, uint64_t nranges) {
   if (nranges > c->rec_cap) {
     if (c->d_rec) HIPCHK(hipFree(c->d_rec));
     if (c->d_spill) HIPCHK(hipFree(c->d_spill));
-    if (c->d_blk) HIPCHK(hipFree(c->d_blk));
     c->d_rec = nullptr;
     c->d_spill = nullptr;
-    c->d_blk = nullptr;
     c->rec_cap = 0;
     const uint64_t cap_r = nranges + nranges / 8 + 64;
     HIPCHK(dev_alloc((void**)&c->d_rec, 2 * cap_r * sizeof(uint4)));
     HIPCHK(dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t)));
-    HIPCHK(dev_alloc((void**)&c->d_blk, (cap_r / kPlaceBlock + 2) * sizeof(unsigned int)));
     c->rec_cap = cap_r;
-    c->blk_dirty = true;
   }
   return DP_OK;
 }
@@ -2957,12 +2867,6 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
   m.place_ticket = a.ticket;
   m.delim = 0;
-  m.blk_done = c->d_blk;
-  if (c->fasta_form == 2 && c->blk_dirty) {
-    // fresh counters (they are put back to zero by the block's placement; an error may leave some set)
-    HIPCHK(hipMemsetAsync(c->d_blk, 0, (c->rec_cap / kPlaceBlock + 2) * sizeof(unsigned int), c->stream));
-    c->blk_dirty = false;
-  }
   PlaceArgs pa;
   pa.map_ticket = m.ticket;
   pa.rec = c->d_rec;
@@ -2984,17 +2888,7 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   hipEvent_t e0;
   rc = ev_begin(c, &e0, ss);
   if (rc) return rc;
-  if (c->fasta_form == 2) {                           // fused: map + placement in one launch
-    if (out_u64)
-      hipLaunchKernelGGL((map_kernel<kFasta, 1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0, pa, a);
-    else
-      hipLaunchKernelGGL((map_kernel<kFasta, 0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0, pa, a);
-    HIPCHK(hipGetLastError());
-    rc = ev_end(c, ss);
-    if (rc) return rc;
-    return scan_leave(c, ss);
-  }
-  hipLaunchKernelGGL((map_kernel<kFasta>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0, pa, a);
+  hipLaunchKernelGGL((map_kernel<kFasta>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   if (out_u64)
     hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
@@ -3061,7 +2955,6 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
   m.place_ticket = a.ticket;
   m.delim = a.delim;
-  m.blk_done = nullptr;
   DPlaceArgs pa;
   pa.rec = c->d_rec;
   pa.spill = c->d_spill;
@@ -3081,7 +2974,7 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   hipEvent_t e0;
   rc = ev_begin(c, &e0, ss);
   if (rc) return rc;
-  hipLaunchKernelGGL((map_kernel<kDelim>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0, PlaceArgs{}, a);
+  hipLaunchKernelGGL((map_kernel<kDelim>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   if (kind == 1)
     hipLaunchKernelGGL((delim_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
@@ -3164,10 +3057,7 @@ int dp_ctx_create(int device, dp_ctx** out) {
   c->grid = c->cus * per_cu;
   if (c->grid > 256) c->grid = 256;   // one look-back window (G <= 256) per unit
   const char* onepass = getenv("DP_FASTA_ONEPASS");
-  const char* form = getenv("DP_FASTA_FORM");
-  if (form) c->fasta_form = atoi(form) == 0 ? 0 : (atoi(form) == 2 ? 2 : 1);
-  if (onepass && atoi(onepass) != 0) c->fasta_form = 0;
-  c->fasta_onepass = c->fasta_form == 0;
+  c->fasta_onepass = onepass && atoi(onepass) != 0;
   // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
   const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
   c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
@@ -3186,7 +3076,6 @@ int dp_ctx_destroy(dp_ctx* c) {
   if (c->d_desc) (void)hipFree(c->d_desc);
   if (c->d_rec) (void)hipFree(c->d_rec);
   if (c->d_spill) (void)hipFree(c->d_spill);
-  if (c->d_blk) (void)hipFree(c->d_blk);
   if (c->d_tab) (void)hipFree(c->d_tab);
   if (c->h_tab) (void)hipHostFree(c->h_tab);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -3325,10 +3214,7 @@ int dp_fasta_result(dp_ctx* c, uint64_t* n_pairs, int64_t* pending, uint64_t* ch
   rc = collect_ctrl(c, 0);
   if (rc) return rc;
   const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
-  if (err) {
-    c->last_tab.clear();                                // the next launch re-uploads err = 0
-    c->blk_dirty = true;                                // and zeroes the fused form's block counters
-  }
+  if (err) c->last_tab.clear();                         // the next launch re-uploads err = 0
   const uint64_t total = c->nchunks ? c->h_tab[c->ctrl_off + 1] : 0;
   if (n_pairs) *n_pairs = total;
   if (pending) memcpy(pending, c->h_tab + c->pend_off, c->nchunks * 8);
@@ -3572,7 +3458,7 @@ int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs) {
 
 int dp_scan_forms(dp_ctx* c, int* fasta_two_kernel, uint64_t* delim_two_kernel_max) {
   if (!c) return fail(DP_ERR_INVALID, "null");
-  if (fasta_two_kernel) *fasta_two_kernel = c->fasta_form;
+  if (fasta_two_kernel) *fasta_two_kernel = c->fasta_onepass ? 0 : 1;
   if (delim_two_kernel_max) *delim_two_kernel_max = c->delim_twopass_max;
   return DP_OK;
 }

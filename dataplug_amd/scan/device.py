@@ -321,7 +321,7 @@ class ScanContext:
         return float(ms.value), int(n.value)
 
     def forms(self) -> Tuple[int, int]:
-        """(FASTA index form: 2 fused map + placement, 1 two kernels, 0 one-pass; largest newline launch in
+        """(FASTA index form: 1 map + placement kernels, 0 one-pass look-back kernel; largest newline launch in
         bytes that runs as two kernels)."""
         f = ctypes.c_int(0)
         d = ctypes.c_uint64(0)

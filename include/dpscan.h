@@ -157,9 +157,8 @@ int dp_debug_profile(dp_ctx* ctx, uint64_t* host_words, uint64_t n_words, int* s
  * FASTA range summaries and spill).  Steady-state calls on warm contexts allocate nothing. */
 int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
 
-/* Which kernels a ctx's scans use: the FASTA index form (1 = map and placement as two kernels, the default;
- * 2 = one launch of the fused map + placement kernel, DP_FASTA_FORM=2; 0 = the one-pass look-back kernel,
- * DP_FASTA_FORM=0 or DP_FASTA_ONEPASS=1), and the largest newline launch (bytes scanned) that runs as two
+/* Which kernels a ctx's scans use: the FASTA index as two kernels (map + placement; 0 = the one-pass
+ * look-back kernel, DP_FASTA_ONEPASS=1), and the largest newline launch (bytes scanned) that runs as two
  * kernels -- larger ones run the one-pass kernel (default 0: always one-pass; DP_DELIM_TWOPASS_MAX sets it). */
 int dp_scan_forms(dp_ctx* ctx, int* fasta_two_kernel, uint64_t* delim_two_kernel_max);
 

@@ -431,28 +431,29 @@ def test_delim_u16_blocks(ctx, base):
         assert ends[-1] == nd
 
 
-def _form_ctx(form):
+
+def _form_ctx(onepass):
     from dataplug_amd.scan import ScanContext
-    os.environ["DP_FASTA_FORM"] = str(form)
+    os.environ["DP_FASTA_ONEPASS"] = "1" if onepass else "0"
     try:
         c = ScanContext(0)
     finally:
-        del os.environ["DP_FASTA_FORM"]
-    assert c.forms()[0] == form, c.forms()
+        del os.environ["DP_FASTA_ONEPASS"]
+    assert c.forms()[0] == (0 if onepass else 1), c.forms()
     return c
 
 
-# sizes around the fused form's geometry: 1 group (16 ranges of 16 KiB), fewer groups than workgroups,
-# one placement block (64 groups) +- a range, several blocks, a partial last group
+# sizes around the two-kernel form's geometry: 1 map group (16 ranges of 16 KiB), fewer groups than
+# workgroups, one placement block (1024 ranges) +- a range, several blocks, a partial last group
 _FORM_SIZES = [1, 5_000, 16 * 16384 - 7, 16 * 16384 + 1, 64 * 16 * 16384 - 1, 64 * 16 * 16384 + 16385,
                (9 << 20) + 333, (300 << 20) + 17]
 
 
 @pytest.mark.parametrize("size", _FORM_SIZES)
 def test_fasta_forms_equal(size):
-    """The fused map + placement kernel (the default), the two-kernel form and the one-pass kernel give the
-    oracle's pairs and chunk ends, on plans that cut ranges, groups and blocks, also through a capacity retry."""
-    ctxs = [_form_ctx(f) for f in (2, 1, 0)]
+    """The two-kernel form (the default) and the one-pass kernel give the oracle's pairs and chunk ends, on
+    plans that cut ranges, groups and blocks, also through a capacity retry."""
+    ctxs = [_form_ctx(False), _form_ctx(True)]
     try:
         rng = np.random.default_rng(size)
         a = synth.fasta(size, size % 97) if size > 4096 else _adversarial("dense", size, 3)
@@ -473,10 +474,10 @@ def test_fasta_forms_equal(size):
             c.close()
 
 
-def test_fused_form_repeated_launches_and_sizes():
-    """Back-to-back fused launches of different sizes on one context: the block counters and both tickets are
-    put back for the next launch by the kernel itself (no per-launch memset)."""
-    c = _form_ctx(2)
+def test_repeated_launches_and_sizes():
+    """Back-to-back launches of different sizes on one context: both kernels' tickets are put back for the
+    next launch by the kernels themselves (no per-launch memset)."""
+    c = _form_ctx(False)
     try:
         for i, size in enumerate([(40 << 20) + 1, 70_000, (40 << 20) + 1, 16 * 16384, (17 << 20) + 5] * 3):
             a = synth.fasta(size, i)

@@ -4,7 +4,8 @@ the map kernel's wave end times, in microseconds from the map kernel's first wav
     DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof2.so python tools/place_timeline.py [--size BYTES]
 
 Per placement block: 0 start (after its ticket), 1 range summaries loaded + wave scans, 2 block scan done,
-3 block prefix resolved (look-back), 4 events staged, 5 output written, 6 dense rescans done.
+3 block prefix resolved (look-back), 7 the block's output run known (two barriers later), 4 events staged,
+5 output written, 6 dense rescans done.
 """
 from __future__ import annotations
 
@@ -50,11 +51,18 @@ def main():
     t0 = mp[:, :, 0][live].min()
     map_end = (mp[:, :, 1][live].max() - t0) / 100.0
     nb = -(-(n // (16 << 10)) // 1024)
-    pl = w[512:512 + min(nb, 512), 0, :7]
+    pl = w[512:512 + min(nb, 512), 0, :8]
     us = (pl - t0) / 100.0
     q = lambda a: [round(float(x), 1) for x in np.percentile(a, [0, 50, 100])]
-    res = {"map_last_wave_end": round(map_end, 1), "blocks": int(len(pl))}
-    names = ["start", "loaded", "scanned", "prefix", "staged", "written", "end"]
+    st = (mp[:, :, 0][live] - t0) / 100.0
+    en = (mp[:, :, 1][live] - t0) / 100.0
+    res = {"map_last_wave_end": round(map_end, 1), "blocks": int(len(pl)),
+           "map_wave_start_q0_50_90_100": [round(float(x), 1) for x in np.percentile(st, [0, 50, 90, 100])],
+           "map_wave_end_q0_10_50_100": [round(float(x), 1) for x in np.percentile(en, [0, 10, 50, 100])]}
+    if len(pl) == 0 or (pl[:, 0] == 0).all():
+        print(json.dumps(res), flush=True)
+        return
+    names = ["start", "loaded", "scanned", "prefix", "staged", "written", "end", "run_bounds"]
     for i, nm in enumerate(names):
         res[nm] = q(us[:, i])
     res["prefix_minus_scanned_med"] = round(float(np.median(us[:, 3] - us[:, 2])), 2)
