@@ -17,11 +17,24 @@ import shutil
 from collections import defaultdict
 
 
+def split_kernels(kernel: str):
+    """Comma-separated kernel names, commas inside template brackets kept ("scan_kernel<1, 2>" is one name)."""
+    out, depth, cur = [], 0, ""
+    for ch in kernel:
+        depth += (ch == "<") - (ch == ">")
+        if ch == "," and depth == 0:
+            out.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    return out + [cur]
+
+
 def counters(path: str, kernel: str):
     """Per-dispatch averages of each counter for one kernel name, or the SUM of those averages over a
     comma-separated list of kernels that make up one launch (the FASTA map + placement kernels)."""
     out = defaultdict(float)
-    for k in kernel.split(","):
+    for k in split_kernels(kernel):
         per = defaultdict(lambda: defaultdict(float))
         for f in glob.glob(os.path.join(path, "**", "*counter_collection.csv"), recursive=True):
             for row in csv.DictReader(open(f)):
