@@ -122,7 +122,16 @@ def launch_mode(args):
         if dev >= device_count():
             log(f"rank {rank}: device {dev} but only {device_count()} device(s) visible")
             sys.exit(2)
-        dist.init_process_group("gloo")
+        # gloo prints "[Gloo] Rank r is connected to ..." on stdout from C++; keep stdout to the ONE JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         return world, rank, [dev], dist
     n = args.gpus
     devs = [int(x) for x in args.devices.split(",")] if args.devices else list(range(n))
