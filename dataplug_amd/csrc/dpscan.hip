@@ -2207,22 +2207,26 @@ struct DPlaceArgs {
   unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
 };
 
+// Round 3: blocks of 64 ranges (one per lane of wave 0) and 16 waves, so a launch has nranges / 64 workgroups:
+// round 2's blocks of 1024 ranges left a 64 MiB CSV launch (466 K entries per block) to four workgroups copying
+// range by range, one dependent load per 64 entries (189 us vs 33 us for the one-pass kernel).  A wave now
+// gathers its four ranges' up to 4 x 512 spill entries with all 32 loads in flight, then stores them.
+constexpr uint32_t kDPlaceRanges = 64;
+constexpr uint32_t kDPlaceWaves = 16;
 template <int OUT64>
-__global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA, ScanArgs A,
-                                                                 const uint64_t* __restrict__ tab_lo,
-                                                                 const uint64_t* __restrict__ tab_hi,
-                                                                 const uint64_t* __restrict__ tab_r0) {
+__global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlaceArgs PA, ScanArgs A,
+                                                                         const uint64_t* __restrict__ tab_lo,
+                                                                         const uint64_t* __restrict__ tab_hi,
+                                                                         const uint64_t* __restrict__ tab_r0) {
   typedef typename std::conditional<OUT64 == 1, uint64_t,
                                     typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
-  constexpr int kPW = kPlaceBlock / kWave;
   constexpr uint32_t kDenseBit = 0x80000000u;
   __shared__ uint32_t s_blk, s_ndense;
-  __shared__ uint32_t s_wsum[kPW];
   __shared__ uint64_t s_P;
-  __shared__ uint32_t s_ex[kPlaceBlock];             // delimiters of the block before range t
-  __shared__ uint32_t s_cnt[kPlaceBlock];            // range t's delimiters (| kDenseBit: not spilled)
-  __shared__ uint64_t s_off[kPlaceBlock];            // object offset of range t's first byte + emit_add
-  __shared__ uint32_t s_dense[kPlaceBlock];
+  __shared__ uint32_t s_ex[kDPlaceRanges];            // delimiters of the block before range t
+  __shared__ uint32_t s_cnt[kDPlaceRanges];           // range t's delimiters (| kDenseBit: not spilled)
+  __shared__ uint64_t s_off[kDPlaceRanges];           // object offset of range t's first byte + emit_add
+  __shared__ uint32_t s_dense[kDPlaceRanges];
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (threadIdx.x == 0) {
@@ -2232,36 +2236,26 @@ __global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA,
   }
   __syncthreads();
   const uint32_t b = s_blk;
-  const uint32_t t = threadIdx.x;
-  const uint64_t r = (uint64_t)b * kPlaceBlock + t;
-  const bool valid = r < PA.nranges;
-  uint4 rc = uint4{0u, 0u, 0u, 0u}, rg = uint4{0u, 0u, 0u, 0u};
-  if (valid) {
-    rc = PA.rec[2 * r];
-    rg = PA.rec[2 * r + 1];
-  }
-  const uint32_t cnt = rc.x, fl = rc.z;
-  const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
-  // block scan of the counts
-  uint32_t inc = cnt;
-  inc += dpp32<kRowShr1, 0xF>(inc, 0u);
-  inc += dpp32<kRowShr2, 0xF>(inc, 0u);
-  inc += dpp32<kRowShr4, 0xF>(inc, 0u);
-  inc += dpp32<kRowShr8, 0xF>(inc, 0u);
-  inc += dpp32<kRowBcast15, 0xA>(inc, 0u);
-  inc += dpp32<kRowBcast31, 0xC>(inc, 0u);
-  if (lane == kWave - 1) s_wsum[wave] = inc;
-  __syncthreads();
   if (wave == 0) {
-    uint32_t w = lane < kPW ? s_wsum[lane] : 0u;
-    uint32_t wi = w;
-    wi += dpp32<kRowShr1, 0xF>(wi, 0u);
-    wi += dpp32<kRowShr2, 0xF>(wi, 0u);
-    wi += dpp32<kRowShr4, 0xF>(wi, 0u);
-    wi += dpp32<kRowShr8, 0xF>(wi, 0u);
-    if (lane < kPW) s_wsum[lane] = wi - w;            // exclusive per wave
-    const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)wi, kPW - 1);
-    uint64_t P = 0;
+    // one range per lane: its count, the block scan, the block prefix (decoupled look-back), per-range results
+    const uint64_t r = (uint64_t)b * kDPlaceRanges + lane;
+    const bool valid = r < PA.nranges;
+    uint4 rc = uint4{0u, 0u, 0u, 0u}, rg = uint4{0u, 0u, 0u, 0u};
+    if (valid) {
+      rc = PA.rec[2 * r];
+      rg = PA.rec[2 * r + 1];
+    }
+    const uint32_t cnt = rc.x, fl = rc.z;
+    const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
+    uint32_t inc = cnt;
+    inc += dpp32<kRowShr1, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr2, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr4, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr8, 0xF>(inc, 0u);
+    inc += dpp32<kRowBcast15, 0xA>(inc, 0u);
+    inc += dpp32<kRowBcast31, 0xC>(inc, 0u);
+    const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
+    uint64_t Pb = 0;
     if (b > 0) {
       if (lane == 0) st_desc(&A.desc[b], pack_count(kStatAgg, total) | A.epoch);
       const uint32_t W = lb_span(b, kNoUnit);
@@ -2269,7 +2263,7 @@ __global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA,
       for (uint32_t spins = 0;; ++spins) {
         uint64_t d[kLbPer];
         lb_load(A, b, W, lane, d);
-        if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P)) break;
+        if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, Pb)) break;
         if (wait_expired(spins, t0)) {
           if (lane == 0) atomicOr(A.err, kErrTimeout);
           break;
@@ -2278,74 +2272,88 @@ __global__ void __launch_bounds__(kPlaceBlock) delim_place_kernel(DPlaceArgs PA,
       }
     }
     if (lane == 0) {
-      st_desc(&A.desc[b], pack_count(kStatPrefix, P + total) | A.epoch);
-      s_P = P;
+      st_desc(&A.desc[b], pack_count(kStatPrefix, Pb + total) | A.epoch);
+      s_P = Pb;
+    }
+    const uint32_t ex = inc - cnt;
+    const uint64_t P = Pb + ex;                       // delimiters of the launch before this range
+    const bool dense = (fl & kFlDense) != 0u;
+    s_ex[lane] = ex;
+    s_cnt[lane] = valid ? (cnt | (dense ? kDenseBit : 0u)) : 0u;
+    s_off[lane] = A.obj_base - A.shift + wbase + A.emit_add;
+    if (valid && dense) s_dense[atomicAdd(&s_ndense, 1u)] = (uint32_t)lane;
+    if (valid) {
+      if (fl & kRecLast) A.chunk_end[rc.w] = P + cnt;
+      if (r + 1 == PA.nranges) A.total[0] = P + cnt;
+      if constexpr (OUT64 == 2) {
+        // the entries before every 64 KiB boundary that starts a range of this chunk (see phase_b)
+        const uint64_t off0 = A.obj_base - A.shift + wbase;
+        const uint64_t j = (off0 >> 16) - A.tab_j0;
+        const bool holds = (rg.z & 0xFFFFu) == 0u && (rg.z >> 16) != 0u;
+        if ((off0 & 0xFFFFull) == 0 && holds && off0 >= (A.tab_j0 << 16) && j < A.tab_n) A.blocktab[j] = P;
+      }
     }
   }
   __syncthreads();
   const uint64_t Pb = s_P;
-  const uint32_t ex = s_wsum[wave] + inc - cnt;
-  const uint64_t P = Pb + ex;                         // delimiters of the launch before this range
-  const bool dense = (fl & kFlDense) != 0u;
-  s_ex[t] = ex;
-  s_cnt[t] = valid ? (cnt | (dense ? kDenseBit : 0u)) : 0u;
-  s_off[t] = A.obj_base - A.shift + wbase + A.emit_add;
-  if (valid && dense) s_dense[atomicAdd(&s_ndense, 1u)] = t;
-  __syncthreads();
-  // output entries of the block: the selected delimiters (global ordinal G = launch ordinal + carry with
-  // G % k == k - 1) go to index G / k - carry / k
-  // A wave copies one range's selected positions at a time: the range's launch ordinals are o0 + e for its
-  // spill entries e, the selected ones (G = o + carry with G % k == k - 1) are e0, e0 + k, ... and land at
-  // consecutive output indexes from q0 = G / k - carry / k. Lanes take consecutive entries, so the spill
-  // loads and the output stores are contiguous per wave instruction.
+  // output entries: the selected delimiters (global ordinal G = launch ordinal + carry with G % k == k - 1)
+  // go to index G / k - carry / k.  A range's launch ordinals are o0 + e for its spill entries e; the selected
+  // ones are e0, e0 + k, ... at consecutive output indexes from q0.  A wave takes one range at a time: lane l
+  // gathers entries l, l + 64, ..., all eight loads issued before the first store (at most 512 entries).
   const uint64_t k = rfl64(A.every_k), carry = rfl64(A.carry);
   const uint64_t cap = A.cap;
   OutT* out = reinterpret_cast<OutT*>(A.out);
   const bool near4g = OUT64 == 0 && !A.wrap32;
   bool ovf = false;
-  const uint16_t* spb = PA.spill + (uint64_t)b * kPlaceBlock * kSpillCap;
-  for (uint32_t tr = (uint32_t)wave; tr < (uint32_t)kPlaceBlock; tr += kPW) {
+  const uint16_t* spb = PA.spill + (uint64_t)b * kDPlaceRanges * kSpillCap;
+  constexpr int kGather = (int)(kSpillCap / kWave);  // 8
+  constexpr int kPer = (int)(kDPlaceRanges / kDPlaceWaves);   // ranges per wave, all gathered at once
+  uint32_t v[kPer][kGather];
+  uint64_t qa[kPer], offa[kPer];
+  uint32_t na[kPer];
+#pragma unroll
+  for (int m = 0; m < kPer; ++m) {
+    const uint32_t tr = (uint32_t)wave + (uint32_t)m * kDPlaceWaves;
     const uint32_t cw = rfl(s_cnt[tr]);
-    if (cw == 0u || (cw & kDenseBit)) continue;      // nothing, or written by the dense rescan
-    const uint64_t o0 = Pb + rfl(s_ex[tr]);
-    const uint64_t off = rfl64(s_off[tr]);
-    const uint16_t* sp = spb + (uint64_t)tr * kSpillCap;
     uint32_t e0 = 0, n = cw, step = 1;
-    uint64_t q0 = o0;
+    uint64_t q0 = Pb + rfl(s_ex[tr]);
     if (k != 1ull) {
-      const uint64_t G0 = o0 + carry;
+      const uint64_t G0 = q0 + carry;
       const uint64_t r0 = k - 1ull - G0 % k;
       e0 = (uint32_t)(r0 < cw ? r0 : cw);
       n = r0 < cw ? (uint32_t)((cw - r0 + k - 1ull) / k) : 0u;
       q0 = (G0 + r0) / k - carry / k;
       step = (uint32_t)k;
     }
-    if (q0 >= cap) continue;
-    if (q0 + n > cap) n = (uint32_t)(cap - q0);
-    for (uint32_t i = (uint32_t)lane; i < n; i += kWave) {
-      const uint64_t val = off + sp[e0 + i * step];
-      if (near4g) ovf |= val > 0xFFFFFFFFull;
-      out[q0 + i] = (OutT)val;
+    if ((cw & kDenseBit) || q0 >= cap) n = 0u;        // written by the dense rescan, or past the capacity
+    else if (q0 + n > cap) n = (uint32_t)(cap - q0);
+    qa[m] = q0;
+    offa[m] = rfl64(s_off[tr]);
+    na[m] = n;
+    const uint16_t* sp = spb + (uint64_t)tr * kSpillCap;
+#pragma unroll
+    for (int j = 0; j < kGather; ++j) {
+      const uint32_t i = (uint32_t)lane + (uint32_t)j * kWave;
+      v[m][j] = i < n ? (uint32_t)sp[e0 + i * step] : 0u;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < kPer; ++m) {
+#pragma unroll
+    for (int j = 0; j < kGather; ++j) {
+      const uint32_t i = (uint32_t)lane + (uint32_t)j * kWave;
+      if (i < na[m]) {
+        const uint64_t val = offa[m] + v[m][j];
+        if (near4g) ovf |= val > 0xFFFFFFFFull;
+        out[qa[m] + i] = (OutT)val;
+      }
     }
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
-  // per-chunk results and the 64 KiB block table, after the output stores
-  if (valid) {
-    if (fl & kRecLast) A.chunk_end[rc.w] = P + cnt;
-    if (r + 1 == PA.nranges) A.total[0] = P + cnt;
-    if constexpr (OUT64 == 2) {
-      // the entries before every 64 KiB boundary that starts a range of this chunk (see phase_b)
-      const uint64_t off0 = A.obj_base - A.shift + wbase;
-      const uint64_t j = (off0 >> 16) - A.tab_j0;
-      const bool holds = (rg.z & 0xFFFFu) == 0u && (rg.z >> 16) != 0u;
-      if ((off0 & 0xFFFFull) == 0 && holds && off0 >= (A.tab_j0 << 16) && j < A.tab_n) A.blocktab[j] = P;
-    }
-  }
-  __syncthreads();
   const uint32_t nd = s_ndense;
-  for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
+  for (uint32_t i = (uint32_t)wave; i < nd; i += kDPlaceWaves) {
     const uint32_t td = s_dense[i];
-    const uint64_t rr = (uint64_t)b * kPlaceBlock + td;
+    const uint64_t rr = (uint64_t)b * kDPlaceRanges + td;
     const uint4 rq = PA.rec[2 * rr + 1];
     dense_b<kDelim, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, Pb + s_ex[td], 0u, lane);
   }
@@ -2528,11 +2536,11 @@ __global__ void __launch_bounds__(1024) stream_rw_kernel(const uint4* __restrict
 // ------------------------------------------------------------------------------------------ host side
 thread_local std::string g_err;
 
-// Newline launches up to this many bytes run as two kernels; larger ones as the one-pass look-back kernel.
-// Default 0: on the CSV/VCF shapes (a newline every 36-80 B) the two-kernel form was 7-25 % slower at 4 and
-// 16 GiB (its placement gathers every position from the spill), so the one-pass kernel stays the newline
-// index; DP_DELIM_TWOPASS_MAX enables the two-kernel form (it wins on sparse newlines: DESIGN.md §4).
-constexpr uint64_t kDelimTwoPassMax = 0;
+// Newline launches up to this many bytes run as two kernels; larger ones as the one-pass look-back kernel
+// (DP_DELIM_TWOPASS_MAX overrides).  Same box, CSV / VCF / FASTA bytes (profiles/r03/delim2/): the two-kernel
+// form is 4-24 % faster up to 512 MiB (the one-pass kernel's ~35-40 us start and tail), the one-pass kernel
+// 2-28 % faster from 1 GiB (the two-kernel form moves every delimiter through the spill: 4 more bytes each).
+constexpr uint64_t kDelimTwoPassMax = 512ull << 20;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -2910,7 +2918,7 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   if (nranges == 0) return DP_OK;
   int rc = ensure_ranges(c, nranges);
   if (rc) return rc;
-  const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
+  const uint64_t nblocks = (nranges + kDPlaceRanges - 1) / kDPlaceRanges;
   rc = ensure_desc(c, nblocks);
   if (rc) return rc;
   if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
@@ -2977,11 +2985,11 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   hipLaunchKernelGGL((map_kernel<kDelim>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   if (kind == 1)
-    hipLaunchKernelGGL((delim_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+    hipLaunchKernelGGL((delim_place_kernel<1>), dim3((unsigned)nblocks), dim3(kWave * kDPlaceWaves), 0, ss, pa, a, tlo, thi, tr0);
   else if (kind == 2)
-    hipLaunchKernelGGL((delim_place_kernel<2>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+    hipLaunchKernelGGL((delim_place_kernel<2>), dim3((unsigned)nblocks), dim3(kWave * kDPlaceWaves), 0, ss, pa, a, tlo, thi, tr0);
   else
-    hipLaunchKernelGGL((delim_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+    hipLaunchKernelGGL((delim_place_kernel<0>), dim3((unsigned)nblocks), dim3(kWave * kDPlaceWaves), 0, ss, pa, a, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   rc = ev_end(c, ss);
   if (rc) return rc;

@@ -159,7 +159,7 @@ int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
 
 /* Which kernels a ctx's scans use: the FASTA index as two kernels (map + placement; 0 = the one-pass
  * look-back kernel, DP_FASTA_ONEPASS=1), and the largest newline launch (bytes scanned) that runs as two
- * kernels -- larger ones run the one-pass kernel (default 0: always one-pass; DP_DELIM_TWOPASS_MAX sets it). */
+ * kernels -- larger ones run the one-pass kernel (default 512 MiB; DP_DELIM_TWOPASS_MAX sets it). */
 int dp_scan_forms(dp_ctx* ctx, int* fasta_two_kernel, uint64_t* delim_two_kernel_max);
 
 /* Launch geometry (for tests/tuning): workgroups of the persistent scan grid, and unit size in bytes. */
