@@ -486,3 +486,57 @@ def test_repeated_launches_and_sizes():
             np.testing.assert_array_equal(pairs.astype(np.uint64), dpref.fasta_pairs(a, plan))
     finally:
         c.close()
+
+
+def _delim_ctx(twopass_max):
+    from dataplug_amd.scan import ScanContext
+    os.environ["DP_DELIM_TWOPASS_MAX"] = str(twopass_max)
+    try:
+        c = ScanContext(0)
+    finally:
+        del os.environ["DP_DELIM_TWOPASS_MAX"]
+    assert c.forms()[1] == twopass_max
+    return c
+
+
+@pytest.mark.parametrize("size", [1, 5_000, 64 * 16384 - 3, 64 * 16384 + 16385, (7 << 20) + 11, (70 << 20) + 5])
+def test_newline_forms_equal(size):
+    """The newline index's two forms (map + 64-range placement blocks, the default up to 512 MiB per launch, and
+    the one-pass kernel) give the oracle's offsets in every output form, with every_k / emit_add / carry, on CSV
+    rows (some ranges over the 512-entry spill slot: dense rescans), a run of newlines and newline-free spans."""
+    two, one = _delim_ctx(1 << 62), _delim_ctx(0)
+    try:
+        a = synth.csv(size, seed=size % 89) if size > 4096 else np.full(size, 10, np.uint8)
+        if size > (1 << 20):
+            a[size // 3: size // 3 + 40_000] = 10                      # every byte a newline: dense ranges
+            a[size // 2: size // 2 + 200_000] = ord("x")               # no newline for 12 ranges
+        n = len(a)
+        d = two.workspace("t_in", n + 64)
+        two.h2d(d.ptr + 3, a)
+        d1 = one.workspace("t_in", n + 64)
+        one.h2d(d1.ptr + 3, a)
+        base = 3
+        full = dpref.delim(a, 0, n)[0] + np.uint64(base)
+        for k, add, carry in ((1, 0, 0), (4, 1, 2), (3, 0, 7)):
+            sel = np.arange(len(full), dtype=np.uint64) + np.uint64(carry)
+            exp = full[(sel % np.uint64(k)) == np.uint64(k - 1)] + np.uint64(add)
+            for mode in (1, 0, 3):
+                outs = []
+                for c, dp in ((two, d.ptr + 3), (one, d1.ptr + 3)):
+                    r = c.delim_ranges(dp, n, base, [(base, base + n)], every_k=k, emit_add=add, carry=carry,
+                                       out_mode=mode)
+                    outs.append(r)
+                    if mode == 3:
+                        low, _, _, tab = r
+                        j0 = base >> 16
+                        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right")
+                        got = ((blk.astype(np.uint64) - np.uint64(1) + np.uint64(j0)) << np.uint64(16)) | low.astype(np.uint64)
+                        if k == 1 and add == 0:
+                            assert np.array_equal(got, exp)
+                    else:
+                        assert np.array_equal(r[0].astype(np.uint64), exp), (k, add, carry, mode)
+                assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
+                assert np.array_equal(np.asarray(outs[0][2]), np.asarray(outs[1][2]))
+    finally:
+        two.close()
+        one.close()
