@@ -136,8 +136,9 @@ int dp_find_delim(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t 
 
 /* Calibration (async, timed like the scans): read `bytes` (16-byte multiple) once with the best plain
  * streaming kernel measured (the read-only ceiling next to the roofline fraction); dp_stream_rw also writes
- * write_q16 / 65536 output bytes per input byte (contiguous, non-temporal), the DELIM index's traffic mix.
- * blocks_per_cu <= 0: one 1024-thread workgroup per CU. */
+ * write_q16 / 65536 output bytes per input byte (contiguous non-temporal runs, one per workgroup step of 16
+ * ranges of 16 KiB; whole 16 KiB ranges only), the newline index's traffic mix: a same-run reference for it,
+ * not a bound.  blocks_per_cu <= 0: one 1024-thread workgroup per CU. */
 int dp_stream_read(dp_ctx* ctx, const void* d_buf, uint64_t bytes, int blocks_per_cu);
 int dp_stream_rw(dp_ctx* ctx, const void* d_in, uint64_t bytes, void* d_out, uint32_t write_q16, int blocks_per_cu);
 
