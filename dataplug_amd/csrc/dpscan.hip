@@ -1588,8 +1588,8 @@ constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 
 #ifndef DP_MAP_DYN         // map kernel: groups of 16 ranges claimed from a ticket (0: static striding)
 #define DP_MAP_DYN 1
 #endif
-#ifndef DP_MAP_RUN         // groups per claim ...
-#define DP_MAP_RUN 2
+#ifndef DP_MAP_RUN         // groups per claim (1: 677-681 us vs 687-689 us per 4 GiB with 2, same box,
+#define DP_MAP_RUN 1       // profiles/r03/knob_ab/) ...
 #endif
 #ifndef DP_MAP_TAIL        // ... and one group per claim once within DP_MAP_TAIL x G groups of the end
 #define DP_MAP_TAIL 3
