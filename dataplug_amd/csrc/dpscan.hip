@@ -1591,6 +1591,9 @@ constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 
 #ifndef DP_MAP_RUN         // groups per claim (1: 677-681 us vs 687-689 us per 4 GiB with 2, same box,
 #define DP_MAP_RUN 1       // profiles/r03/knob_ab/) ...
 #endif
+#ifndef DP_MAP_AHEAD       // steps claimed ahead of the current one (2: step it + 2 has its group by the
+#define DP_MAP_AHEAD 2     // barrier of step it + 1, where its loads are issued)
+#endif
 #ifndef DP_MAP_TAIL        // ... and one group per claim once within DP_MAP_TAIL x G groups of the end
 #define DP_MAP_TAIL 3
 #endif
@@ -1755,7 +1758,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     const uint32_t gnext = s_grp[(it + 1) % kGrpQ];
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
     // wave 0 keeps two steps claimed ahead: step it + 2 needs its group by the barrier of step it + 1
-    const bool do_claim = wave == 0 && claimed < it + 3u && s_grp[(claimed - 1) % kGrpQ] < ngroups;
+    const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD && s_grp[(claimed - 1) % kGrpQ] < ngroups;
     if (do_claim) run = s_grp[(claimed - 1) % kGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
 #else
     const uint32_t rn = r + NW;
