@@ -2214,6 +2214,9 @@ struct DPlaceArgs {
 // round 2's blocks of 1024 ranges left a 64 MiB CSV launch (466 K entries per block) to four workgroups copying
 // range by range, one dependent load per 64 entries (189 us vs 33 us for the one-pass kernel).  A wave now
 // gathers its four ranges' up to 4 x 512 spill entries with all 32 loads in flight, then stores them.
+#ifndef DP_DPLACE_TICKET   // newline placement blocks in ticket order (0: blockIdx order, A/B only)
+#define DP_DPLACE_TICKET 1
+#endif
 constexpr uint32_t kDPlaceRanges = 64;
 constexpr uint32_t kDPlaceWaves = 16;
 template <int OUT64>
@@ -2234,7 +2237,11 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) PA.map_ticket[0] = 0u;
+#if DP_DPLACE_TICKET
     s_blk = atomicAdd(&A.ticket[0], 1u);             // claim order: a block only waits on lower blocks
+#else
+    s_blk = blockIdx.x;                              // A/B only: relies on in-order workgroup dispatch
+#endif
     s_ndense = 0;
   }
   __syncthreads();
