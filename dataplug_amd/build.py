@@ -1,9 +1,22 @@
-"""Build libdpscan.so in-tree for gfx950:  python -m dataplug_amd.build"""
+"""Build libdpscan.so in-tree for gfx950:  python -m dataplug_amd.build
+
+The scan library is compiled with -save-temps and the ISA guard (dataplug_amd/isa_guard.py) checks that exact
+device assembly: every kernel, no touched in-flight load destination, no scratch segment.  Only a library that
+passes is installed (os.replace after the guard), next to a stamp ``<lib>.isa.json`` holding the guard's report
+and the installed file's sha256; the loader (scan/_lib.py) refuses a library whose stamp is missing, failed or
+belongs to another file.
+"""
 from __future__ import annotations
 
+import hashlib
+import json
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
+
+from dataplug_amd import isa_guard
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "dpscan.hip")
@@ -15,20 +28,53 @@ GZ_OUT = os.path.join(HERE, "lib", "libdpgz.so")            # host-side gzip acc
 ARCH = os.environ.get("DPSCAN_ARCH", "gfx950")
 
 
-def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=SRC) -> str:
+class IsaGuardError(RuntimeError):
+    """The compiled kernels fail the ISA guard: the library is not installed."""
+
+
+def sha256_file(path: str) -> str:
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def stamp_path(lib: str) -> str:
+    return lib + ".isa.json"
+
+
+def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=SRC, guard=None) -> str:
+    """Compile ``src`` for gfx950, run the ISA guard on its assembly, install it at ``out`` if it passes.
+    ``guard`` defaults to on except for the DP_PROF diagnostics build (whose section timers spill by design:
+    it is never the shipped library, and its stamp records the failed guard)."""
     out = out or (OUT_PROF if prof else OUT)
+    guard = (not prof) if guard is None else guard
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-Wno-unused-result", "-o", out + ".tmp", src]
-    if prof:
-        cmd.insert(1, "-DDP_PROF")
-    for d in defines:                      # tuning variants, e.g. DP_RING=5 (tools/probe_perf.py)
-        cmd.insert(1, f"-D{d}")
-    if verbose:
-        cmd.append("-Rpass-analysis=kernel-resource-usage")
-    subprocess.run(cmd, check=True)
-    os.replace(out + ".tmp", out)
+    defs = (["DP_PROF"] if prof else []) + list(defines)  # tuning variants, e.g. DP_RING=5 (tools/probe_perf.py)
+    with tempfile.TemporaryDirectory(prefix="dpscan_build_") as d:
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
+               "-Wno-unused-result", "-save-temps"] + [f"-D{x}" for x in defs] + ["-o", os.path.join(d, "lib.so"),
+                                                                                  os.path.abspath(src)]
+        if verbose:
+            cmd.append("-Rpass-analysis=kernel-resource-usage")
+        subprocess.run(cmd, check=True, cwd=d)
+        stem = os.path.splitext(os.path.basename(src))[0]
+        asm = os.path.join(d, f"{stem}-hip-amdgcn-amd-amdhsa-{ARCH}.s")
+        rep = isa_guard.verify(asm)
+        print(f"ISA guard: {rep['result']} ({len(rep['kernels'])} kernels, {os.path.basename(out)})",
+              file=sys.stderr if rep["result"] != "ok" else sys.stdout, flush=True)
+        if guard and rep["result"] != "ok":
+            raise IsaGuardError(f"{out} not installed: the ISA guard failed on its assembly: "
+                                f"{rep['violations'][:3]} {rep['scratch'][:3]} missing {rep['missing_kernels']}")
+        shutil.copyfile(os.path.join(d, "lib.so"), out + ".tmp")
+        rep.update(so_sha256=sha256_file(out + ".tmp"), asm_sha256=sha256_file(asm), defines=defs, arch=ARCH,
+                   source=os.path.relpath(os.path.abspath(src), os.path.dirname(HERE)), guard_enforced=guard)
+        with open(stamp_path(out) + ".tmp", "w") as f:
+            json.dump(rep, f, indent=1)
+        os.replace(stamp_path(out) + ".tmp", stamp_path(out))
+        os.replace(out + ".tmp", out)
     return out
 
 

@@ -2608,6 +2608,7 @@ struct dp_ctx {
   uint64_t carry = 0;
   std::vector<uint64_t> range_map;    // out_mode 3: caller range of each internal range (split at 64 KiB)
   uint64_t pend_off = 0, ctrl_off = 0;
+  int last_form = -1;                 // the last scan's form on this ctx: 0 one-pass, 1 two kernels
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -2792,6 +2793,12 @@ int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
     c->desc_epoch = 0;
   }
   a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
+  // ctrl[4] is the one-pass kernel's unit ticket {next unit, workgroups finished}, which its last workgroup puts
+  // back to zero; a two-kernel launch leaves its placement block ticket there ({nblocks, 0}, zeroed only by the
+  // next map kernel).  A form switch usually re-uploads the table anyway (its unit size differs), but a
+  // one-pass launch after a two-kernel one never relies on that
+  if (c->last_form == 1) HIPCHK(hipMemsetAsync(c->d_tab + c->ctrl_off + 4, 0, 8, c->stream));
+  c->last_form = 0;
   const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
   DeviceSerial& ds = g_serial[c->device];
   std::lock_guard<std::mutex> lock(ds.m);
@@ -2831,7 +2838,14 @@ int ensure_ranges(dp_ctx* c, uint64_t nranges) {
     c->rec_cap = 0;
     const uint64_t cap_r = nranges + nranges / 8 + 64;
     HIPCHK(dev_alloc((void**)&c->d_rec, 2 * cap_r * sizeof(uint4)));
-    HIPCHK(dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t)));
+    const hipError_t e = dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t));
+    if (e != hipSuccess) {                             // leave no half-allocated workspace behind
+      (void)hipFree(c->d_rec);
+      c->d_rec = nullptr;
+      c->d_spill = nullptr;
+      return fail(DP_ERR_HIP, std::string("workspace of ") + std::to_string(nranges) + " ranges: " +
+                                  hipGetErrorString(e));
+    }
     c->rec_cap = cap_r;
   }
   return DP_OK;
@@ -2861,7 +2875,13 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   a.nunits = nranges;
   a.desc = c->d_desc;
   a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
-  static const bool probe_count_only = getenv("DP_PROBE_PLACE_COUNT_ONLY") != nullptr;   // perf probe only
+#ifdef DP_STAMPS
+  // perf probe of the diagnostics build only (the placement without its stores): never in the shipped library,
+  // where a stray environment variable would otherwise leave the caller's index unwritten
+  static const bool probe_count_only = getenv("DP_PROBE_PLACE_COUNT_ONLY") != nullptr;
+#else
+  constexpr bool probe_count_only = false;
+#endif
   const int count_only = (cap == 0 || d_out == nullptr || probe_count_only);
   if (count_only) {
     d_out = c->d_tab + c->ctrl_off + 2;
@@ -2876,6 +2896,7 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
   a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
   a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  c->last_form = 1;
   MapArgs m;
   m.base = a.base;
   m.nchunks = n;
@@ -2964,6 +2985,7 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
   a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
   a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  c->last_form = 1;
   MapArgs m;
   m.base = a.base;
   m.nchunks = n;
@@ -3272,6 +3294,10 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   if (out_mode < 0 || out_mode > 3)
     return fail(DP_ERR_INVALID, "out_mode must be 0 (uint32), 1 (uint64), 2 (uint32 low words) or 3 (uint16 + blocks)");
   if (nranges == 0 || !ranges) return fail(DP_ERR_INVALID, "no ranges");
+  // the block table holds delimiter ordinals before each 64 KiB boundary: entry indexes only when every
+  // delimiter is an entry, and the low 16 bits locate an entry in its block only without an added offset
+  if (out_mode == 3 && (every_k != 1 || emit_add != 0))
+    return fail(DP_ERR_INVALID, "out_mode 3 needs every_k == 1 and emit_add == 0");
   for (uint64_t i = 0; i < nranges; ++i) {
     if (ranges[2 * i + 1] > ranges[2 * i] && !d_buf) return fail(DP_ERR_INVALID, "null buffer");
     if (ranges[2 * i + 1] < ranges[2 * i]) return fail(DP_ERR_INVALID, "range end before its start");
@@ -3413,19 +3439,27 @@ int dp_stream_rw(dp_ctx* c, const void* d_in, uint64_t bytes, void* d_out, uint3
   if (rc) return rc;
   const int bpc = blocks_per_cu > 0 ? blocks_per_cu : 1;
   c->last_tab.clear();   // the table area is the (practically never written) sink
+  // on the device's scan stream like a scan: a calibration never shares the chip with a scan of this process
+  DeviceSerial& ds = g_serial[c->device];
+  std::lock_guard<std::mutex> lock(ds.m);
+  hipStream_t ss = nullptr;
+  rc = scan_enter(c, ds, &ss);
+  if (rc) return rc;
   hipEvent_t e0;
-  rc = ev_begin(c, &e0, c->stream);
+  rc = ev_begin(c, &e0, ss);
   if (rc) return rc;
   if (write_q16)
-    hipLaunchKernelGGL(stream_rw_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, c->stream,
+    hipLaunchKernelGGL(stream_rw_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, ss,
                        reinterpret_cast<const uint4*>(d_in), bytes / 16, reinterpret_cast<uint4*>(d_out),
                        (uint64_t)write_q16, reinterpret_cast<unsigned*>(c->d_tab));
   else
-    hipLaunchKernelGGL(stream_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, c->stream,
+    hipLaunchKernelGGL(stream_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, ss,
                        reinterpret_cast<const uint4*>(d_in), bytes / 16, nullptr, 0ull,
                        reinterpret_cast<unsigned*>(c->d_tab));
   HIPCHK(hipGetLastError());
-  return ev_end(c, c->stream);
+  rc = ev_end(c, ss);
+  if (rc) return rc;
+  return scan_leave(c, ss);
 }
 
 int dp_stream_read(dp_ctx* c, const void* d_buf, uint64_t bytes, int blocks_per_cu) {

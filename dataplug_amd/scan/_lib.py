@@ -2,11 +2,16 @@
 
 The library is built in-tree (``__graft_entry__.build()`` / ``python -m dataplug_amd.build``) into
 ``dataplug_amd/lib/libdpscan.so``.  There is NO fallback: if the library is missing or cannot be loaded
-the import of anything that scans raises ``DPScanUnavailable``.
+the import of anything that scans raises ``DPScanUnavailable``.  Nor is a library loaded that the build's
+ISA guard did not pass: ``<lib>.isa.json`` (written by ``dataplug_amd.build``) must say "ok" and carry the
+sha256 of the very file being loaded (a library whose kernels touch an in-flight load destination can fault
+the GPU).
 """
 from __future__ import annotations
 
 import ctypes
+import hashlib
+import json
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -90,6 +95,7 @@ def load():
     if not os.path.exists(LIB_PATH):
         raise DPScanUnavailable(f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; "
                                 f"g.build()'` (hipcc --offload-arch=gfx950)")
+    guard_check(LIB_PATH)
     try:
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover - depends on the ROCm runtime being present
@@ -100,6 +106,24 @@ def load():
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+def guard_check(path: str) -> dict:
+    """The ISA-guard stamp of ``path`` (raises DPScanUnavailable unless it passed for exactly this file)."""
+    stamp = path + ".isa.json"
+    try:
+        with open(stamp) as f:
+            rep = json.load(f)
+    except (OSError, ValueError) as e:
+        raise DPScanUnavailable(f"{path} has no ISA-guard stamp ({e}): rebuild it with python -m dataplug_amd.build") from e
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    if rep.get("result") != "ok" or rep.get("so_sha256") != h.hexdigest():
+        raise DPScanUnavailable(f"{path}: ISA guard {rep.get('result')!r}, stamp for sha256 "
+                                f"{str(rep.get('so_sha256'))[:12]}, file {h.hexdigest()[:12]}: not loaded")
+    return rep
 
 
 def check(rc: int) -> None:

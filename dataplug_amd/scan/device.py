@@ -75,6 +75,7 @@ class ScanContext:
         self.device = int(device)
         self._bufs = {}
         self._pinned = {}
+        self._get_pool = None
 
     # ---------------------------------------------------------------- memory
     def workspace(self, name: str, nbytes: int) -> DeviceBuffer:
@@ -96,6 +97,16 @@ class ScanContext:
             b = PinnedBuffer(max(int(nbytes), 1 << 16))
             self._pinned[name] = b
         return b
+
+    def get_pool(self, threads: int):
+        """The context's persistent pool of ranged-GET threads (``fetch_to_device``): created once per context,
+        i.e. once per (host thread, device) — a persistent per-GPU worker reuses it for every object."""
+        import concurrent.futures as cf
+        if self._get_pool is None or self._get_pool._max_workers < threads:
+            if self._get_pool is not None:
+                self._get_pool.shutdown(wait=True)
+            self._get_pool = cf.ThreadPoolExecutor(threads, thread_name_prefix=f"dpscan-get{self.device}")
+        return self._get_pool
 
     def h2d_async(self, dst: int, src_ptr: int, nbytes: int) -> None:
         """Async copy from pinned host memory on the context stream (caller keeps the source alive)."""
@@ -335,6 +346,9 @@ class ScanContext:
         return int(g.value), int(u.value)
 
     def close(self) -> None:
+        if self._get_pool is not None:
+            self._get_pool.shutdown(wait=True)
+            self._get_pool = None
         if self.handle:
             for b in list(self._bufs.values()) + list(self._pinned.values()):
                 b.free()

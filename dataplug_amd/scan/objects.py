@@ -22,13 +22,19 @@ from ..storage.ranges import GET_PART as _GET_PART, GET_THREADS as _GET_THREADS,
 from .device import ScanContext, device_count, get_context
 
 _HALO0 = 64 << 10             # first look-ahead window when a header line crosses the fetched bytes
-# bytes one FASTA launch holds in HBM at most: a GPU's chunk group larger than this (an object far beyond
-# 288 GB x GPUs, or a small budget set for tests) is scanned in several passes of whole chunks
+# HBM one FASTA launch may hold: a GPU's chunk group whose bytes plus scan workspace exceed this (an object far
+# beyond 288 GB x GPUs, or a small budget set for tests) is scanned in several passes of whole chunks
 MAX_LAUNCH_BYTES = 64 << 30
+# the two-kernel scan's workspace per input byte (libdpscan ensure_ranges): a 32-byte record and a 1 KiB spill
+# slot per 16 KiB range, grown with 1/8 headroom -- 7.3 % on top of the input bytes
+WORKSPACE_PER_BYTE = (2 * 16 + 512 * 2) / 16384 * 1.125
 
 
 def max_launch_bytes() -> int:
-    return int(os.environ.get("DATAPLUG_AMD_MAX_LAUNCH_BYTES", MAX_LAUNCH_BYTES))
+    """Input bytes one launch may span: the HBM budget (``DATAPLUG_AMD_MAX_LAUNCH_BYTES``) less the workspace
+    the scan allocates for them."""
+    budget = int(os.environ.get("DATAPLUG_AMD_MAX_LAUNCH_BYTES", MAX_LAUNCH_BYTES))
+    return max(1, int(budget / (1.0 + WORKSPACE_PER_BYTE)))
 
 
 DEVICES_ATTR = "_dataplug_devices"
@@ -94,11 +100,17 @@ def fetch_to_device(ctx: ScanContext, storage, bucket: str, key: str, lo: int, h
         read_range_into(storage, bucket, key, lo + a, lo + min(n, a + part), view[a:], part=part, threads=1)
         return a
 
-    with cf.ThreadPoolExecutor(min(threads, len(starts))) as ex:
-        futs = [ex.submit(one, a) for a in starts]
+    ex = ctx.get_pool(threads)                # the context's persistent GET threads (no pool per call)
+    futs = [ex.submit(one, a) for a in starts]
+    try:
         for f in cf.as_completed(futs):       # H2D issued from this (the context's) thread only
             a = f.result()
             ctx.h2d_async(d_ptr + a, host.ptr + a, min(n, a + part) - a)
+    except BaseException:
+        for f in futs:                        # a failed GET: no part may still land in the staging buffer
+            f.cancel()
+        cf.wait(futs)
+        raise
     return host
 
 

@@ -113,7 +113,9 @@ int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
  *   ranges at multiples of 2^32 and read each page's first entry from range_end).
  *   out_mode 3: uint16 low words plus a 64 KiB block table -- the stored CSV/VCF index (<key>.lines and
  *   <key>.lines.blocks), a quarter of the uint64 index's bytes:
- *     - d_out[0 .. n_out) are uint16: entry i = (offset_i + emit_add) & 0xFFFF;
+ *     - every_k must be 1 and emit_add 0 (DP_ERR_INVALID otherwise): every delimiter is an entry, so the
+ *       table's delimiter counts are entry indexes, and each low word locates its own byte;
+ *     - d_out[0 .. n_out) are uint16: entry i = offset_i & 0xFFFF;
  *     - the block table follows at byte offset (2 * cap + 15) & ~15 of d_out: uint64 tab[j] for
  *       j = 0 .. J-1, J = ((last - 1) >> 16) - j0 + 1 (1 if last == first), j0 = first >> 16, where first =
  *       ranges[0] and last = ranges[2 * nranges - 1]; tab[j] = entries (relative to this launch) before
@@ -138,7 +140,8 @@ int dp_find_delim(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t 
  * streaming kernel measured (the read-only ceiling next to the roofline fraction); dp_stream_rw also writes
  * write_q16 / 65536 output bytes per input byte (contiguous non-temporal runs, one per workgroup step of 16
  * ranges of 16 KiB; whole 16 KiB ranges only), the newline index's traffic mix: a same-run reference for it,
- * not a bound.  blocks_per_cu <= 0: one 1024-thread workgroup per CU. */
+ * not a bound.  blocks_per_cu <= 0: one 1024-thread workgroup per CU.  Like the scans, they run on the
+ * device's scan stream, so within a process they never overlap a scan (another process's grids still may). */
 int dp_stream_read(dp_ctx* ctx, const void* d_buf, uint64_t bytes, int blocks_per_cu);
 int dp_stream_rw(dp_ctx* ctx, const void* d_in, uint64_t bytes, void* d_out, uint32_t write_q16, int blocks_per_cu);
 

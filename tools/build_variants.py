@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import subprocess  # noqa: E402
 
-from dataplug_amd.build import HERE, SRC, build  # noqa: E402
+from dataplug_amd.build import HERE, SRC, IsaGuardError, build  # noqa: E402
 
 
 def main(specs):
@@ -35,20 +35,19 @@ def main(specs):
                 fh.write(subprocess.run(["git", "show", f"{rev}:dataplug_amd/csrc/dpscan.hip"], check=True,
                                         capture_output=True, text=True).stdout)
         jobs.append((defines, prof, out, src))
+    # build() runs the ISA guard on each variant's own assembly and installs nothing that fails it: a variant
+    # whose compiled code touches an in-flight load destination (or spills) can corrupt addresses and fault the GPU
+
+    def one(j):
+        try:
+            return build(defines=j[0], prof=j[1], out=j[2], src=j[3], guard=True)
+        except IsaGuardError as e:
+            if os.path.exists(j[2]):
+                os.remove(j[2])
+            return f"REFUSED {j[2]}: {e}"
     with ThreadPoolExecutor(4) as ex:
-        for out in ex.map(lambda j: build(defines=j[0], prof=j[1], out=j[2], src=j[3]), jobs):
+        for out in ex.map(one, jobs):
             print(out)
-    # a variant whose compiled code touches an in-flight load destination (or spills to scratch) can corrupt
-    # addresses and fault the GPU: it is deleted, never run (tools/isa_guard.py on the same defines)
-    guard = os.path.join(os.path.dirname(os.path.abspath(__file__)), "isa_guard.py")
-    for defines, prof, out, src in jobs:
-        if src != SRC:
-            continue
-        env = dict(os.environ, DP_DEFINES=",".join(defines + (["DP_PROF"] if prof else [])))
-        r = subprocess.run([sys.executable, guard], env=env, capture_output=True, text=True)
-        if r.returncode != 0:
-            os.remove(out)
-            print(f"REFUSED {out}: ISA guard failed ({r.stdout.strip().splitlines()[-1]})")
     for j in jobs:
         if j[3] != SRC:
             os.remove(j[3])
