@@ -1,37 +1,45 @@
 #!/usr/bin/env python3
-"""Benchmark: device-resident FASTA header-index scan (BASELINE.json configs[1]) on 1..N MI355X.
+"""Benchmark: the device-resident record-boundary index of BASELINE.json on 1..N MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--size BYTES] [--no-cpu-baseline]
-    python bench.py --workload csv|vcf ...    (BASELINE configs[2] / configs[3]: newline index)
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--legs fasta,csv,vcf] [--no-cpu-baseline]
+    python bench.py --workload csv|vcf ...        (one newline leg alone as the headline line)
 
-The workload is ONE synthetic FASTA object of N x 4 GiB (N = --gpus) with the reference's chunk plan at
-chunk_size = 1 GiB (size / 4N: 4 chunks per GPU, the configs[1] plan at N = 1), split over the N GPUs by
-the product's multi-GPU split (``scan.objects.fasta_groups``: contiguous chunk groups, one per GPU, no
-collective; the reference runs the chunks as independent map jobs, preprocess.py:39-51).  Each GPU holds
-its group's bytes (+ a 64 KiB look-ahead halo) in HBM before the timed region.
+ONE JSON line (rank 0).  Its headline is BASELINE configs[1], the FASTA '>' header index; the BASELINE
+configs[2] and configs[3] newline indexes ride along as the ``csv`` and ``vcf`` sub-objects of the same line
+(``--legs`` picks them; a failing leg reports ``{"error": ...}`` and never drops the headline).
 
-One step = on every GPU, one dp_fasta_index over its chunk group: the chunk-table check, the single-pass
-scan kernel, the split-header resolve kernel and the read-back of pair count / per-chunk state (the index
-stays in HBM; the H2D/D2H-inclusive end-to-end rate is in DESIGN.md §6).  Steps alternate between two
-scan contexts (streams) and step k + 1 is enqueued before step k's result is collected, so the host round
-trip hides behind the next scan.  The library runs one scan grid at a time per GPU (a scan launch waits on
-the device for the device's previous scan), while step k's resolve kernel and read-back overlap scan k + 1,
-as consecutive objects do in production: ``value`` is this pipelined rate, provided its ``ms_per_step`` is
-at least the scan kernel's own average duration (checked in the run; otherwise ``value`` falls back to the
-``serialized`` rate, where each step also waits on the device for the previous step's tail, which is always
-reported as a secondary field).
+Workloads (synthetic bytes of the named shapes, resident in HBM before any timed region):
+  * FASTA (configs[1]): every GPU indexes its own 4 GiB FASTA object with the reference's chunk plan
+    ``chunk_size = size / 4`` (uint32 index): ``value`` is the WEAK-scaling rate, N x the N = 1 workload.
+    ``strong`` (N > 1): ONE such object's plan cut over the N GPUs by the product split
+    (``scan.objects.fasta_split``: byte-balanced groups, chunks cut where a boundary falls inside one, no
+    collective; the reference runs chunks as independent map jobs, preprocess.py:39-51).
+  * CSV (configs[2]): a 32 GiB cities.csv-shaped object per GPU (weak), the newline index as co.preprocess
+    stores it (uint16 low words + 64 KiB block table, dp_delim_ranges out_mode 3).
+  * VCF (configs[3]): ONE 64 GiB VCF whose body is cut into one byte part per GPU (strong: the 1/2/4/8-GPU
+    curve of north_star), same index form.
+
+One step = on every GPU, one scan call over its bytes: FASTA = dp_fasta_index_async + dp_fasta_result (the
+chunk-table check, the two scan kernels -- map_kernel<FASTA> over 16 KiB ranges, then fasta_place_kernel --,
+the split-header resolve kernel, the read-back of count / pending / chunk ends); newline = dp_delim_ranges
+(two kernels up to 512 MiB per launch, the one-pass look-back kernel above: a 32 GiB CSV or a 64/N GiB VCF
+part is one-pass).  The index stays in HBM (the H2D/D2H-inclusive end-to-end rate is DESIGN.md §6).  Steps
+alternate between two contexts and step k + 1 is enqueued before step k's result is collected; the library
+runs one scan at a time per GPU (its scan stream), so ``value`` is this pipelined rate provided
+``ms_per_step`` >= the scan's own average span (checked; else the ``serialized`` rate, always reported).
 
 Launch modes (the same worker code in both):
-  * ``python bench.py --gpus N``: one process, one host thread per GPU (how ``co.preprocess`` runs a
-    multi-GPU object, scan/objects.py); exits non-zero if fewer than N devices are visible
-    (``--devices 0,0,0,0`` maps workers to devices explicitly, e.g. to rehearse the split on one GPU).
+  * ``python bench.py --gpus N``: one process, one host thread per GPU (``--devices 0,0`` maps workers to
+    devices explicitly, e.g. to rehearse the multi-GPU split on one GPU);
   * ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``: one rank per GPU; barriers and
-    the max/sum reductions go over a gloo CPU group, so RCCL is never initialised (nothing is exchanged).
+    the final gather go over a gloo CPU group, RCCL is never initialised (nothing is exchanged).
 
-Also measured in this run: every GPU's scan-kernel average duration from HIP events on its own stream
-(-> roofline, with a read-only stream kernel's rate on the same buffer as the measured peak), the fixed-
-total ("strong") curve point — the configs[1] 4 GiB object split over the same N GPUs — and, at N = 1, the
-reference algorithm on the host cores (cpu_baseline).
+Also in the line: per leg the scan's average span from HIP events on the device's scan stream (-> roofline:
+algorithmic bytes / span vs 8 TB/s; ``traffic`` from a committed rocprofv3 PMC summary of the same command),
+the same run's read-only calibration kernel (``measured_peak``, measured behind a barrier with no worker
+scanning; null when workers share a device), for the newline legs a same-run mixed read/write reference, every
+offset verified after the timed loops, and at N = 1 the reference algorithm on the host cores (cpu_baseline,
+pool sized from the cgroup CPU quota).
 """
 from __future__ import annotations
 
@@ -39,6 +47,7 @@ import argparse
 import json
 import math
 import os
+import resource
 import sys
 import threading
 import time
@@ -50,48 +59,75 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK = 8.0e12   # B/s, MI355X spec (MI355X_MICROARCH.md §Chip-level parameters)
 GiB = float(1 << 30)
+LEGS = ("fasta", "csv", "vcf")
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--workload", choices=["fasta", "csv", "vcf"], default="fasta",
-                   help="fasta: configs[1] (default, the headline line); csv: configs[2], a 32 GiB CSV per GPU; "
-                        "vcf: configs[3], one 64 GiB VCF whose body is cut into one part per GPU")
+    p.add_argument("--workload", choices=list(LEGS), default="fasta",
+                   help="the headline leg: fasta = configs[1] (default); csv = configs[2]; vcf = configs[3]")
+    p.add_argument("--legs", default=None,
+                   help="comma-separated legs in the line (default with --workload fasta: fasta,csv,vcf; "
+                        "otherwise the workload alone); the first non-headline legs become sub-objects")
     p.add_argument("--size", type=int, default=None,
-                   help="bytes per GPU (default 4 GiB fasta, 32 GiB csv) / object bytes (vcf, default 64 GiB)")
-    p.add_argument("--chunks", type=int, default=4, help="FASTA map chunks per GPU (chunk_size = size / (chunks*N))")
+                   help="bytes of the headline leg (per GPU: fasta 4 GiB, csv 32 GiB; vcf: the object, 64 GiB)")
+    p.add_argument("--fasta-size", type=int, default=4 << 30, help="fasta leg: bytes per GPU")
+    p.add_argument("--csv-size", type=int, default=32 << 30, help="csv leg: bytes per GPU")
+    p.add_argument("--vcf-size", type=int, default=64 << 30, help="vcf leg: object bytes (cut over the GPUs)")
+    p.add_argument("--chunks", type=int, default=4, help="FASTA map chunks per object (chunk_size = size / chunks)")
     p.add_argument("--index-dtype", choices=["u16b", "u32p", "u64"], default="u16b",
                    help="csv/vcf newline index form: u16b = uint16 low words + 64 KiB block table (what "
                         "co.preprocess stores), u32p = uint32 low words + 4 GiB page counts, u64 = plain uint64")
     p.add_argument("--devices", default=None,
                    help="comma-separated device of each worker / local rank (default 0..N-1); e.g. 0,0,0,0 "
                         "rehearses the multi-GPU split on one GPU")
-    p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) point")
+    p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) FASTA point")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--traffic-bytes", type=float, default=None,
-                   help="HBM bytes per scan launch from a rocprofv3 --pmc pass (overrides --traffic-from)")
+                   help="HBM bytes per headline scan launch from a rocprofv3 --pmc pass (overrides --traffic-from)")
     p.add_argument("--traffic-from", default=None,
-                   help="pmc_summary.json (tools/pmc_summary.py) of this same command: FETCH_SIZE x2 (gfx950) "
-                        "+ WRITE_SIZE per scan-kernel launch (default profiles/latest_pmc_summary[_<workload>].json)")
-    return p.parse_args()
+                   help="pmc_summary.json (tools/pmc_summary.py) of the headline leg: FETCH_SIZE x2 (gfx950) "
+                        "+ WRITE_SIZE per scan launch (default profiles/latest_pmc_summary[_<leg>].json)")
+    a = p.parse_args(argv)
+    legs = a.legs.split(",") if a.legs else (list(LEGS) if a.workload == "fasta" else [a.workload])
+    if a.workload not in legs:
+        legs = [a.workload] + legs
+    bad = [x for x in legs if x not in LEGS]
+    if bad:
+        p.error(f"unknown leg(s) {bad}")
+    a.legs = [a.workload] + [x for x in legs if x != a.workload]
+    return a
 
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def peak_rss_gib() -> float:
+    """Peak resident set of this process so far (ru_maxrss: KiB on Linux)."""
+    return round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / float(1 << 20), 3)
+
+
 # ------------------------------------------------------------------------------------------ team of workers
 class Team:
     """The workers of one run: host threads of this process (one per GPU), or this process as one rank of
-    a torch.distributed.run launch (gloo CPU group: barriers and the final gather only, never RCCL)."""
+    a torch.distributed.run launch (gloo CPU group: barriers and gathers only, never RCCL).  ``devices``:
+    every worker's device, all ranks (a device listed twice = workers sharing a GPU, a rehearsal)."""
 
-    def __init__(self, n_local: int, pg=None):
+    def __init__(self, n_local: int, pg=None, local_devices=()):
         self._tb = threading.Barrier(n_local)
         self.pg = pg
+        devs = list(local_devices)
+        if pg is not None:
+            out = [None] * pg.get_world_size()
+            pg.all_gather_object(out, devs)
+            devs = [d for ds in out for d in ds]
+        self.devices = devs
+        self.shared = len(set(devs)) < len(devs)
 
     def barrier(self):
         self._tb.wait()
@@ -168,6 +204,10 @@ def run_workers(fn, devs, rank0_index, team):
     return res
 
 
+# host-side verification holds one group's bytes at a time per slot: at most this many workers at once
+_VERIFY_SLOTS = threading.Semaphore(2)
+
+
 class Steps:
     """K steps of one scan workload alternating between two contexts of one GPU (see the module doc)."""
 
@@ -237,6 +277,16 @@ def stream_peak(ctx, d_ptr, nbytes, reps=5, write_per_read=0.0, d_out=0):
     return n16 * (1.0 + write_per_read) / (ms / 1e3 / max(1, n))
 
 
+def calibrate(team, fn):
+    """Run a calibration ``fn()`` with no worker scanning: behind a team barrier (every worker's timed steps
+    are over) and followed by one, so no worker starts anything else on the GPU meanwhile.  When workers
+    share a device (a rehearsal) the calibrations of one device would overlap each other: None."""
+    team.barrier()
+    v = None if team.shared else fn()
+    team.barrier()
+    return v
+
+
 # ------------------------------------------------------------------------------------------ CPU baseline
 _CPU_OBJ = b""
 
@@ -266,7 +316,39 @@ def _warm(_):
     return os.getpid()
 
 
-def host_info():
+def cgroup_cpu_quota():
+    """(CPUs the cgroup quota allows or None when unlimited/absent, the raw setting): cgroup v2 cpu.max
+    ("<quota> <period>" or "max <period>"), else cgroup v1 cpu.cfs_quota_us / cpu.cfs_period_us."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            raw = f.read().strip()
+        q, per = raw.split()[:2]
+        return (None if q == "max" else int(q) / int(per)), f"cpu.max={raw}"
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return (None if q <= 0 else q / per), f"cfs_quota_us={q} cfs_period_us={per}"
+    except (OSError, ValueError):
+        return None, "no cgroup cpu controller found"
+
+
+def pool_plan():
+    """(fork-pool size, host facts): every CPU this process may run on (affinity) capped by the cgroup CPU
+    quota; with no quota (unlimited), by OMP_NUM_THREADS -- the box's stated CPU share (16 per GPU), where
+    os.cpu_count() and the affinity report the whole machine."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota, raw = cgroup_cpu_quota()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if quota is not None:
+        n, basis = max(1, min(aff, int(math.floor(quota + 1e-9)))), "cgroup CPU quota"
+    elif omp > 0:
+        n, basis = max(1, min(aff, omp)), "OMP_NUM_THREADS (the cgroup sets no CPU quota)"
+    else:
+        n, basis = aff, "affinity (no cgroup quota, no OMP_NUM_THREADS)"
     model = None
     try:
         with open("/proc/cpuinfo") as f:
@@ -276,28 +358,20 @@ def host_info():
                     break
     except OSError:
         pass
-    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
-    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
-
-
-def pool_workers():
-    """Fork-pool size: every CPU this process may use, capped by the box's CPU share (OMP_NUM_THREADS=16
-    on the GPU box, where os.cpu_count() reports the whole machine)."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(n, cap) if cap > 0 else n)
+    return n, {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": aff,
+               "cgroup_cpu": raw, "cgroup_quota_cpus": None if quota is None else round(quota, 2),
+               "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "pool_processes": n, "pool_basis": basis}
 
 
 def _pool_scan(host: np.ndarray, worker_fn, chunks_per_worker: int = 8):
-    """Time ``worker_fn`` over the whole object cut into chunks_per_worker x workers chunks on a fork pool.
+    """Time ``worker_fn`` over the whole sample cut into chunks_per_worker x workers chunks on a fork pool.
     The pool is created and warmed (every worker started, the oracle imported) before the clock starts, and
-    the object is shared with the workers copy-on-write (no per-task copy): the timed region is the scan.
-    Returns (wall s, busiest worker's scan s, workers, chunks, one-core s over the same chunks)."""
+    the bytes are shared with the workers copy-on-write (no per-task copy): the timed region is the scan.
+    Returns (wall s, busiest worker's scan s, workers, chunks, one-core s over the same chunks, host facts)."""
     import multiprocessing as mp
     global _CPU_OBJ
     _CPU_OBJ = host
-    workers = pool_workers()
+    workers, hinfo = pool_plan()
     n = len(host)
     nch = max(1, chunks_per_worker * workers)
     cs = -(-n // nch)
@@ -315,17 +389,17 @@ def _pool_scan(host: np.ndarray, worker_fn, chunks_per_worker: int = 8):
         worker_fn(c)
     t_one = time.perf_counter() - t0
     _CPU_OBJ = b""
-    return t_pool, max(busy.values()), workers, len(plan), t_one
+    return t_pool, max(busy.values()), workers, len(plan), t_one, hinfo
 
 
 def cpu_baseline(host: np.ndarray, chunk_size: int):
     """The reference algorithm (re.finditer per chunk + split-header fix-up, fasta.py:24-63) on the host:
-    (1) a warm fork pool over every usable core scanning the WHOLE object in 8 chunks per core;
+    (1) a warm fork pool over every core the cgroup allows scanning the WHOLE object in 8 chunks per core;
     (2) one core, the same chunks; (3) the reference's default shape, parallel_config={} (sequential): the
     configs[1] chunk plan over the whole object, each chunk copied out first (the ranged GET's bytes,
     handler.py:39-42)."""
     from oracle import cpu_ref
-    t_pool, t_busy, workers, nch, t_one = _pool_scan(host, _regex_chunk)
+    t_pool, t_busy, workers, nch, t_one, hinfo = _pool_scan(host, _regex_chunk)
     seq_plan = cpu_ref.chunk_plan(len(host), chunk_size)
     t0 = time.perf_counter()
     for c0, c1 in seq_plan:
@@ -347,29 +421,30 @@ def cpu_baseline(host: np.ndarray, chunk_size: int):
                                    "sample": f"the whole {n / GiB:g} GiB object, {len(seq_plan)} chunks "
                                              f"of {chunk_size} B in order (parallel_config={{}}): chunk copy + "
                                              f"regex + uint32 packing"},
-            "host": host_info()}
+            "host": hinfo}
 
 
-def cpu_baseline_delim(host: np.ndarray):
+def cpu_baseline_delim(sample: np.ndarray):
     """The CPU newline index (numpy restatement of the '\\n' search CSVSlice.get / VCFSlice.get do per slice,
-    csv.py:60-98, vcf.py:98-140) on the host cores, bounded sample: the first 4 GiB of the scanned range."""
-    sample = host[: min(len(host), 4 << 30)]
-    t_pool, t_busy, workers, nch, t_one = _pool_scan(sample, _delim_chunk)
+    csv.py:60-98, vcf.py:98-140) on the host cores over a bounded sample of the scanned range."""
+    t_pool, t_busy, workers, nch, t_one, hinfo = _pool_scan(sample, _delim_chunk)
     n = len(sample)
     return {"value": round(n / t_pool / GiB, 3), "unit": "GiB/s", "cores": workers, "kind": "port",
             "sample": f"first {n / GiB:.2f} GiB of the scanned range, {nch} chunks ({nch // workers} per core), "
                       f"numpy flatnonzero(== '\\n') per chunk on a warm {workers}-process fork pool",
             "value_1core": round(n / t_one / GiB, 3), "speedup_vs_1core": round(t_one / t_pool, 2),
-            "busiest_worker_s": round(t_busy, 4), "wall_s": round(t_pool, 4), "host": host_info()}
+            "busiest_worker_s": round(t_busy, 4), "wall_s": round(t_pool, 4), "host": hinfo}
 
 
-def load_traffic(args, size, kernel):
-    """(HBM bytes per scan launch, source) from --traffic-bytes or a committed rocprofv3 PMC summary of the
-    same workload and per-GPU size (tools/pmc_summary.py), else (None, None)."""
-    if args.traffic_bytes:
+def load_traffic(args, leg, size, kernel, index_dtype=None):
+    """(HBM bytes per scan launch, source) from --traffic-bytes (headline leg only) or the committed rocprofv3
+    PMC summary of the same leg and per-GPU size (profiles/latest_pmc_summary[_<leg>].json, written by
+    tools/pmc_summary.py), else (None, None)."""
+    if leg == args.workload and args.traffic_bytes:
         return args.traffic_bytes, "--traffic-bytes"
-    suffix = "" if args.workload == "fasta" else "_" + args.workload
-    path = args.traffic_from or os.path.join(REPO, "profiles", f"latest_pmc_summary{suffix}.json")
+    suffix = "" if leg == "fasta" else "_" + leg
+    path = (args.traffic_from if leg == args.workload else None) or \
+        os.path.join(REPO, "profiles", f"latest_pmc_summary{suffix}.json")
     if not os.path.exists(path):
         return None, None
     with open(path) as f:
@@ -377,9 +452,10 @@ def load_traffic(args, size, kernel):
     if pmc.get("object_bytes", size) != size or "hbm_traffic_bytes" not in pmc \
             or not pmc.get("kernel", kernel).startswith(kernel):
         return None, None
-    if args.workload != "fasta" and pmc.get("index_dtype", "u64") != args.index_dtype:
+    if leg != "fasta" and pmc.get("index_dtype", "u64") != index_dtype:
         return None, None                              # a profile of the other index form
-    return pmc["hbm_traffic_bytes"], os.path.relpath(os.path.realpath(path), REPO)
+    src = pmc.get("source") or os.path.relpath(os.path.realpath(path), REPO)
+    return pmc["hbm_traffic_bytes"], src
 
 
 # ------------------------------------------------------------------------------------------ FASTA
@@ -410,7 +486,7 @@ class FastaSpec:
         self.u64 = size > (1 << 32)
 
 
-def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, dev: int, keep_host: bool):
+def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, dev: int):
     from dataplug_amd.scan import ScanContext
     out = {"worker": k, "device": dev}
     ctxs = (ScanContext(dev), ScanContext(dev))
@@ -422,6 +498,8 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
         host = sp.obj.bytes_range(g.lo, g.buf_hi)
         d_in = ctxs[0].workspace(f"in_{tag}", len(host) + 64)
         ctxs[0].h2d(d_in.ptr, host)
+        n_buf = len(host)
+        del host                        # the host copy is not kept: verify() regenerates the bytes it checks
         chunks = np.ascontiguousarray(np.asarray(g.chunks(sp.scan_plan), np.uint64).reshape(-1))
         nch = len(chunks) // 2
         cap = (g.hi - g.lo) // 256 + 1024
@@ -429,14 +507,13 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
         d_outs = (ctxs[0].workspace(f"out_{tag}", osz), ctxs[1].workspace(f"out_{tag}", osz))
 
         def launch(i):
-            ctxs[i % 2].fasta_index_async(d_in.ptr, len(host), g.lo, sp.size, chunks, d_outs[i % 2].ptr,
-                                           sp.u64, cap)
+            ctxs[i % 2].fasta_index_async(d_in.ptr, n_buf, g.lo, sp.size, chunks, d_outs[i % 2].ptr, sp.u64, cap)
 
         def collect(i):
             return ctxs[i % 2].fasta_result(nch)
 
         scanned = sum(p.b - p.a for p in sp.pieces[g.i0:g.i1])         # the plan's bytes (not the overlap byte)
-        return {"g": g, "host": host, "d_in": d_in, "d_outs": d_outs, "steps": Steps(team, ctxs, launch, collect),
+        return {"g": g, "d_in": d_in, "d_outs": d_outs, "steps": Steps(team, ctxs, launch, collect),
                 "scanned": scanned, "chunks": chunks}
 
     def verify(sp: FastaSpec, st, res, i_last):
@@ -446,9 +523,10 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
         from oracle import dpref          # the checker (test infrastructure), outside every timed region
         g = st["g"]
         rel = [(c0 - g.lo, c1 - g.lo) for c0, c1 in g.chunks(sp.scan_plan)]
-        exp = dpref.fasta_pairs(st["host"], rel)
         got = np.empty((n_pairs, 2), np.uint64 if sp.u64 else np.uint32)
         ctxs[0].d2h(got, st["d_outs"][i_last % 2].ptr)
+        with _VERIFY_SLOTS:
+            exp = dpref.fasta_pairs(sp.obj.bytes_range(g.lo, g.buf_hi), rel)
         return bool((pending == -1).all() and np.array_equal(got.astype(np.uint64) - np.uint64(g.lo), exp))
 
     t0 = time.perf_counter()
@@ -458,16 +536,16 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
     team.barrier()                    # every worker's uploads are done before any scan (shared-GPU rehearsals)
     S = st["steps"]
     S.warm(args.warmup)
-    # (1) HIP events on each context's own stream around every scan launch: the kernel's own duration
+    # (1) HIP events on the device's scan stream around every scan launch: the kernels' own span
     dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
     # (2) the K steps with each scan also waiting for the previous step's tail (the secondary `serialized`)
     dt, _, _ = S.timed(args.steps)
     # (3) the K timed steps of `value`: pipelined (no events); its last result is the one verified
     dt_ov, _, res = S.timed(args.steps, serialize=False)
+    nbytes = st["g"].hi - st["g"].lo
     out.update(dt=dt, dt_overlap=dt_ov, kern_s=kms / 1e3 / max(1, kn), scanned=st["scanned"], pairs=res[0],
                alg_bytes=st["scanned"] + (16 if spec.u64 else 8) * res[0],
-               stream_peak=stream_peak(ctxs[0], st["d_in"].ptr, st["g"].hi - st["g"].lo))
-    out["verified"] = verify(spec, st, res, args.steps - 1)
+               stream_peak=calibrate(team, lambda: stream_peak(ctxs[0], st["d_in"].ptr, nbytes)))
     if ss is not None:
         ss["steps"].warm(args.warmup)
         dts, (sms, sn), sres = ss["steps"].timed(args.steps, timing=True)
@@ -476,30 +554,29 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
     elif strong is not None:
         team.barrier()                 # no group for this worker in the strong split: keep the barriers paired
         team.barrier()
-    if keep_host:
-        out["host"] = st["host"]
+    out["verified"] = verify(spec, st, res, args.steps - 1)
     for c in ctxs:
         c.close()
+    out["rss_gib"] = peak_rss_gib()
     return out
 
 
-def main_fasta(args, world, rank, devs, team):
-    per_gpu = args.size or (4 << 30)
-    size = per_gpu
+def leg_fasta(args, world, rank, devs, team):
+    """The configs[1] leg: every worker's result (rank 0: all ranks'; others: None) and the specs."""
+    per_gpu = args.size if (args.size and args.workload == "fasta") else args.fasta_size
     # weak: every GPU indexes its own configs[1] object (the reference's plan, chunk_size = size / 4, uint32
     # index) -- N x the N = 1 workload; strong: ONE such object cut over the N GPUs by the product's split
-    spec = FastaSpec(size, args.chunks, 1)
+    spec = FastaSpec(per_gpu, args.chunks, 1)
     strong = None
     if world > 1 and not args.no_strong:
         strong = FastaSpec(per_gpu, args.chunks, world)
-    log(f"{world} GPU(s): a {size / GiB:g} GiB FASTA per GPU, {len(spec.plan)} chunks of {spec.chunk_size} B, "
-        f"{'uint64' if spec.u64 else 'uint32'} index, devices {devs} (rank {rank})")
-    keep = world == 1 and not args.no_cpu_baseline
-    res = run_workers(lambda k, d: fasta_worker(args, team, spec, strong, k, d, keep), devs, rank * len(devs), team)
-    host = res[0].pop("host", None) if keep else None
-    allres = team.gather(res)
-    if allres is None:
-        return
+    log(f"fasta: {world} GPU(s), a {per_gpu / GiB:g} GiB FASTA per GPU, {len(spec.plan)} chunks of "
+        f"{spec.chunk_size} B, {'uint64' if spec.u64 else 'uint32'} index, devices {devs} (rank {rank})")
+    res = run_workers(lambda k, d: fasta_worker(args, team, spec, strong, k, d), devs, rank * len(devs), team)
+    return team.gather(res), spec, strong
+
+
+def report_fasta(args, world, team, allres, spec, strong, t_leg):
     K = args.steps
     dt_ser = max(r["dt"] for r in allres)
     dt_ov = max(r["dt_overlap"] for r in allres)
@@ -509,10 +586,15 @@ def main_fasta(args, world, rank, devs, team):
     pipelined = dt_ov / K >= kern            # one scan at a time: a step is never shorter than the scan
     dt = dt_ov if pipelined else dt_ser
     ach = min(r["alg_bytes"] / r["kern_s"] for r in allres)
-    peak_meas = min(r["stream_peak"] for r in allres)
+    peaks = [r["stream_peak"] for r in allres]
+    peak_meas = None if any(p is None for p in peaks) else min(peaks)
     verified = None if args.no_verify else all(r["verified"] for r in allres)
-    cpu = cpu_baseline(host, spec.chunk_size) if host is not None else None
-    traffic, traffic_src = load_traffic(args, per_gpu, FASTA_PMC_KERNELS) if world == 1 else (None, None)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        host = spec.obj.bytes_range(0, spec.size)        # regenerated: the worker kept no host copy
+        cpu = cpu_baseline(host, spec.chunk_size)
+        del host
+    traffic, traffic_src = load_traffic(args, "fasta", spec.size, FASTA_PMC_KERNELS) if world == 1 else (None, None)
     strong_out = None
     if strong is not None:
         sr = [r["strong"] for r in allres if "strong" in r]
@@ -541,10 +623,10 @@ def main_fasta(args, world, rank, devs, team):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic",
-        "config": {"workload": f"FASTA '>' header index of a {size / GiB:g} GiB synthetic object per GPU "
+        "config": {"workload": f"FASTA '>' header index of a {spec.size / GiB:g} GiB synthetic object per GPU "
                                f"(BASELINE configs[1]: chunk_size={spec.chunk_size} = size/{len(spec.plan)}), "
                                f"{world} object(s)",
-                   "object_bytes": size, "objects": world, "chunks": len(spec.plan), "pairs": int(pairs),
+                   "object_bytes": spec.size, "objects": world, "chunks": len(spec.plan), "pairs": int(pairs),
                    "index_dtype": "uint64" if spec.u64 else "uint32",
                    "parallelism": f"independent objects x{world}, "
                                   f"{'one rank per GPU (gloo for barriers)' if team.pg is not None else 'one host thread per GPU'}, "
@@ -562,36 +644,65 @@ def main_fasta(args, world, rank, devs, team):
                      "kernel": FASTA_KERNEL, "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(r0["alg_bytes"]),
                      "alg_bytes_def": "N + 8 * H (N chunk bytes read once, H headers x two uint32 offsets)",
-                     "measured_peak": round(peak_meas / 1e9, 1),
-                     "frac_of_measured_peak": round(ach / peak_meas, 4),
-                     "note": "per GPU (the slowest GPU's algorithmic bytes / its average scan launch); "
-                             "measured_peak = read-only stream kernel over the same buffer, same run"},
+                     "measured_peak": None if peak_meas is None else round(peak_meas / 1e9, 1),
+                     "frac_of_measured_peak": None if peak_meas is None else round(ach / peak_meas, 4),
+                     "note": "per GPU (the slowest GPU's algorithmic bytes / its average scan span); measured_peak"
+                             " = read-only stream kernel over the same buffer, same run, behind a barrier with no "
+                             "worker scanning (null when workers share a GPU)"},
         "cpu_baseline": cpu,
         "verified_bit_exact": verified,
         "gen_s": round(max(r["gen_s"] for r in allres), 2),
+        "leg_s": round(t_leg, 2),
+        "rss_gib_max_worker": max(r["rss_gib"] for r in allres),
     }
     if world > 1:
         out["per_gpu"] = [{"worker": r["worker"], "device": r["device"], "bytes": r["scanned"],
                            "ms_per_step": round((r["dt_overlap"] if pipelined else r["dt"]) / K * 1e3, 4),
                            "kernel_avg_us": round(r["kern_s"] * 1e6, 2),
                            "verified": r["verified"]} for r in allres]
-    print(json.dumps(out), flush=True)
+    return out
 
 
 # ------------------------------------------------------------------------------------------ CSV / VCF
-def delim_worker(args, team, k, world, dev, keep_host):
+def _verify_blocked(obj, begin, end, got, tab, n_out):
+    """Every offset of a uint16 + 64 KiB-block-table index against the object's analytic newline positions
+    (synth.TiledText): the low words equal the expected offsets' low 16 bits, and every table entry equals the
+    number of expected offsets below its boundary (0 for a boundary at or below ``begin``); together they pin
+    every full offset."""
+    j0 = begin >> 16
+    nb = len(tab)
+    i, nxt = 0, j0                                   # offsets checked so far; the next boundary to check
+    for piece in obj.delims_range(begin, end):
+        if len(piece) == 0:
+            continue
+        if i + len(piece) > n_out or not np.array_equal(got[i:i + len(piece)],
+                                                        (piece & np.uint64(0xFFFF)).astype(np.uint16)):
+            return False
+        hi = min(int(piece[-1]) >> 16, j0 + nb - 1)  # boundaries at or below this piece's last offset
+        if hi >= nxt:
+            bnd = np.arange(nxt, hi + 1, dtype=np.uint64) << np.uint64(16)
+            exp = np.uint64(i) + np.searchsorted(piece, bnd).astype(np.uint64)
+            if not np.array_equal(tab[nxt - j0:hi + 1 - j0], exp):
+                return False
+            nxt = hi + 1
+        i += len(piece)
+    # boundaries past the last offset: every entry before them
+    return bool(i == n_out and (tab[nxt - j0:] == np.uint64(n_out)).all())
+
+
+def delim_worker(args, team, leg, k, world, dev):
     """configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3] (vcf: ONE
     64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong scaling): the
-    newline index as co.preprocess builds it — uint32 low words with the ranges split at 4 GiB page
-    boundaries (dp_delim_ranges out_mode 2; --index-dtype u64: plain uint64) — device-resident, timed like
-    the FASTA line."""
+    newline index as co.preprocess builds it (uint16 low words + 64 KiB block table, dp_delim_ranges out_mode
+    3; --index-dtype u32p / u64: the other forms) -- device-resident, timed like the FASTA leg."""
     from dataplug_amd import synth
     from dataplug_amd.dist import rank_byte_range
     from dataplug_amd.scan import ScanContext
     from dataplug_amd.scan.objects import page_ranges
-    csv_mode = args.workload == "csv"
+    csv_mode = leg == "csv"
     fmt = args.index_dtype
-    size = args.size or ((32 << 30) if csv_mode else (64 << 30))
+    head = args.size if (args.size and args.workload == leg) else None
+    size = head or (args.csv_size if csv_mode else args.vcf_size)
     t0 = time.perf_counter()
     obj = synth.tiled_csv(size, seed=9 + k) if csv_mode else synth.tiled_vcf(size, seed=9)
     begin, end = (0, size) if csv_mode else rank_byte_range(len(obj.head), size, k, world)
@@ -600,8 +711,8 @@ def delim_worker(args, team, k, world, dev, keep_host):
     ctxs = (ScanContext(dev), ScanContext(dev))
     d_buf = ctxs[0].workspace("bench_in", nbytes + 64)
     d_ptr = d_buf.ptr + (begin & 15)                       # object offset and device address congruent mod 16
-    step = 4 << 30                                           # materialize + upload 4 GiB at a time
-    stage = np.empty(min(step, nbytes), np.uint8)
+    step = 2 << 30                                           # materialize + upload 2 GiB at a time
+    stage = np.empty(min(step, max(1, nbytes)), np.uint8)
     for p in range(begin, end, step):
         q = min(end, p + step)
         ctxs[0].h2d(d_ptr + (p - begin), obj.bytes_range(p, q, out=stage))
@@ -631,53 +742,53 @@ def delim_worker(args, team, k, world, dev, keep_host):
     dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
     dt, _, _ = S.timed(args.steps)                                         # serialized (secondary)
     dt_ov, _, (n_out, _, ends) = S.timed(args.steps, serialize=False)      # pipelined (`value`), verified
-    verified = None
+    wpr = item * n_out / max(1, nbytes)
+    d_mix = ctxs[0].workspace("bench_mix", int(wpr * nbytes) + (1 << 20))
+    peak = calibrate(team, lambda: stream_peak(ctxs[0], d_buf.ptr, nbytes))
+    mixed = calibrate(team, lambda: stream_peak(ctxs[0], d_buf.ptr, nbytes, write_per_read=wpr, d_out=d_mix.ptr))
+    verified, t_ver = None, time.perf_counter()
     if not args.no_verify:
-        # every offset, against the object's analytic newline positions (synth.TiledText)
         last = d_outs[(args.steps - 1) % 2].ptr
         got = ctxs[0].d2h(np.empty(n_out, {"u16b": np.uint16, "u32p": np.uint32, "u64": np.uint64}[fmt]), last)
-        page_first = [0] + [int(e) for e in ends[:-1]]          # entry index where each page range starts
-        page_of = [int(rg[2 * j]) >> 32 for j in range(nr)]
-        tab = ctxs[0].block_table(last, cap, rg).astype(np.int64) if fmt == "u16b" else None
-        ok, i = n_out == n_exp, 0
-        for piece in obj.delims_range(begin, end):
-            if not ok:
-                break
-            seg = got[i:i + len(piece)].astype(np.uint64)
-            idx = np.arange(i, i + len(piece))
-            if fmt == "u32p":                                    # rebuild uint64 from the page of each entry
-                j = np.searchsorted(np.asarray(page_first[1:], np.int64), idx, side="right")
-                seg |= np.asarray(page_of, np.uint64)[j] << np.uint64(32)
-            elif fmt == "u16b":                                  # ... from the 64 KiB block of each entry
-                blk = np.searchsorted(tab, idx, side="right").astype(np.uint64) - np.uint64(1)
-                seg |= (blk + np.uint64(begin >> 16)) << np.uint64(16)
-            ok = np.array_equal(seg, piece)
-            i += len(piece)
-        verified = bool(ok and i == n_out)
+        with _VERIFY_SLOTS:
+            if fmt == "u16b":
+                verified = n_out == n_exp and _verify_blocked(obj, begin, end, got, ctxs[0].block_table(last, cap, rg),
+                                                              n_out)
+            else:
+                page_first = [0] + [int(e) for e in ends[:-1]]      # entry index where each page range starts
+                page_of = [int(rg[2 * j]) >> 32 for j in range(nr)]
+                ok, i = n_out == n_exp, 0
+                for piece in obj.delims_range(begin, end):
+                    if not ok:
+                        break
+                    seg = got[i:i + len(piece)].astype(np.uint64)
+                    if fmt == "u32p":                             # rebuild uint64 from the page of each entry
+                        idx = np.arange(i, i + len(piece))
+                        j = np.searchsorted(np.asarray(page_first[1:], np.int64), idx, side="right")
+                        seg |= np.asarray(page_of, np.uint64)[j] << np.uint64(32)
+                    ok = np.array_equal(seg, piece)
+                    i += len(piece)
+                verified = bool(ok and i == n_out)
         del got
-    wpr = item * n_out / nbytes
-    d_mix = ctxs[0].workspace("bench_mix", int(wpr * nbytes) + (1 << 20))
-    out = {"dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn), "scanned": nbytes, "offsets": n_out,
-           "kernel": kernel,
+    t_ver = time.perf_counter() - t_ver
+    out = {"worker": k, "device": dev, "dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn),
+           "scanned": nbytes, "offsets": n_out, "kernel": kernel,
            "alg_bytes": nbytes + item * n_out + (8 * ScanContext.block_table_size(rg)[1] if fmt == "u16b" else 0),
-           "verified": verified, "gen_s": gen_s, "size": size,
-           "stream_peak": stream_peak(ctxs[0], d_buf.ptr, nbytes),
-           "mixed_peak": stream_peak(ctxs[0], d_buf.ptr, nbytes, write_per_read=wpr, d_out=d_mix.ptr)}
-    if keep_host:
-        out["host"] = obj.bytes_range(begin, min(end, begin + (1 << 30)))
+           "verified": verified, "verify_s": t_ver, "gen_s": gen_s, "size": size, "wpr": wpr,
+           "stream_peak": peak, "mixed_peak": mixed, "range": (begin, end)}
     for c in ctxs:
         c.close()
+    out["rss_gib"] = peak_rss_gib()
     return out
 
 
-def main_delim(args, world, rank, devs, team):
-    keep = world == 1 and not args.no_cpu_baseline
-    res = run_workers(lambda k, d: delim_worker(args, team, k, world, d, keep), devs, rank * len(devs), team)
-    host = res[0].pop("host", None) if keep else None
-    allres = team.gather(res)
-    if allres is None:
-        return
-    csv_mode = args.workload == "csv"
+def leg_delim(args, world, rank, devs, team, leg):
+    res = run_workers(lambda k, d: delim_worker(args, team, leg, k, world, d), devs, rank * len(devs), team)
+    return team.gather(res)
+
+
+def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
+    csv_mode = leg == "csv"
     K = args.steps
     size = allres[0]["size"]
     dt_ser = max(r["dt"] for r in allres)
@@ -688,10 +799,21 @@ def main_delim(args, world, rank, devs, team):
     pipelined = dt_ov / K >= kern            # one scan at a time: a step is never shorter than the scan
     dt = dt_ov if pipelined else dt_ser
     ach = min(r["alg_bytes"] / r["kern_s"] for r in allres)
-    peak_meas = min(r["stream_peak"] for r in allres)
-    mixed = min(r["mixed_peak"] for r in allres)
-    cpu = cpu_baseline_delim(host) if host is not None else None
-    traffic, traffic_src = load_traffic(args, allres[0]["scanned"], "scan_kernel<1") if world == 1 else (None, None)
+    peaks = [r["stream_peak"] for r in allres]
+    mixes = [r["mixed_peak"] for r in allres]
+    peak_meas = None if any(p is None for p in peaks) else min(peaks)
+    mixed = None if any(p is None for p in mixes) else min(mixes)
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        from dataplug_amd import synth
+        obj = synth.tiled_csv(size, seed=9) if csv_mode else synth.tiled_vcf(size, seed=9)
+        b0, b1 = allres[0]["range"]
+        sample = obj.bytes_range(b0, min(b1, b0 + (1 << 30)))     # bounded sample: the first GiB scanned
+        cpu = cpu_baseline_delim(sample)
+        del sample
+    pmc_kernel = "scan_kernel<1" if "one-pass" in allres[0]["kernel"] else "map_kernel<1>,delim_place_kernel"
+    traffic, traffic_src = (load_traffic(args, leg, allres[0]["scanned"], pmc_kernel, args.index_dtype)
+                            if world == 1 else (None, None))
     name = "CSV" if csv_mode else "VCF"
     idx = {"u16b": "uint16 low words + 64 KiB block table", "u32p": "uint32 low words + 4 GiB pages",
            "u64": "uint64"}[args.index_dtype]
@@ -699,19 +821,14 @@ def main_delim(args, world, rank, devs, team):
            if csv_mode else
            f"'\\n' index ({idx}) of one {size / GiB:g} GiB VCF body cut into {world} part(s), one per GPU "
            f"(BASELINE configs[3])")
+    verified = None if args.no_verify else all(r["verified"] for r in allres)
     out = {
         "metric": f"GiB/s scanned (device-resident) + offsets/s, {name} newline index",
         "value": round(scanned * K / dt / GiB, 3),
         "unit": "GiB/s",
         "n_gpus": world,
-        "steps": K,
-        "warmup": args.warmup,
         "ms_per_step": round(dt / K * 1e3, 4),
-        "higher_is_better": True,
         "scaling": "weak" if csv_mode else "strong",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic",
         "config": {"workload": cfg, "object_bytes": size, "scanned_bytes_per_gpu": allres[0]["scanned"],
                    "offsets_per_gpu": int(allres[0]["offsets"]),
                    "parallelism": f"independent {'objects' if csv_mode else 'body parts'} x{world}, no collective"},
@@ -727,30 +844,69 @@ def main_delim(args, world, rank, devs, team):
                      "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)%s" % (
                          {"u16b": 2, "u32p": 4, "u64": 8}[args.index_dtype],
                          " + 8 B per 64 KiB block" if args.index_dtype == "u16b" else ""),
-                     "measured_peak": round(peak_meas / 1e9, 1),
-                     "frac_of_measured_peak": round(ach / peak_meas, 4),
-                     "measured_mixed_ref": round(mixed / 1e9, 1),
-                     "frac_of_mixed_ref": round(ach / mixed, 4),
+                     "measured_peak": None if peak_meas is None else round(peak_meas / 1e9, 1),
+                     "frac_of_measured_peak": None if peak_meas is None else round(ach / peak_meas, 4),
+                     "measured_mixed_ref": None if mixed is None else round(mixed / 1e9, 1),
+                     "frac_of_mixed_ref": None if mixed is None else round(ach / mixed, 4),
                      "note": "measured_peak: read-only stream kernel (same run, same buffer); measured_mixed_ref: "
                              "the best plain streaming shape measured (stream_rw_kernel) reading the same buffer "
                              "while writing the index's bytes per input byte: a same-run reference for the "
-                             "read/write mix, not a bound (reads and writes share the HBM bus)"},
+                             "read/write mix, not a bound (reads and writes share the HBM bus); both behind a "
+                             "barrier with no worker scanning, null when workers share a GPU"},
         "cpu_baseline": cpu,
-        "verified_bit_exact": None if args.no_verify else all(r["verified"] for r in allres),
+        "verified_every_offset": verified,
         "gen_s": round(max(r["gen_s"] for r in allres), 2),
+        "verify_s": round(max(r["verify_s"] for r in allres), 2),
+        "leg_s": round(t_leg, 2),
+        "rss_gib_max_worker": max(r["rss_gib"] for r in allres),
     }
-    print(json.dumps(out), flush=True)
+    if headline:
+        out.update(steps=K, warmup=args.warmup, higher_is_better=True, vs_baseline=None, dtype="u8",
+                   data="synthetic", verified_bit_exact=verified)
+    if world > 1:
+        out["per_gpu"] = [{"worker": r["worker"], "device": r["device"], "bytes": r["scanned"],
+                           "kernel_avg_us": round(r["kern_s"] * 1e6, 2), "verified": r["verified"]} for r in allres]
+    return out
 
 
-def main():
-    args = parse()
+# ------------------------------------------------------------------------------------------ main
+def run_leg(args, world, rank, devs, team, leg, headline):
+    t0 = time.perf_counter()
+    if leg == "fasta":
+        allres, spec, strong = leg_fasta(args, world, rank, devs, team)
+        if allres is None:
+            return None
+        return report_fasta(args, world, team, allres, spec, strong, time.perf_counter() - t0)
+    allres = leg_delim(args, world, rank, devs, team, leg)
+    if allres is None:
+        return None
+    return report_delim(args, world, team, allres, leg, time.perf_counter() - t0, headline)
+
+
+def main(argv=None):
+    args = parse(argv)
     world, rank, devs, pg = launch_mode(args)
-    team = Team(len(devs), pg)
+    team = Team(len(devs), pg, devs)
+    t_all = time.perf_counter()
     try:
-        if args.workload == "fasta":
-            main_fasta(args, world, rank, devs, team)
-        else:
-            main_delim(args, world, rank, devs, team)
+        head = run_leg(args, world, rank, devs, team, args.workload, True)   # the headline: errors propagate
+        for leg in args.legs[1:]:
+            try:
+                sub = run_leg(args, world, rank, devs, team, leg, False)
+            except Exception as e:            # a failing extra leg never drops the headline line
+                log(f"leg {leg} failed: {type(e).__name__}: {e}")
+                sub = {"error": f"{type(e).__name__}: {e}"}
+                if pg is not None:            # the other ranks may wait in a barrier of the failed leg
+                    raise
+                team._tb.reset()              # a failed worker aborted the threads' barrier
+            if head is not None:
+                head[leg] = sub
+        if head is not None:
+            rss = [head.get("rss_gib_max_worker", 0.0)] + [(head.get(x) or {}).get("rss_gib_max_worker", 0.0)
+                                                           for x in args.legs[1:]]
+            head["peak_rss_gib"] = max([peak_rss_gib()] + [r or 0.0 for r in rss])
+            head["bench_wall_s"] = round(time.perf_counter() - t_all, 2)
+            print(json.dumps(head), flush=True)
     finally:
         if pg is not None:
             pg.destroy_process_group()

@@ -306,7 +306,8 @@ def test_bench_thread_mode_split_on_one_gpu(tmp_path):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "4", "--devices", "0,0,0,0",
-           "--size", str((48 << 20) + 4096), "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+           "--size", str((48 << 20) + 4096), "--csv-size", str((40 << 20) + 77), "--vcf-size", str((96 << 20) + 5),
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
@@ -316,6 +317,75 @@ def test_bench_thread_mode_split_on_one_gpu(tmp_path):
     assert line["strong"]["verified_bit_exact"] is True and line["strong"]["gpus_used"] == 4
     assert line["strong"]["chunks"] == 4 and line["strong"]["pieces"] == 4
     assert line["ms_per_step"] * 1e3 >= line["roofline"]["kernel_avg_us"]
+    # workers share the GPU: no calibration ratio is reported (it would mix the workers' kernels)
+    assert line["roofline"]["measured_peak"] is None and line["roofline"]["frac_of_measured_peak"] is None
+    for leg in ("csv", "vcf"):
+        sub = line[leg]
+        assert "error" not in sub, sub
+        assert sub["n_gpus"] == 4 and sub["verified_every_offset"] is True and len(sub["per_gpu"]) == 4
+        assert sub["roofline"]["frac"] > 0 and sub["roofline"]["measured_mixed_ref"] is None
+    assert line["vcf"]["scaling"] == "strong" and line["csv"]["scaling"] == "weak"
+    assert line["peak_rss_gib"] > 0
+
+
+def test_bench_default_line_carries_the_newline_legs():
+    """The driver's command (bench.py, N = 1) at small sizes: ONE line whose headline is the FASTA leg and whose
+    csv / vcf sub-objects (BASELINE configs[2] / [3]) carry value, roofline (measured read ceiling and mixed
+    reference, behind a barrier), cpu_baseline with the cgroup-derived pool, and every offset verified."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--size", str((64 << 20) + 12), "--csv-size",
+           str((72 << 20) + 3), "--vcf-size", str((80 << 20) + 9), "--steps", "3", "--warmup", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    assert line["verified_bit_exact"] is True and line["roofline"]["measured_peak"] > 0
+    assert line["cpu_baseline"]["host"]["pool_processes"] == line["cpu_baseline"]["cores"]
+    for leg in ("csv", "vcf"):
+        sub = line[leg]
+        assert "error" not in sub, sub
+        assert sub["verified_every_offset"] is True and sub["value"] > 0 and sub["ms_per_step"] > 0
+        rf = sub["roofline"]
+        assert rf["frac"] > 0 and rf["measured_peak"] > 0 and rf["measured_mixed_ref"] > 0
+        assert sub["cpu_baseline"]["value"] > 0 and sub["cpu_baseline"]["cores"] >= 1
+        assert rf["kernel"].startswith("map_kernel<DELIM>")          # <= 512 MiB: the two-kernel form
+    assert line["bench_wall_s"] > 0
+
+
+@pytest.mark.parametrize("workload", ["fasta", "vcf"])
+def test_bench_under_torch_distributed_run(workload):
+    """The driver's N > 1 launch (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N),
+    rehearsed with two ranks on one GPU (--devices 0,0), started as a fresh child before any GPU call in it:
+    ONE JSON line from rank 0 with both ranks' results, every launch exact, and no calibration ratio (the
+    ranks share the GPU)."""
+    import socket
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(repo, "bench.py"), "--gpus", "2", "--devices", "0,0",
+           "--workload", workload, "--fasta-size", str(256 << 20), "--legs", "fasta,vcf",
+           "--vcf-size", str((200 << 20) + 1),
+           "--steps", "3", "--warmup", "1", "--no-cpu-baseline"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    fasta = line if workload == "fasta" else line["fasta"]
+    vcf = line if workload == "vcf" else line["vcf"]
+    assert "error" not in fasta and "error" not in vcf
+    assert fasta["n_gpus"] == 2 and len(fasta["per_gpu"]) == 2 and fasta["verified_bit_exact"] is True
+    assert fasta["strong"]["verified_bit_exact"] is True and fasta["strong"]["gpus_used"] == 2
+    assert vcf["n_gpus"] == 2 and len(vcf["per_gpu"]) == 2 and vcf["verified_every_offset"] is True
+    assert fasta["roofline"]["frac_of_measured_peak"] is None and vcf["roofline"]["frac_of_measured_peak"] is None
 
 
 def test_bench_refuses_more_gpus_than_visible():

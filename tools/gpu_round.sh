@@ -1,19 +1,21 @@
 #!/bin/bash
-# One GPU verification pass: the GPU tests, the default bench, CSV/VCF bench lines, the multi-worker
-# rehearsals on one GPU (threads, then two torchrun ranks sharing the device).
+# One GPU verification pass (on the GPU box):  bash tools/gpu_round.sh <tag> [quick]
+# the GPU tests, smoke, the driver's bench command (FASTA headline + CSV / VCF legs in one line), and the
+# multi-worker rehearsal on one GPU (threads).  Every step under its own time limit; the first failure ends it.
 set -o pipefail
-O=gpurun_out/${1:-run}
-mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 &&
-tail -3 $O/gpu_tests.log &&
-timeout -k 10 240 python -u bench.py > $O/bench_fasta.json 2> $O/bench_fasta.err &&
-cat $O/bench_fasta.json &&
-timeout -k 10 240 python -u bench.py --workload csv --no-cpu-baseline > $O/bench_csv.json 2> $O/bench_csv.err &&
-cat $O/bench_csv.json &&
-timeout -k 10 300 python -u bench.py --workload vcf --no-cpu-baseline > $O/bench_vcf.json 2> $O/bench_vcf.err &&
-cat $O/bench_vcf.json &&
-timeout -k 10 240 python -u bench.py --gpus 4 --devices 0,0,0,0 --no-cpu-baseline --no-strong > $O/bench_t4.json 2> $O/bench_t4.err &&
-cat $O/bench_t4.json &&
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --devices 0,0 --no-cpu-baseline --no-strong > $O/bench_tr2.json 2> $O/bench_tr2.err &&
-cat $O/bench_tr2.json
+O=gpurun_out/${1:-run}; mkdir -p $O
+step() { echo "== $1 $(date +%T)"; }
+if [ "${2:-}" != quick ]; then
+  step tests
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
+  tail -2 $O/gpu_tests.log
+  step smoke
+  timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+  tail -1 $O/smoke.log
+fi
+step bench
+/usr/bin/time -v timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+grep -E "Elapsed|Maximum resident" $O/bench.err
+python3 tools/bench_summary.py $O/bench.json
+step done
