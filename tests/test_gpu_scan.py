@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from dataplug_amd import synth
+from dataplug_amd.scan._lib import DPScanError
 from oracle import cpu_ref, dpref
 
 pytestmark = pytest.mark.gpu
@@ -523,6 +524,12 @@ def test_newline_forms_equal(size):
             for mode in (1, 0, 3):
                 outs = []
                 for c, dp in ((two, d.ptr + 3), (one, d1.ptr + 3)):
+                    if mode == 3 and (k != 1 or add != 0):
+                        # the block table counts delimiters: an entry index only when every delimiter is one
+                        with pytest.raises(DPScanError, match="out_mode 3 needs every_k == 1"):
+                            c.delim_ranges(dp, n, base, [(base, base + n)], every_k=k, emit_add=add, carry=carry,
+                                           out_mode=mode)
+                        continue
                     r = c.delim_ranges(dp, n, base, [(base, base + n)], every_k=k, emit_add=add, carry=carry,
                                        out_mode=mode)
                     outs.append(r)
@@ -531,12 +538,51 @@ def test_newline_forms_equal(size):
                         j0 = base >> 16
                         blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right")
                         got = ((blk.astype(np.uint64) - np.uint64(1) + np.uint64(j0)) << np.uint64(16)) | low.astype(np.uint64)
-                        if k == 1 and add == 0:
-                            assert np.array_equal(got, exp)
+                        assert np.array_equal(got, exp)
                     else:
                         assert np.array_equal(r[0].astype(np.uint64), exp), (k, add, carry, mode)
+                if not outs:
+                    continue
                 assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
                 assert np.array_equal(np.asarray(outs[0][2]), np.asarray(outs[1][2]))
+                if mode == 3:                                     # the two forms' block tables too
+                    assert np.array_equal(outs[0][3], outs[1][3])
     finally:
         two.close()
         one.close()
+
+
+def test_forms_alternate_on_one_context():
+    """One context switching between the two-kernel and the one-pass newline forms (and the two-kernel FASTA
+    index) launch after launch: the one-pass kernel's unit ticket shares a control word with the placement
+    kernels' block ticket, which a two-kernel launch leaves non-zero; every result stays exact."""
+    c = _delim_ctx(1 << 20)                               # up to 1 MiB per launch: two kernels
+    try:
+        a = synth.csv((3 << 20) + 333, seed=4)
+        n = len(a)
+        d = c.workspace("t_in", n + 64)
+        c.h2d(d.ptr, a)
+        full = dpref.delim(a, 0, n)[0]
+        f = synth.fasta((2 << 20) + 5, seed=6)
+        df = c.workspace("t_fa", len(f) + 64)
+        c.h2d(df.ptr, f)
+        plan = cpu_ref.chunk_plan(len(f), -(-len(f) // 3))
+        fexp = dpref.fasta_pairs(f, plan)
+        for it in range(6):
+            for lo, hi in ((0, 700_000), (0, n), (1000, 900_000), (5, n - 7)):   # two-kernel, one-pass, ...
+                for mode in (1, 3):
+                    r = c.delim_ranges(d.ptr, n, 0, [(lo, hi)], out_mode=mode)
+                    exp = full[(full >= lo) & (full < hi)]
+                    if mode == 3:
+                        low, _, _, tab = r
+                        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right")
+                        got = ((blk.astype(np.uint64) - np.uint64(1) + np.uint64(lo >> 16)) << np.uint64(16)) | \
+                            low.astype(np.uint64)
+                    else:
+                        got = r[0]
+                    assert np.array_equal(got, exp), (it, lo, hi, mode)
+            if it % 2:
+                pairs, pending, _ = c.fasta_index(df.ptr, len(f), 0, len(f), plan)
+                assert (pending == -1).all() and np.array_equal(pairs.astype(np.uint64), fexp)
+    finally:
+        c.close()
