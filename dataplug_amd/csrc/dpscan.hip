@@ -976,6 +976,95 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
 
+// The stores of one range's delimiter list (a data wave's phase B, or the lockstep kernel's placement): list
+// entry i is ev(i), a position relative to the range's first byte (object offset obj_off); the range's first
+// delimiter has launch ordinal P.  every_k / emit_add / carry select and shift the entries (FASTQ read ends);
+// stores go to min(q, cap - 1) (an overflowing launch reports DP_ERR_CAPACITY and is discarded).  Returns
+// whether a uint32 value overflowed.
+template <int OUT64, bool PAIR = true, class Ev>
+__device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_t nev, uint64_t P, uint64_t obj_off,
+                                             int lane) {
+  typedef typename std::conditional<OUT64 == 1, uint64_t,
+                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
+  const bool near4g = OUT64 == 0 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
+  bool ovf = false;
+  const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
+  const uint32_t k = A.every_k;
+  // every k-th delimiter overall (FASTQ read ends), counting from the carried ordinal: list entries
+  // r0, r0 + k, ... go to q0, q0 + 1, ...
+  const uint64_t Pc = P + A.carry;
+  const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - Pc % k);
+  const uint64_t q0 = (Pc + r0) / k - A.carry / k;
+  const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
+#if DP_PAIRSTORE
+  if constexpr (OUT64 == 1 && PAIR) {
+    // Every delimiter, uint64 output, the whole list in bounds (wave-uniform): two offsets per lane and
+    // one 16-byte store, which halves the store instructions that queue behind the input loads.  An odd
+    // q0 puts its first entry in a single store so that the pairs are 16-byte aligned.
+    if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
+      uint64_t* o = reinterpret_cast<uint64_t*>(A.out) + q0;
+      const uint32_t h = nq ? (uint32_t)(q0 & 1u) : 0u;
+      if (h && lane == 0) o[0] = add + ev(0u);
+      const uint32_t m = nq - h;
+      for (uint32_t t = 2u * (uint32_t)lane; t < m; t += 2u * kWave) {
+        const uint32_t i = h + t;
+        const uint64_t v0 = add + ev(i);
+        if (t + 1u < m) {
+          const uint64_t v1 = add + ev(i + 1u);
+#if DP_NTSTORE
+          __builtin_nontemporal_store(v2u64{v0, v1}, reinterpret_cast<v2u64*>(o + i));
+        } else {
+          __builtin_nontemporal_store((uint64_t)v0, o + i);
+        }
+#else
+          *reinterpret_cast<v2u64*>(o + i) = v2u64{v0, v1};
+        } else {
+          o[i] = v0;
+        }
+#endif
+      }
+      return false;
+    }
+  }
+#endif
+  if constexpr (OUT64 == 2) {
+    // uint16 low words, every delimiter, whole list in bounds: eight entries per lane, one 16-byte store;
+    // the first (8 - q0 % 8) % 8 entries go alone so that the groups are 16-byte aligned
+    if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
+      uint16_t* o = reinterpret_cast<uint16_t*>(A.out) + q0;
+      const uint32_t hh = (uint32_t)((8u - (uint32_t)(q0 & 7u)) & 7u);
+      const uint32_t h = hh < nq ? hh : nq;
+      if ((uint32_t)lane < h) o[lane] = (uint16_t)(add + ev((uint32_t)lane));
+      const uint32_t m = nq - h, g = m >> 3;
+      for (uint32_t t = (uint32_t)lane; t < g; t += kWave) {
+        const uint32_t i = h + 8u * t;
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t a = (uint32_t)(uint16_t)(add + ev(i + 2u * e));
+          const uint32_t b = (uint32_t)(uint16_t)(add + ev(i + 2u * e + 1u));
+          w[e] = a | (b << 16);
+        }
+        const v4u pk = {w[0], w[1], w[2], w[3]};
+#if DP_NTSTORE
+        __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + i));
+#else
+        *reinterpret_cast<v4u*>(o + i) = pk;
+#endif
+      }
+      for (uint32_t t = h + 8u * g + (uint32_t)lane; t < nq; t += kWave) o[t] = (uint16_t)(add + ev(t));
+      return false;
+    }
+  }
+  for (uint32_t t = (uint32_t)lane; t < nq; t += kWave) {
+    const uint64_t q = q0 + t;
+    const uint64_t val = add + ev(r0 + t * k);
+    if (near4g) ovf |= val > 0xFFFFFFFFull;
+    put<OutT, DP_NTSTORE != 0>(A.out, q < last ? q : last, val);
+  }
+  return ovf;
+}
+
 // Phase B of one unit on one data wave, once its prefix is set: the event list copied to the output at
 // its final index.  FASTA: the list was built under "no header pending at the range start"; if the true
 // state S says one is pending, the range's first segment emits nothing (drop its start, fV) and its first
@@ -1027,80 +1116,8 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
       put<OutT>(A.out, slot < last ? slot : last, val);
     }
   } else {
-    const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
-    const uint32_t k = A.every_k;
-    // every k-th delimiter overall (FASTQ read ends), counting from the carried ordinal: list entries
-    // r0, r0 + k, ... go to q0, q0 + 1, ...
-    const uint64_t Pc = P + A.carry;
-    const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - Pc % k);
-    const uint64_t q0 = (Pc + r0) / k - A.carry / k;
-    const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
-#if DP_PAIRSTORE
-    if constexpr (OUT64 == 1) {
-      // Every delimiter, uint64 output, the whole list in bounds (wave-uniform): two offsets per lane and
-      // one 16-byte store, which halves the store instructions that queue behind the input loads.  An odd
-      // q0 puts its first entry in a single store so that the pairs are 16-byte aligned.
-      if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
-        uint64_t* o = reinterpret_cast<uint64_t*>(A.out) + q0;
-        const uint32_t h = nq ? (uint32_t)(q0 & 1u) : 0u;
-        if (h && lane == 0) o[0] = add + evw[ev0 & kEvMask];
-        const uint32_t m = nq - h;
-        for (uint32_t t = 2u * (uint32_t)lane; t < m; t += 2u * kWave) {
-          const uint32_t i = h + t;
-          const uint64_t v0 = add + evw[(ev0 + i) & kEvMask];
-          if (t + 1u < m) {
-            const uint64_t v1 = add + evw[(ev0 + i + 1u) & kEvMask];
-#if DP_NTSTORE
-            __builtin_nontemporal_store(v2u64{v0, v1}, reinterpret_cast<v2u64*>(o + i));
-          } else {
-            __builtin_nontemporal_store((uint64_t)v0, o + i);
-          }
-#else
-            *reinterpret_cast<v2u64*>(o + i) = v2u64{v0, v1};
-          } else {
-            o[i] = v0;
-          }
-#endif
-        }
-        return;
-      }
-    }
-#endif
-    if constexpr (OUT64 == 2) {
-      // uint16 low words, every delimiter, whole list in bounds: eight entries per lane, one 16-byte store;
-      // the first (8 - q0 % 8) % 8 entries go alone so that the groups are 16-byte aligned
-      if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
-        uint16_t* o = reinterpret_cast<uint16_t*>(A.out) + q0;
-        const uint32_t hh = (uint32_t)((8u - (uint32_t)(q0 & 7u)) & 7u);
-        const uint32_t h = hh < nq ? hh : nq;
-        if ((uint32_t)lane < h) o[lane] = (uint16_t)(add + evw[(ev0 + (uint32_t)lane) & kEvMask]);
-        const uint32_t m = nq - h, g = m >> 3;
-        for (uint32_t t = (uint32_t)lane; t < g; t += kWave) {
-          const uint32_t i = h + 8u * t;
-          uint32_t w[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const uint32_t a = (uint32_t)(uint16_t)(add + evw[(ev0 + i + 2u * e) & kEvMask]);
-            const uint32_t b = (uint32_t)(uint16_t)(add + evw[(ev0 + i + 2u * e + 1u) & kEvMask]);
-            w[e] = a | (b << 16);
-          }
-          const v4u pk = {w[0], w[1], w[2], w[3]};
-#if DP_NTSTORE
-          __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + i));
-#else
-          *reinterpret_cast<v4u*>(o + i) = pk;
-#endif
-        }
-        for (uint32_t t = h + 8u * g + (uint32_t)lane; t < nq; t += kWave) o[t] = (uint16_t)(add + evw[(ev0 + t) & kEvMask]);
-        return;
-      }
-    }
-    for (uint32_t t = (uint32_t)lane; t < nq; t += kWave) {
-      const uint64_t q = q0 + t;
-      const uint64_t val = add + evw[(ev0 + r0 + t * k) & kEvMask];
-      if (near4g) ovf |= val > 0xFFFFFFFFull;
-      put<OutT, DP_NTSTORE != 0>(A.out, q < last ? q : last, val);
-    }
+    ovf = place_delims<OUT64>(A, [&](uint32_t i) { return (uint32_t)evw[(ev0 + i) & kEvMask]; }, nev, P, obj_off,
+                              lane);
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
@@ -2369,6 +2386,313 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
   }
 }
 
+// ------------------------------------------------------------------------------------------ DELIM, lockstep one pass
+// line_kernel<OUT64>: the newline index in ONE kernel with the map kernel's geometry (round 4).  A workgroup of
+// 16 waves scans a group of 16 consecutive 16 KiB ranges per step (claimed from a ticket, a barrier per step,
+// exactly map_kernel<kDelim>'s streaming loop), but keeps each range's delimiter positions in LDS instead of
+// spilling them to HBM, and places them itself once the group's prefix is known:
+//   * step k: phase A of group g_k -> LDS slot k % kLineSlots (positions, count, geometry per wave);
+//   * step k + 1: wave 0 publishes g_k's delimiter count as an AGG descriptor right after the barrier (every
+//     wave wrote its count before it), then resolves g_k's prefix by a decoupled look-back over the group
+//     descriptors with hand-waited loads: issued after one buffer wait, reduced after the next (no stall);
+//     a resolved group gets its PREFIX descriptor and its LDS slot's `res` tag;
+//   * the step after: every wave copies its range's positions to their final index (place_delims).
+// A wave only blocks when the slot it is about to overwrite is still unplaced (its group's predecessors
+// are late); wave 0 then resolves in the foreground.  No spill round trip (the two-kernel form moves every
+// delimiter through HBM twice more), no coordinator wave and no placement launch (the one-pass look-back
+// kernel's start and tail).  Deadlock-free: a workgroup publishes the AGG of every group it has scanned before
+// it blocks, groups are claimed in increasing order by running workgroups, and a group's prefix depends only
+// on lower groups, so the lowest unresolved group can always resolve.
+#ifndef DP_LINE_SLOTS
+#define DP_LINE_SLOTS 4
+#endif
+#ifndef DP_LINE_CAP
+#define DP_LINE_CAP 640
+#endif
+constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
+constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
+static_assert(kLineSlots >= 3 && kLineSlots <= 6, "line slots: phase A, resolution, placement + slack");
+static_assert(kLineCap % 8 == 0 && kLineCap <= 1024, "line cap");
+constexpr uint32_t kLineGrpQ = 8;                  // claimed groups by step (>= slots + claim-ahead + 1)
+static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + 1, "group queue spans the pending and claimed steps");
+constexpr uint32_t kLineDense = 0x80000000u;
+constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
+
+struct LineShared {
+  uint16_t ev[kLineSlots][kMapWaves][kLineCap];    // per slot and wave: the range's positions
+  uint4 geo[kLineSlots][kMapWaves];                // {wbase lo, wbase hi, lo_w | flags | hi_w << 16, chunk}
+  uint32_t cnt[kLineSlots][kMapWaves];             // the range's delimiters (| kLineDense)
+  uint32_t ex[kLineSlots][kMapWaves];              // delimiters of the group before the range (wave 0)
+  unsigned long long P[kLineSlots];                // the group's launch prefix, valid once res == group + 1
+  unsigned long long tot[kLineSlots];              // the group's delimiters
+  uint32_t res[kLineSlots];
+  uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
+};
+
+struct LineArgs {
+  const uint8_t* base;          // = ScanArgs::base
+  uint64_t nchunks, nranges;
+  unsigned int* ticket;         // [2] group tickets: this launch claims from ticket[parity] and zeroes the other
+  uint32_t parity;
+};
+
+// Look-back loads of group u's window, hand-waited (inline asm: the compiler adds no wait; the caller reads
+// them after a buffer wait that covers them).  Relaxed agent-scope loads (sc1), as ld_desc.
+__device__ __forceinline__ void lb_issue_nowait(const ScanArgs& A, uint32_t u, uint32_t W, int lane, uint64_t (&d)[kLbPer]) {
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) {
+    const uint32_t k = kLbPer * rl + j;
+    const unsigned long long* p = A.desc + (k < W ? u - 1 - k : 0u);
+    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(d[j]) : "v"(p) : "memory");
+  }
+}
+__device__ __forceinline__ void lb_touch(uint64_t (&d)[kLbPer]) {
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) asm volatile("" : "+v"(d[j]) :: "memory");
+}
+// Reduce a loaded window of group u: true with the group's launch prefix P once resolvable.
+__device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P) {
+  const uint32_t W = u < kLbSlots ? u : kLbSlots;
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) {
+    const uint32_t k = kLbPer * rl + j;
+    d[j] = k < W ? ((d[j] & kEpochMask) == A.epoch ? d[j] : 0ull) : kIdentDesc;
+  }
+  return lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P);
+}
+
+template <int OUT64>
+__global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, ScanArgs A,
+                                                                 const uint64_t* __restrict__ tab_lo,
+                                                                 const uint64_t* __restrict__ tab_hi,
+                                                                 const uint64_t* __restrict__ tab_r0) {
+  static_assert(kMapWaves == 16, "line_kernel: one workgroup of 16 waves per CU");
+  __shared__ __attribute__((aligned(16))) LineShared sh;
+  const int lane = __lane_id();
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
+  const uint32_t nranges = (uint32_t)L.nranges, nchunks = (uint32_t)L.nchunks;
+  const uint32_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
+  const uint32_t G = gridDim.x;
+  unsigned int* ticket = L.ticket + L.parity;
+  if (blockIdx.x == 0 && threadIdx.x == 0) L.ticket[L.parity ^ 1u] = 0u;   // the next launch's ticket
+  uint32_t claimed = 2, run = 0, pend = 0, claim_res = 0;
+  if (threadIdx.x == 0) {
+    sh.grp[0] = blockIdx.x;                          // (the host launches at most one workgroup per group)
+    sh.grp[1] = G + blockIdx.x;
+  }
+  if (threadIdx.x < kLineSlots) sh.res[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint32_t key = A.delim ^ kSel12;
+  uint32_t r = sh.grp[0] * kMapWaves + (uint32_t)wave;
+  Cursor cur{0, 0, 0, 0, 0, 0};
+  Geo g = range_geo(T, nchunks, nranges, r, cur);
+  Buf b[kBufs];
+#pragma unroll
+  for (int h = 0; h < kBufs; ++h) load_buf(b[h], A, g, 0, lane, h);
+  bool ovf = false;
+  uint32_t nb = 0;                                   // (every wave) the next step to place
+  // (wave 0) steps with a published AGG / a resolved prefix; the step of the look-back in flight
+  uint32_t agg_next = 0, res_next = 0, lb_step = 0xFFFFFFFFu;
+  uint64_t lbd[kLbPer] = {0, 0, 0, 0};
+
+  // phase B of step q for this wave's range
+  auto place = [&](uint32_t q) {
+    const uint32_t s = q % kLineSlots;
+    const uint4 gq = sh.geo[s][wave];
+    if (!(gq.z & kLineValid)) return;
+    const uint32_t cw = sh.cnt[s][wave];
+    const uint32_t n = cw & ~kLineDense;
+    const uint64_t Pw = sh.P[s] + sh.ex[s][wave];
+    const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
+    const uint32_t lo_w = gq.z & 15u, hi_w = gq.z >> 16;
+    const uint64_t off0 = A.obj_base - A.shift + wbase;
+    if (lane == 0) {
+      if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
+      if (sh.grp[q % kLineGrpQ] * kMapWaves + (uint32_t)wave + 1u == nranges) A.total[0] = Pw + n;
+      if constexpr (OUT64 == 2) {
+        // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
+        const uint64_t j = (off0 >> 16) - A.tab_j0;
+        if ((off0 & 0xFFFFull) == 0 && lo_w == 0 && hi_w != 0 && off0 >= (A.tab_j0 << 16) && j < A.tab_n)
+          A.blocktab[j] = Pw;
+      }
+    }
+    if (cw & kLineDense) {
+      dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
+      return;
+    }
+    const uint16_t* evw = sh.ev[s][wave];
+    // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
+    ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
+  };
+  // (wave 0) step q's AGG: the group's count from the 16 ranges (lanes 0..15), their exclusive prefixes
+  auto publish_agg = [&](uint32_t q) {
+    const uint32_t s = q % kLineSlots;
+    const uint32_t c = lane < (int)kMapWaves ? (sh.cnt[s][lane] & ~kLineDense) : 0u;
+    uint32_t inc = c;
+    inc += dpp32<kRowShr1, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr2, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr4, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr8, 0xF>(inc, 0u);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kMapWaves - 1);
+    if (lane < (int)kMapWaves) sh.ex[s][lane] = inc - c;
+    if (lane == 0) {
+      sh.tot[s] = total;
+      st_desc(&A.desc[sh.grp[q % kLineGrpQ]], pack_count(kStatAgg, total) | A.epoch);
+    }
+    agg_next = q + 1;
+  };
+  // (wave 0) a resolved prefix: LDS tag for the other waves, PREFIX descriptor for the other workgroups
+  auto resolved = [&](uint32_t q, uint64_t P) {
+    const uint32_t s = q % kLineSlots;
+    const uint32_t u = sh.grp[q % kLineGrpQ];
+    if (lane == 0) {
+      sh.P[s] = P;
+      cbar();
+      lds_st(&sh.res[s], u + 1u);
+      st_desc(&A.desc[u], pack_count(kStatPrefix, P + sh.tot[s]) | A.epoch);
+    }
+    res_next = q + 1;
+  };
+  // (wave 0) resolve every step up to q in the foreground (compiler-waited look-back loads)
+  auto resolve_upto = [&](uint32_t q) {
+    if (lb_step != 0xFFFFFFFFu) {                    // a hand-waited look-back in flight: let it land
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lb_touch(lbd);
+      lb_step = 0xFFFFFFFFu;
+    }
+    uint64_t t0 = 0;
+    uint32_t spins = 0;
+    while (res_next <= q) {
+      const uint32_t u = sh.grp[res_next % kLineGrpQ];
+      const uint32_t W = u < kLbSlots ? u : kLbSlots;
+      uint64_t d[kLbPer];
+      lb_load(A, u, W, lane, d);
+      uint64_t P = 0;
+      if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P)) {
+        resolved(res_next, P);
+        continue;
+      }
+      if (wait_expired(spins++, t0)) {               // give up: flag it and release the waiting waves
+        if (lane == 0) atomicOr(A.err, kErrTimeout);
+        resolved(res_next, 0ull);
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  // (every wave) place steps nb .. q, waiting for their prefixes
+  auto place_upto = [&](uint32_t q) {
+    for (; nb <= q; ++nb) {
+      if (wave == 0) {
+        resolve_upto(nb);
+      } else {
+        const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
+        uint64_t t0 = 0;
+        for (uint32_t spins = 0; lds_ld(&sh.res[nb % kLineSlots]) != want; ++spins) {
+          if (wait_expired(spins, t0)) {
+            if (lane == 0) atomicOr(A.err, kErrTimeout);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        cbar();
+      }
+      place(nb);
+    }
+  };
+
+  uint32_t it = 0;
+  for (;; ++it) {
+    __syncthreads();
+    const uint32_t gnext = sh.grp[(it + 1) % kLineGrpQ];
+    const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
+    const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD &&
+                          sh.grp[(claimed - 1) % kLineGrpQ] < ngroups;
+    if (do_claim) run = sh.grp[(claimed - 1) % kLineGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
+    const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
+    const uint32_t slot = it % kLineSlots;
+    // every wave wrote step it - 1's count before the barrier: its AGG goes out first (before anything blocks)
+    if (wave == 0 && it > 0) publish_agg(it - 1);
+    // the slot this step fills held step it - kLineSlots: it must be placed by this wave first
+    if (it >= kLineSlots && nb <= it - kLineSlots) place_upto(it - kLineSlots);
+    uint32_t nev = 0;
+    const int lo = (int)g.lo_u, hi = (int)g.hi_u;
+    const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
+    uint16_t* evw = sh.ev[slot][wave];
+    auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kLineCap - 1u ? rk : kLineCap - 1u] = (uint16_t)pos; };
+#pragma unroll
+    for (int h = 0; h < kBufs; ++h) {
+      wait_buf(b[h]);                                 // this buffer landed; the other stays in flight
+      if (h == 0 && do_claim) {                       // the youngest vector-memory operation until the next wait
+        claim_res = atomic_add_nowait(ticket, run);
+        pend = run;
+      }
+      if (h == kBufs - 1 && pend) {                   // the wait above covered the claim: its value is back
+        asm volatile("" : "+v"(claim_res) :: "memory");
+        const uint32_t u = 2u * G + rfl(claim_res);
+        if (lane == 0)
+          for (uint32_t i = 0; i < pend; ++i) sh.grp[(claimed + i) % kLineGrpQ] = u + i;
+        claimed += pend;
+        pend = 0;
+      }
+      if (wave == 0) {
+        // the look-back issued at the previous wait point has landed (a buffer's loads were issued after it)
+        if (lb_step != 0xFFFFFFFFu) {
+          lb_touch(lbd);
+          uint64_t P = 0;
+          const uint32_t q = lb_step;
+          lb_step = 0xFFFFFFFFu;
+          if (lb_count_window(A, sh.grp[q % kLineGrpQ], lbd, lane, P)) resolved(q, P);
+        }
+        if (res_next < agg_next) {                    // the oldest unresolved group with a published AGG
+          const uint32_t u = sh.grp[res_next % kLineGrpQ];
+          lb_issue_nowait(A, u, u < kLbSlots ? u : kLbSlots, lane, lbd);
+          lb_step = res_next;
+        }
+      }
+      v4u x[kRows];
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
+      if (interior) delim_rows<true>(x, h, lo, hi, key, lane, nev, keep);
+      else delim_rows<false>(x, h, lo, hi, key, lane, nev, keep);
+      if (h + 1 < kBufs) load_buf(b[h], A, gn, 0, lane, h);
+    }
+    cbar();
+    if (lane == 0) {
+      const bool valid = (g.fl & kGeoValid) != 0u;
+      sh.cnt[slot][wave] = valid ? (nev | (nev > kLineCap ? kLineDense : 0u)) : 0u;
+      sh.geo[slot][wave] = uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32),
+                                 g.lo_u | (valid ? kLineValid : 0u) | ((g.fl & kGeoFirst) ? kLineFirst : 0u) |
+                                     ((g.fl & kGeoLast) ? kLineLast : 0u) | (g.hi_u << 16),
+                                 g.c};
+    }
+    // place every older step whose prefix is known (wave-local order)
+    while (nb < it) {
+      const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
+      if (lds_ld(&sh.res[nb % kLineSlots]) != want) break;
+      cbar();
+      place(nb);
+      ++nb;
+    }
+    load_buf(b[kBufs - 1], A, gn, 0, lane, kBufs - 1);
+    if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
+    r = rn;
+    g = gn;
+  }
+  drain_bufs(b);
+  if (wave == 0 && lb_step != 0xFFFFFFFFu) {         // drained with the buffers above
+    lb_touch(lbd);
+    lb_step = 0xFFFFFFFFu;
+  }
+  __syncthreads();                                    // every wave's last count is in LDS
+  if (wave == 0) publish_agg(it);
+  place_upto(it);
+  if (ovf) atomicOr(A.err, kErrOverflow);
+}
+
 // x - pa clamped to 0..16 (the byte bound inside one 16-byte lane), without 32-bit truncation
 __device__ __forceinline__ int lane_rel(uint64_t x, uint64_t pa) {
   return x <= pa ? 0 : (x - pa >= 16u ? 16 : (int)(x - pa));
@@ -2600,6 +2924,8 @@ struct dp_ctx {
   uint64_t rec_cap = 0;               // ranges
   bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
   uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
+  int delim_form = 0;                 // newline kernels: 0 auto (by size), 1 line_kernel, 2 two kernels, 3 one-pass
+  uint32_t line_launches = 0;         // line_kernel launches (ticket parity)
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
   uint64_t nchunks = 0, cap = 0;
@@ -2692,8 +3018,9 @@ int harvest_events(dp_ctx* c) {
 }
 
 // Lay out the chunk table in aligned coordinates and enqueue its upload when it changed.
-// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[6] (err | total | spare x2 |
-// unit ticket: next unit, workgroups finished | map-kernel group ticket: the same pair; zero between launches).
+// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[7] (err | total | spare x2 |
+// unit ticket: next unit, workgroups finished | map-kernel group ticket: the same pair; zero between launches |
+// line_kernel's two group tickets: a launch claims from one half and zeroes the other, the next launch's).
 // No per-launch reset: every launch rewrites pending / chunk_end of each non-empty chunk and total (when it
 // has units), so only the upload sets their defaults (-1, ~0, 0) and err = 0.  A launch that sets an err
 // bit drops last_tab, so the next one re-uploads (results of a failed launch are discarded anyway).
@@ -2715,7 +3042,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
   }
   tab[3 * n] = units;
   tab.push_back(unit_bytes);                          // (host-side only: a change of geometry re-uploads)
-  const uint64_t words = 5 * n + 1 + 6;
+  const uint64_t words = 5 * n + 1 + 7;
   int rc = ensure_tab(c, words);
   if (rc) return rc;
   c->pend_off = 3 * n + 1;
@@ -2725,7 +3052,7 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(c->h_tab, tab.data(), (3 * n + 1) * 8);
     memset(c->h_tab + c->pend_off, 0xFF, 2 * n * 8);
-    memset(c->h_tab + c->ctrl_off, 0, 6 * 8);
+    memset(c->h_tab + c->ctrl_off, 0, 7 * 8);
     HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, words * 8, hipMemcpyHostToDevice, c->stream));
     c->last_tab.swap(tab);
   }
@@ -3028,6 +3355,79 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   return scan_leave(c, ss);
 }
 
+// The lockstep one-pass newline index (line_kernel), over the same 16 KiB-range staging as launch_delim2.
+int launch_line(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
+                int kind, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
+                uint32_t wrap32, unsigned long long* blocktab, uint64_t tab_j0, uint64_t tab_n) {
+  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
+  if (nranges == 0) return DP_OK;
+  if (nranges >= 0xFFFFFFFFull - kMapWaves) return fail(DP_ERR_INVALID, "launch exceeds 2^32 ranges of 16 KiB");
+  const uint64_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
+  int rc = ensure_desc(c, ngroups);
+  if (rc) return rc;
+  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
+    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
+    c->desc_epoch = 0;
+  }
+  ScanArgs a;
+  memset(&a, 0, sizeof(a));
+  a.base = d_buf - shift;
+  a.shift = shift;
+  a.obj_base = buf_base;
+  a.nchunks = n;
+  a.nunits = nranges;
+  a.desc = c->d_desc;
+  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
+  if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
+    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
+    cap = 1;
+  }
+  a.out = d_out;
+  a.cap = cap;
+  a.out_u64 = kind;
+  a.wrap32 = wrap32;
+  a.blocktab = blocktab;
+  a.tab_j0 = tab_j0;
+  a.tab_n = tab_n;
+  a.carry = carry;
+  a.delim = delim * 0x01010101u;
+  a.every_k = every_k;
+  a.emit_add = emit_add;
+  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
+  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
+  a.ticket = nullptr;
+  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
+  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  LineArgs L;
+  L.base = a.base;
+  L.nchunks = n;
+  L.nranges = nranges;
+  L.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 6);
+  L.parity = (c->line_launches++) & 1u;
+  const unsigned grid = (unsigned)(ngroups < (uint64_t)c->cus ? ngroups : (uint64_t)c->cus);
+  const uint64_t* tlo = c->d_tab;
+  const uint64_t* thi = c->d_tab + n;
+  const uint64_t* tr0 = c->d_tab + 2 * n;
+  DeviceSerial& ds = g_serial[c->device];
+  std::lock_guard<std::mutex> lock(ds.m);
+  hipStream_t ss = nullptr;
+  rc = scan_enter(c, ds, &ss);
+  if (rc) return rc;
+  hipEvent_t e0;
+  rc = ev_begin(c, &e0, ss);
+  if (rc) return rc;
+  if (kind == 1)
+    hipLaunchKernelGGL((line_kernel<1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  else if (kind == 2)
+    hipLaunchKernelGGL((line_kernel<2>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  else
+    hipLaunchKernelGGL((line_kernel<0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  HIPCHK(hipGetLastError());
+  rc = ev_end(c, ss);
+  if (rc) return rc;
+  return scan_leave(c, ss);
+}
+
 int check_ctx(dp_ctx* c) {
   if (!c) return fail(DP_ERR_INVALID, "null dp_ctx");
   HIPCHK(hipSetDevice(c->device));
@@ -3101,6 +3501,9 @@ int dp_ctx_create(int device, dp_ctx** out) {
   // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
   const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
   c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
+  // newline kernels (A/B): DP_DELIM_FORM = line | two | one (default: by launch size)
+  const char* form = getenv("DP_DELIM_FORM");
+  c->delim_form = !form ? 0 : (!strcmp(form, "line") ? 1 : (!strcmp(form, "two") ? 2 : (!strcmp(form, "one") ? 3 : 0)));
   *out = c;
   return DP_OK;
 }
@@ -3338,7 +3741,12 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   uint64_t units = 0, span = 0;
   for (uint64_t i = 0; i < nr; ++i) span += rg[2 * i + 1] - rg[2 * i];
   const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
-  if (span <= c->delim_twopass_max) {                 // the two-kernel form
+  if (c->delim_form == 1) {                           // the lockstep one-pass kernel
+    rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
+    if (rc) return rc;
+    rc = launch_line(c, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
+                     out_mode == 2, tab, j0, ntab);
+  } else if (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) {   // two kernels
     rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
     if (rc) return rc;
     rc = launch_delim2(c, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,

@@ -28,7 +28,7 @@ SRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "dpscan.h
 # every kernel symbol of the device assembly (anonymous-namespace kernels: _ZN12_GLOBAL__N_1<len><name>...)
 KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1\d+\w+?_kernel\w*):", re.M)
 # kernels the shipped library must contain (a build that lost one is not the library the tests describe)
-REQUIRED = ("scan_kernel", "map_kernel", "fasta_place_kernel", "delim_place_kernel", "fasta_resolve_kernel",
+REQUIRED = ("scan_kernel", "map_kernel", "fasta_place_kernel", "delim_place_kernel", "line_kernel", "fasta_resolve_kernel",
             "find_kernel", "stream_kernel", "stream_rw_kernel")
 
 
@@ -122,8 +122,10 @@ def _scan(ins, q, problems, k):
         if VMEM_RE.match(op):
             # hand-waited destinations: the input buffer loads and the returning (sc0) ticket atomic
             # (global atomics: only the inline-asm claims are hand-waited; the compiler waits for its own)
+            # (and inline-asm global loads: line_kernel's look-back descriptors, read after a later buffer wait)
             if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]) or \
-                    (op.startswith("global_atomic") and "sc0" in toks[1:] and "@asm" in toks[1:]):
+                    (op.startswith("global_atomic") and "sc0" in toks[1:] and "@asm" in toks[1:]) or \
+                    (op.startswith("global_load") and "@asm" in toks[1:]):
                 dst = regs(toks[1])
                 srcs = set()
                 for t in toks[2:]:

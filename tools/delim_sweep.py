@@ -1,7 +1,9 @@
-"""Newline index: one-pass vs two-kernel form over launch sizes, on CSV / VCF / FASTA bytes (same box).
+"""Newline index: its kernel forms over launch sizes, on CSV / VCF / FASTA bytes (same box).
 
-Two contexts on device 0, one created with DP_DELIM_TWOPASS_MAX=0 (every launch one-pass) and one with it
-above every size (every launch two kernels), run `dp_delim_ranges` over [0, size) of the same resident
+Contexts on device 0 pinned to one form each -- the one-pass look-back kernel (DP_DELIM_TWOPASS_MAX=0), the
+two-kernel form (map + placement: DP_DELIM_TWOPASS_MAX above every size) and, round 4, the lockstep one-pass
+line_kernel (DP_DELIM_FORM=line) -- plus the library's default choice, run `dp_delim_ranges` over [0, size) of
+the same resident
 object in the stored CSV/VCF form (out_mode 3: uint16 low words + the 64 KiB block table) and time the scan
 with HIP events.  Both outputs are compared byte for byte at every size, and the linear fit t = a + b * size
 per form gives its fixed cost and steady rate: where the lines cross is the crossover the library's
@@ -24,11 +26,22 @@ from dataplug_amd import synth  # noqa: E402
 from dataplug_amd.scan import ScanContext  # noqa: E402
 
 
-def make_ctx(twopass_max):
-    os.environ["DP_DELIM_TWOPASS_MAX"] = str(twopass_max)
+def make_ctx(twopass_max=None, form=None):
+    env = {"DP_DELIM_TWOPASS_MAX": None if twopass_max is None else str(twopass_max), "DP_DELIM_FORM": form}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
     ctx = ScanContext(0)
-    del os.environ["DP_DELIM_TWOPASS_MAX"]
-    assert ctx.forms()[1] == twopass_max, ctx.forms()
+    for k, v in old.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    if twopass_max is not None:
+        assert ctx.forms()[1] == twopass_max, ctx.forms()
     return ctx
 
 
@@ -37,11 +50,14 @@ def main():
     ap.add_argument("--content", default="csv,vcf,fasta")
     ap.add_argument("--sizes-gib", default="0.0625,0.25,0.5,1,2,4")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--forms", default="onepass,twokernel,line,default")
     args = ap.parse_args()
     sizes = [int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")]
     top = max(sizes)
-    forms = {"onepass": make_ctx(0), "twokernel": make_ctx(1 << 62)}
-    ctx0 = forms["onepass"]
+    makers = {"onepass": lambda: make_ctx(0, "one"), "twokernel": lambda: make_ctx(1 << 62, "two"),
+              "line": lambda: make_ctx(None, "line"), "default": lambda: make_ctx()}
+    forms = {k: makers[k]() for k in args.forms.split(",")}
+    ctx0 = next(iter(forms.values()))
     d = ctx0.workspace("in", top + 64)
     for content in args.content.split(","):
         if content == "fasta":
@@ -78,9 +94,13 @@ def main():
                 res[name] = (n, words, ctx.block_table(out.ptr, cap, ranges))
                 line[f"{name}_us"] = round(t * 1e6, 1)
                 line[f"{name}_GBps"] = round(size / t / 1e9, 1)
-            a, b = res["onepass"], res["twokernel"]
+                # roofline fraction on algorithmic bytes: input + 2 B per entry + 8 B per 64 KiB block
+                line[f"{name}_frac"] = round((size + 2 * n + 8 * len(res[name][2])) / t / 8e12, 4)
+            vals = list(res.values())
+            a = vals[0]
             line["entries"] = a[0]
-            line["equal"] = bool(a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]))
+            line["equal"] = bool(all(b[0] == a[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+                                     for b in vals[1:]))
             print(json.dumps(line), flush=True)
             if not line["equal"]:
                 print("MISMATCH", flush=True)

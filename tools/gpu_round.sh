@@ -15,7 +15,7 @@ if [ "${2:-}" != quick ]; then
   tail -1 $O/smoke.log
 fi
 step bench
-/usr/bin/time -v timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
-grep -E "Elapsed|Maximum resident" $O/bench.err
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+
 python3 tools/bench_summary.py $O/bench.json
 step done
