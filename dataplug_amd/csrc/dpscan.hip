@@ -2417,6 +2417,11 @@ constexpr uint32_t kLineGrpQ = 8;                  // claimed groups by step (>=
 static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + 1, "group queue spans the pending and claimed steps");
 constexpr uint32_t kLineDense = 0x80000000u;
 constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
+// A look-back window (kLbSlots descriptors before a group) arrives by LDS-DMA: kLineWinLoads 16-byte-per-lane
+// loads from an even descriptor index, so 384 descriptors cover any 256 before the group.
+constexpr uint32_t kLineWinLoads = 3;
+constexpr uint32_t kLineWin = kLineWinLoads * kWave * 2;
+static_assert(kLineWin >= kLbSlots + 2 + 126, "window loads cover kLbSlots descriptors from an even start");
 
 struct LineShared {
   uint16_t ev[kLineSlots][kMapWaves][kLineCap];    // per slot and wave: the range's positions
@@ -2427,29 +2432,49 @@ struct LineShared {
   unsigned long long tot[kLineSlots];              // the group's delimiters
   uint32_t res[kLineSlots];
   uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
+  unsigned long long win[kLineWin];                // wave 0: a look-back window's descriptors, by LDS-DMA
+  unsigned long long win_dummy[kLineWin];          // every other wave's / step's window loads (never read)
 };
 
 struct LineArgs {
   const uint8_t* base;          // = ScanArgs::base
   uint64_t nchunks, nranges;
+  uint64_t desc_cap;            // descriptors allocated (a window load never reads past them)
   unsigned int* ticket;         // [2] group tickets: this launch claims from ticket[parity] and zeroes the other
   uint32_t parity;
 };
 
-// Look-back loads of group u's window, hand-waited (inline asm: the compiler adds no wait; the caller reads
-// them after a buffer wait that covers them).  Relaxed agent-scope loads (sc1), as ld_desc.
-__device__ __forceinline__ void lb_issue_nowait(const ScanArgs& A, uint32_t u, uint32_t W, int lane, uint64_t (&d)[kLbPer]) {
+// LDS byte address of a __shared__ object (the LDS-DMA destination base, M0)
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// Look-back window of group u into LDS by LDS-DMA, hand-waited (inline asm: the compiler adds no wait, and no
+// VGPR is held while the loads travel): descriptors [base, base + kLineWin) of which [u - kLbSlots, u) matter.
+// Relaxed agent-scope reads (sc1), as ld_desc.  Returns base.
+__device__ __forceinline__ uint64_t lb_window_dma(const ScanArgs& A, uint64_t desc_cap, uint32_t u, unsigned long long* win,
+                                                  int lane) {
+  uint64_t base = u > kLbSlots ? ((uint64_t)(u - kLbSlots) & ~1ull) : 0ull;
+  if (base + kLineWin > desc_cap) base = desc_cap - kLineWin;      // (desc_cap: a multiple of 1024 >= kLineWin)
+  const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(win));
+#pragma unroll
+  for (uint32_t i = 0; i < kLineWinLoads; ++i) {
+    const void* g = A.desc + base + i * 2u * kWave + 2u * (uint32_t)lane;
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(g), "s"(dst + i * 16u * kWave) : "memory");
+  }
+  return base;
+}
+// the window of group u from LDS (after a wait that retired its loads), as lb_load lays it out
+__device__ __forceinline__ void lb_window_read(const unsigned long long* win, uint64_t base, uint32_t u, int lane,
+                                               uint64_t (&d)[kLbPer]) {
+  const uint32_t W = u < kLbSlots ? u : kLbSlots;
   const uint32_t rl = (uint32_t)(kWave - 1 - lane);
 #pragma unroll
   for (int j = 0; j < kLbPer; ++j) {
     const uint32_t k = kLbPer * rl + j;
-    const unsigned long long* p = A.desc + (k < W ? u - 1 - k : 0u);
-    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(d[j]) : "v"(p) : "memory");
+    d[j] = k < W ? win[(uint64_t)(u - 1 - k) - base] : 0ull;
   }
-}
-__device__ __forceinline__ void lb_touch(uint64_t (&d)[kLbPer]) {
-#pragma unroll
-  for (int j = 0; j < kLbPer; ++j) asm volatile("" : "+v"(d[j]) :: "memory");
 }
 // Reduce a loaded window of group u: true with the group's launch prefix P once resolvable.
 __device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P) {
@@ -2496,7 +2521,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t nb = 0;                                   // (every wave) the next step to place
   // (wave 0) steps with a published AGG / a resolved prefix; the step of the look-back in flight
   uint32_t agg_next = 0, res_next = 0, lb_step = 0xFFFFFFFFu;
-  uint64_t lbd[kLbPer] = {0, 0, 0, 0};
+  uint64_t lb_base = 0;
 
   // phase B of step q for this wave's range
   auto place = [&](uint32_t q) {
@@ -2560,7 +2585,6 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   auto resolve_upto = [&](uint32_t q) {
     if (lb_step != 0xFFFFFFFFu) {                    // a hand-waited look-back in flight: let it land
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lb_touch(lbd);
       lb_step = 0xFFFFFFFFu;
     }
     uint64_t t0 = 0;
@@ -2604,6 +2628,11 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
   };
 
+  // Vector-memory order per step (vmcnt counts in issue order): [b1 reload of the previous step] | wait b0 |
+  // claim atomic, wave 0's descriptor stores | b0 reload | wave 0's look-back window (LDS-DMA: no VGPRs held) |
+  // wait b1 (the b0 reload and the window may stay in flight) | phase-B stores | b1 reload | barrier | wait b0:
+  // the window has landed.  So the look-back travels for a whole step and no wait covers a load just issued.
+  static_assert(kBufs == 2, "line_kernel: two input buffers per range");
   uint32_t it = 0;
   for (;; ++it) {
     __syncthreads();
@@ -2614,52 +2643,64 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     if (do_claim) run = sh.grp[(claimed - 1) % kLineGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
     const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
     const uint32_t slot = it % kLineSlots;
-    // every wave wrote step it - 1's count before the barrier: its AGG goes out first (before anything blocks)
-    if (wave == 0 && it > 0) publish_agg(it - 1);
-    // the slot this step fills held step it - kLineSlots: it must be placed by this wave first
-    if (it >= kLineSlots && nb <= it - kLineSlots) place_upto(it - kLineSlots);
     uint32_t nev = 0;
     const int lo = (int)g.lo_u, hi = (int)g.hi_u;
     const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
     uint16_t* evw = sh.ev[slot][wave];
     auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kLineCap - 1u ? rk : kLineCap - 1u] = (uint16_t)pos; };
-#pragma unroll
-    for (int h = 0; h < kBufs; ++h) {
-      wait_buf(b[h]);                                 // this buffer landed; the other stays in flight
-      if (h == 0 && do_claim) {                       // the youngest vector-memory operation until the next wait
-        claim_res = atomic_add_nowait(ticket, run);
-        pend = run;
-      }
-      if (h == kBufs - 1 && pend) {                   // the wait above covered the claim: its value is back
-        asm volatile("" : "+v"(claim_res) :: "memory");
-        const uint32_t u = 2u * G + rfl(claim_res);
-        if (lane == 0)
-          for (uint32_t i = 0; i < pend; ++i) sh.grp[(claimed + i) % kLineGrpQ] = u + i;
-        claimed += pend;
-        pend = 0;
-      }
-      if (wave == 0) {
-        // the look-back issued at the previous wait point has landed (a buffer's loads were issued after it)
-        if (lb_step != 0xFFFFFFFFu) {
-          lb_touch(lbd);
-          uint64_t P = 0;
-          const uint32_t q = lb_step;
-          lb_step = 0xFFFFFFFFu;
-          if (lb_count_window(A, sh.grp[q % kLineGrpQ], lbd, lane, P)) resolved(q, P);
-        }
-        if (res_next < agg_next) {                    // the oldest unresolved group with a published AGG
-          const uint32_t u = sh.grp[res_next % kLineGrpQ];
-          lb_issue_nowait(A, u, u < kLbSlots ? u : kLbSlots, lane, lbd);
-          lb_step = res_next;
-        }
-      }
-      v4u x[kRows];
-#pragma unroll
-      for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
-      if (interior) delim_rows<true>(x, h, lo, hi, key, lane, nev, keep);
-      else delim_rows<false>(x, h, lo, hi, key, lane, nev, keep);
-      if (h + 1 < kBufs) load_buf(b[h], A, gn, 0, lane, h);
+    v4u x[kRows];
+    // ---- buffer 0
+    wait_buf(b[0]);                                   // the youngest operations in flight: b[1]'s loads
+    if (do_claim) {
+      claim_res = atomic_add_nowait(ticket, run);
+      pend = run;
     }
+    if (wave == 0) {
+      if (lb_step != 0xFFFFFFFFu) {                   // issued a step ago, older than b[1]'s loads: landed
+        const uint32_t q = lb_step, u = sh.grp[q % kLineGrpQ];
+        lb_step = 0xFFFFFFFFu;
+        uint64_t d[kLbPer];
+        lb_window_read(sh.win, lb_base, u, lane, d);
+        uint64_t P = 0;
+        if (lb_count_window(A, u, d, lane, P)) resolved(q, P);
+      }
+      // every wave wrote step it - 1's count before the barrier: its AGG goes out before anything blocks
+      if (it > 0) publish_agg(it - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) x[i] = b[0].x[i];
+    if (interior) delim_rows<true>(x, 0, lo, hi, key, lane, nev, keep);
+    else delim_rows<false>(x, 0, lo, hi, key, lane, nev, keep);
+    load_buf(b[0], A, gn, 0, lane, 0);
+    // Every wave issues the window's kLineWinLoads LDS-DMA loads every step, so the wait below has one count on
+    // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
+    // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
+    // (other waves, or no such group) land in the wave's own dummy area and are never read.
+    {
+      const bool want = wave == 0 && res_next < agg_next;
+      const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
+      const uint64_t base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
+      if (want) {
+        lb_base = base;
+        lb_step = res_next;
+      }
+    }
+    // ---- buffer 1
+    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsPerBuf + kLineWinLoads) : "memory");   // b[0] + window in flight
+    touch_buf(b[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (pend) {                                       // the wait above covered the claim: its value is back
+      asm volatile("" : "+v"(claim_res) :: "memory");
+      const uint32_t u = 2u * G + rfl(claim_res);
+      if (lane == 0)
+        for (uint32_t i = 0; i < pend; ++i) sh.grp[(claimed + i) % kLineGrpQ] = u + i;
+      claimed += pend;
+      pend = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < kRows; ++i) x[i] = b[1].x[i];
+    if (interior) delim_rows<true>(x, 1, lo, hi, key, lane, nev, keep);
+    else delim_rows<false>(x, 1, lo, hi, key, lane, nev, keep);
     cbar();
     if (lane == 0) {
       const bool valid = (g.fl & kGeoValid) != 0u;
@@ -2677,16 +2718,17 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       place(nb);
       ++nb;
     }
+    // the next step fills the slot of step it + 1 - kLineSlots: this wave must have placed it.  Blocking here
+    // (only b[0]'s loads in flight, so the registers are free) holds back this workgroup's AGG of step it, its
+    // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+    if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
     load_buf(b[kBufs - 1], A, gn, 0, lane, kBufs - 1);
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
   }
-  drain_bufs(b);
-  if (wave == 0 && lb_step != 0xFFFFFFFFu) {         // drained with the buffers above
-    lb_touch(lbd);
-    lb_step = 0xFFFFFFFFu;
-  }
+  drain_bufs(b);                                      // (and a look-back window still in flight)
+  lb_step = 0xFFFFFFFFu;
   __syncthreads();                                    // every wave's last count is in LDS
   if (wave == 0) publish_agg(it);
   place_upto(it);
@@ -3402,6 +3444,7 @@ int launch_line(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, 
   L.base = a.base;
   L.nchunks = n;
   L.nranges = nranges;
+  L.desc_cap = c->desc_cap;
   L.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 6);
   L.parity = (c->line_launches++) & 1u;
   const unsigned grid = (unsigned)(ngroups < (uint64_t)c->cus ? ngroups : (uint64_t)c->cus);

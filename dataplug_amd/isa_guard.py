@@ -126,7 +126,7 @@ def _scan(ins, q, problems, k):
             if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]) or \
                     (op.startswith("global_atomic") and "sc0" in toks[1:] and "@asm" in toks[1:]) or \
                     (op.startswith("global_load") and "@asm" in toks[1:]):
-                dst = regs(toks[1])
+                dst = set() if "_lds" in op else regs(toks[1])   # LDS-DMA: no VGPR destination
                 srcs = set()
                 for t in toks[2:]:
                     srcs |= regs(t)
