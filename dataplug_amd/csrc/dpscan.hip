@@ -2409,6 +2409,12 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_CAP
 #define DP_LINE_CAP 640
 #endif
+#ifndef DP_LINE_EARLY      // b[1]'s reload before the step's placements (0: after them)
+#define DP_LINE_EARLY 1
+#endif
+#ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
+#define DP_LINE_PRIO 0
+#endif
 constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
 constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
 static_assert(kLineSlots >= 3 && kLineSlots <= 6, "line slots: phase A, resolution, placement + slack");
@@ -2517,6 +2523,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   Buf b[kBufs];
 #pragma unroll
   for (int h = 0; h < kBufs; ++h) load_buf(b[h], A, g, 0, lane, h);
+  if (DP_LINE_PRIO && wave == 0) set_prio(DP_LINE_PRIO);
   bool ovf = false;
   uint32_t nb = 0;                                   // (every wave) the next step to place
   // (wave 0) steps with a published AGG / a resolved prefix; the step of the look-back in flight
@@ -2524,11 +2531,14 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint64_t lb_base = 0;
 
   // phase B of step q for this wave's range
-  auto place = [&](uint32_t q) {
+  // ``light``: only a range kept in LDS (false for a dense one, which waits for the full path: its rescan needs
+  // the registers that the input buffers in flight hold at the light call site)
+  auto place = [&](uint32_t q, bool light) -> bool {
     const uint32_t s = q % kLineSlots;
     const uint4 gq = sh.geo[s][wave];
-    if (!(gq.z & kLineValid)) return;
+    if (!(gq.z & kLineValid)) return true;
     const uint32_t cw = sh.cnt[s][wave];
+    if (light && (cw & kLineDense)) return false;
     const uint32_t n = cw & ~kLineDense;
     const uint64_t Pw = sh.P[s] + sh.ex[s][wave];
     const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
@@ -2544,13 +2554,17 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
           A.blocktab[j] = Pw;
       }
     }
+#ifdef DP_LINE_NOPLACE
+    return true;    // timing probe only (wrong results): every step's bookkeeping without the index stores
+#endif
     if (cw & kLineDense) {
       dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
-      return;
+      return true;
     }
     const uint16_t* evw = sh.ev[s][wave];
     // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
     ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
+    return true;
   };
   // (wave 0) step q's AGG: the group's count from the 16 ranges (lanes 0..15), their exclusive prefixes
   auto publish_agg = [&](uint32_t q) {
@@ -2624,7 +2638,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         }
         cbar();
       }
-      place(nb);
+      place(nb, false);
     }
   };
 
@@ -2710,19 +2724,32 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
                                      ((g.fl & kGeoLast) ? kLineLast : 0u) | (g.hi_u << 16),
                                  g.c};
     }
-    // place every older step whose prefix is known (wave-local order)
+    // the next step fills the slot of step it + 1 - kLineSlots: this wave must have placed it.  Blocking here
+    // (only b[0]'s loads in flight, so the registers are free) holds back this workgroup's AGG of step it, its
+    // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+#if DP_LINE_EARLY
+    if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
+    // b[1]'s reload goes out before this step's placements, so both buffers' loads travel during them
+    load_buf(b[kBufs - 1], A, gn, 0, lane, kBufs - 1);
+    // place every older step whose prefix is known (wave-local order); a dense range waits for the full path
     while (nb < it) {
       const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
       if (lds_ld(&sh.res[nb % kLineSlots]) != want) break;
       cbar();
-      place(nb);
+      if (!place(nb, true)) break;
       ++nb;
     }
-    // the next step fills the slot of step it + 1 - kLineSlots: this wave must have placed it.  Blocking here
-    // (only b[0]'s loads in flight, so the registers are free) holds back this workgroup's AGG of step it, its
-    // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+#else
+    while (nb < it) {
+      const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
+      if (lds_ld(&sh.res[nb % kLineSlots]) != want) break;
+      cbar();
+      place(nb, false);
+      ++nb;
+    }
     if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
     load_buf(b[kBufs - 1], A, gn, 0, lane, kBufs - 1);
+#endif
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
