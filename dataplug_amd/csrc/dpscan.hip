@@ -2409,8 +2409,8 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_CAP
 #define DP_LINE_CAP 640
 #endif
-#ifndef DP_LINE_EARLY      // b[1]'s reload before the step's placements (0: after them)
-#define DP_LINE_EARLY 1
+#ifndef DP_LINE_EARLY      // b[1]'s reload before the step's placements (0, default: after them; 1 measured
+#define DP_LINE_EARLY 0    // 962 vs 845 us per 4 GiB CSV: the stores then sit after the reload in vmcnt order)
 #endif
 #ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
 #define DP_LINE_PRIO 0

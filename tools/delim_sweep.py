@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--sizes-gib", default="0.0625,0.25,0.5,1,2,4")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--forms", default="onepass,twokernel,line,default")
+    ap.add_argument("--no-check", action="store_true", help="timing probes with wrong results: keep going")
     args = ap.parse_args()
     sizes = [int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")]
     top = max(sizes)
@@ -102,7 +103,7 @@ def main():
             line["equal"] = bool(all(b[0] == a[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
                                      for b in vals[1:]))
             print(json.dumps(line), flush=True)
-            if not line["equal"]:
+            if not line["equal"] and not args.no_check:
                 print("MISMATCH", flush=True)
                 sys.exit(1)
         for name, ts in rows.items():
