@@ -991,11 +991,15 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
   const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
   const uint32_t k = A.every_k;
   // every k-th delimiter overall (FASTQ read ends), counting from the carried ordinal: list entries
-  // r0, r0 + k, ... go to q0, q0 + 1, ...
-  const uint64_t Pc = P + A.carry;
-  const uint32_t r0 = k == 1u ? 0u : (uint32_t)((k - 1u) - Pc % k);
-  const uint64_t q0 = (Pc + r0) / k - A.carry / k;
-  const uint32_t nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
+  // r0, r0 + k, ... go to q0, q0 + 1, ...  (k == 1, the newline index: no 64-bit divisions)
+  uint32_t r0 = 0, nq = nev;
+  uint64_t q0 = P;
+  if (k != 1u) {
+    const uint64_t Pc = P + A.carry;
+    r0 = (uint32_t)((k - 1u) - Pc % k);
+    q0 = (Pc + r0) / k - A.carry / k;
+    nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
+  }
 #if DP_PAIRSTORE
   if constexpr (OUT64 == 1 && PAIR) {
     // Every delimiter, uint64 output, the whole list in bounds (wave-uniform): two offsets per lane and
