@@ -2427,6 +2427,7 @@ constexpr uint32_t kLineGrpQ = 8;                  // claimed groups by step (>=
 static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + 1, "group queue spans the pending and claimed steps");
 constexpr uint32_t kLineDense = 0x80000000u;
 constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
+constexpr uint32_t kLineEnd = 128u;                // geo.z: the launch's last range (writes the total)
 // A look-back window (kLbSlots descriptors before a group) arrives by LDS-DMA: kLineWinLoads 16-byte-per-lane
 // loads from an even descriptor index, so 384 descriptors cover any 256 before the group.
 constexpr uint32_t kLineWinLoads = 3;
@@ -2438,7 +2439,7 @@ struct LineShared {
   uint4 geo[kLineSlots][kMapWaves];                // {wbase lo, wbase hi, lo_w | flags | hi_w << 16, chunk}
   uint32_t cnt[kLineSlots][kMapWaves];             // the range's delimiters (| kLineDense)
   uint32_t ex[kLineSlots][kMapWaves];              // delimiters of the group before the range (wave 0)
-  unsigned long long P[kLineSlots];                // the group's launch prefix, valid once res == group + 1
+  unsigned long long pw[kLineSlots][kMapWaves];    // the range's launch prefix, valid once res == group + 1
   unsigned long long tot[kLineSlots];              // the group's delimiters
   uint32_t res[kLineSlots];
   uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
@@ -2539,18 +2540,19 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   // the registers that the input buffers in flight hold at the light call site)
   auto place = [&](uint32_t q, bool light) -> bool {
     const uint32_t s = q % kLineSlots;
+    // every LDS read up front (one round trip: the branches below would otherwise serialize them)
     const uint4 gq = sh.geo[s][wave];
-    if (!(gq.z & kLineValid)) return true;
     const uint32_t cw = sh.cnt[s][wave];
+    const uint64_t Pw = sh.pw[s][wave];
+    if (!(gq.z & kLineValid)) return true;
     if (light && (cw & kLineDense)) return false;
     const uint32_t n = cw & ~kLineDense;
-    const uint64_t Pw = sh.P[s] + sh.ex[s][wave];
     const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
     const uint32_t lo_w = gq.z & 15u, hi_w = gq.z >> 16;
     const uint64_t off0 = A.obj_base - A.shift + wbase;
     if (lane == 0) {
       if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
-      if (sh.grp[q % kLineGrpQ] * kMapWaves + (uint32_t)wave + 1u == nranges) A.total[0] = Pw + n;
+      if (gq.z & kLineEnd) A.total[0] = Pw + n;
       if constexpr (OUT64 == 2) {
         // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
         const uint64_t j = (off0 >> 16) - A.tab_j0;
@@ -2591,9 +2593,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   auto resolved = [&](uint32_t q, uint64_t P) {
     const uint32_t s = q % kLineSlots;
     const uint32_t u = sh.grp[q % kLineGrpQ];
+    if (lane < (int)kMapWaves) sh.pw[s][lane] = P + sh.ex[s][lane];   // every range's launch prefix
+    cbar();
     if (lane == 0) {
-      sh.P[s] = P;
-      cbar();
       lds_st(&sh.res[s], u + 1u);
       st_desc(&A.desc[u], pack_count(kStatPrefix, P + sh.tot[s]) | A.epoch);
     }
@@ -2725,7 +2727,8 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       sh.cnt[slot][wave] = valid ? (nev | (nev > kLineCap ? kLineDense : 0u)) : 0u;
       sh.geo[slot][wave] = uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32),
                                  g.lo_u | (valid ? kLineValid : 0u) | ((g.fl & kGeoFirst) ? kLineFirst : 0u) |
-                                     ((g.fl & kGeoLast) ? kLineLast : 0u) | (g.hi_u << 16),
+                                     ((g.fl & kGeoLast) ? kLineLast : 0u) | (r + 1u == nranges ? kLineEnd : 0u) |
+                                     (g.hi_u << 16),
                                  g.c};
     }
     // the next step fills the slot of step it + 1 - kLineSlots: this wave must have placed it.  Blocking here
