@@ -691,6 +691,35 @@ __device__ __forceinline__ void drain_bufs(Buf (&b)[kBufs]) {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// The same buffers without the lookahead dword (a FASTA row needs the byte after it; a delimiter row does not):
+// kRows loads per buffer, 2 VGPRs fewer per wave (line_kernel runs at the 128-VGPR limit).
+struct BufN {
+  v4u x[kRows];
+};
+constexpr int kLoadsPerBufN = kRows;
+__device__ __forceinline__ void load_buf_n(BufN& b, const ScanArgs& A, const Geo& g, int lane, int half) {
+  int hb = (g.fl & kGeoValid) ? wave_hi(g, 0) - half * kBufBytes : 0;
+  hb = hb < 0 ? 0 : (hb > kBufBytes + 16 ? kBufBytes + 16 : hb);
+  const v4i r = buf_rsrc(A.base, g.ubase + (uint64_t)half * kBufBytes, hb);
+  Buf& bb = *reinterpret_cast<Buf*>(&b);          // (load_rows writes x[] only)
+  load_rows<kRows>(bb, (uint32_t)lane * 16u, r);
+}
+__device__ __forceinline__ void touch_buf_n(BufN& b) {
+#pragma unroll
+  for (int r = 0; r < kRows; ++r) asm volatile("" : "+v"(b.x[r]) :: "memory");
+}
+__device__ __forceinline__ void wait_buf_n(BufN& b) {
+  asm volatile("s_waitcnt vmcnt(%0)" :: "i"((kBufs - 1) * kLoadsPerBufN) : "memory");
+  touch_buf_n(b);
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void drain_bufs_n(BufN (&b)[kBufs]) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int h = 0; h < kBufs; ++h) touch_buf_n(b[h]);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // ------------------------------------------------------------------------------------------ LDS state
 struct WaveRec {                   // one data wave's phase-A result for one unit (written by its lane 0)
   uint64_t wbase;                  // aligned coordinate of the wave range's first byte
@@ -2413,8 +2442,8 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_CAP
 #define DP_LINE_CAP 640
 #endif
-#ifndef DP_LINE_EARLY      // b[1]'s reload before the step's placements (0, default: after them; 1 measured
-#define DP_LINE_EARLY 0    // 962 vs 845 us per 4 GiB CSV: the stores then sit after the reload in vmcnt order)
+#ifndef DP_LINE_GROUP      // the uint16 index's placements as one contiguous run per group (0: one run per range)
+#define DP_LINE_GROUP 1
 #endif
 #ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
 #define DP_LINE_PRIO 0
@@ -2441,9 +2470,13 @@ struct LineShared {
   uint32_t ex[kLineSlots][kMapWaves];              // delimiters of the group before the range (wave 0)
   unsigned long long pw[kLineSlots][kMapWaves];    // the range's launch prefix, valid once res == group + 1
   unsigned long long tot[kLineSlots];              // the group's delimiters
+  uint32_t b16[kLineSlots][kMapWaves];             // low 16 bits of the range's first object offset
   uint32_t res[kLineSlots];
+  uint32_t rstep[kLineSlots];                      // the step in which wave 0 set res
   uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
   unsigned long long win[kLineWin];                // wave 0: a look-back window's descriptors, by LDS-DMA
+  unsigned long long win_base;                     // wave 0: the descriptor index of win[0]
+  uint32_t agg_next, res_next, lb_step;            // wave 0: steps with an AGG / resolved; the window's step
   unsigned long long win_dummy[kLineWin];          // every other wave's / step's window loads (never read)
 };
 
@@ -2525,27 +2558,31 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t r = sh.grp[0] * kMapWaves + (uint32_t)wave;
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
-  Buf b[kBufs];
+  BufN b[kBufs];
 #pragma unroll
-  for (int h = 0; h < kBufs; ++h) load_buf(b[h], A, g, 0, lane, h);
+  for (int h = 0; h < kBufs; ++h) load_buf_n(b[h], A, g, lane, h);
   if (DP_LINE_PRIO && wave == 0) set_prio(DP_LINE_PRIO);
   bool ovf = false;
+  uint32_t cur_it = 0;                               // the step the loop is in
   uint32_t nb = 0;                                   // (every wave) the next step to place
-  // (wave 0) steps with a published AGG / a resolved prefix; the step of the look-back in flight
-  uint32_t agg_next = 0, res_next = 0, lb_step = 0xFFFFFFFFu;
-  uint64_t lb_base = 0;
+  // (wave 0) steps with a published AGG / a resolved prefix, the step of the look-back window in flight and its
+  // first descriptor: kept in LDS, not in registers (every wave would carry them; SGPRs are at their limit)
+  if (threadIdx.x == 0) {
+    sh.agg_next = 0;
+    sh.res_next = 0;
+    sh.lb_step = 0xFFFFFFFFu;
+    sh.win_base = 0;
+  }
 
   // phase B of step q for this wave's range
-  // ``light``: only a range kept in LDS (false for a dense one, which waits for the full path: its rescan needs
-  // the registers that the input buffers in flight hold at the light call site)
-  auto place = [&](uint32_t q, bool light) -> bool {
+  // ``list``: also copy the range's LDS list to the output (false: the group run does; see place_group)
+  auto place = [&](uint32_t q, bool list) -> bool {
     const uint32_t s = q % kLineSlots;
     // every LDS read up front (one round trip: the branches below would otherwise serialize them)
     const uint4 gq = sh.geo[s][wave];
     const uint32_t cw = sh.cnt[s][wave];
     const uint64_t Pw = sh.pw[s][wave];
     if (!(gq.z & kLineValid)) return true;
-    if (light && (cw & kLineDense)) return false;
     const uint32_t n = cw & ~kLineDense;
     const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
     const uint32_t lo_w = gq.z & 15u, hi_w = gq.z >> 16;
@@ -2567,10 +2604,70 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
       return true;
     }
+    if (!list) return true;
     const uint16_t* evw = sh.ev[s][wave];
     // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
     ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
     return true;
+  };
+  // (every thread of the workgroup) step q's uint16 index as ONE contiguous run [P_g, P_g + total) (the
+  // best-measured store shape, stream_rw_kernel): thread t stores group entries h + 8t .. h + 8t + 7 as one
+  // aligned 16-byte store, gathering each entry from the LDS list of the range holding it (the largest w with
+  // ex[w] <= e); ranges too dense for LDS are rescanned by their own wave (dense_b) and left out of the run.
+  // Every delimiter an entry (out_mode 3 implies every_k == 1) and the output 16-byte aligned (both checked by the
+  // host); entries at or past the capacity are not stored (the launch then reports DP_ERR_CAPACITY).
+  auto place_group = [&](uint32_t q) {
+    const uint32_t s = q % kLineSlots;
+    const uint32_t Tg = (uint32_t)sh.tot[s];
+    const uint64_t Pg = sh.pw[s][0];                   // (ex[0] == 0)
+    place(q, false);                                   // this wave's range: its bookkeeping, or its rescan
+#ifdef DP_LINE_NOPLACE
+    return;
+#endif
+    if (Pg >= A.cap) return;
+    const uint32_t T = A.cap - Pg < (uint64_t)Tg ? (uint32_t)(A.cap - Pg) : Tg;
+    uint16_t* o = reinterpret_cast<uint16_t*>(A.out) + Pg;
+    const uint32_t* ex = sh.ex[s];
+    auto find = [&](uint32_t e) {
+      uint32_t w = 0;
+#pragma unroll
+      for (uint32_t st = kMapWaves / 2; st; st >>= 1)
+        if (ex[w + st] <= e) w += st;
+      return w;
+    };
+    auto dense = [&](uint32_t w) { return (sh.cnt[s][w] & kLineDense) != 0u; };
+    auto value = [&](uint32_t e, uint32_t w) { return (uint16_t)(sh.b16[s][w] + sh.ev[s][w][e - ex[w]]); };
+    auto one = [&](uint32_t e) {
+      const uint32_t w = find(e);
+      if (!dense(w)) o[e] = value(e, w);
+    };
+    const uint32_t t = threadIdx.x;
+    const uint32_t hh = (uint32_t)((8u - (uint32_t)(Pg & 7u)) & 7u);
+    const uint32_t h = hh < T ? hh : T;
+    if (t < h) one(t);
+    const uint32_t G8 = (T - h) >> 3;
+    for (uint32_t jg = t; jg < G8; jg += kWave * kMapWaves) {
+      const uint32_t e0 = h + 8u * jg;
+      const uint32_t w0 = find(e0);
+      if (w0 == find(e0 + 7u) && !dense(w0)) {        // the common case: one range's 8 consecutive positions
+        const uint16_t* ev = sh.ev[s][w0] + (e0 - ex[w0]);
+        const uint32_t b = sh.b16[s][w0];
+        uint32_t wd[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          wd[i] = (uint32_t)(uint16_t)(b + ev[2 * i]) | ((uint32_t)(uint16_t)(b + ev[2 * i + 1]) << 16);
+        const v4u pk = {wd[0], wd[1], wd[2], wd[3]};
+#if DP_NTSTORE
+        __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + e0));
+#else
+        *reinterpret_cast<v4u*>(o + e0) = pk;
+#endif
+      } else {
+        for (uint32_t i = 0; i < 8u; ++i) one(e0 + i);
+      }
+    }
+    const uint32_t tail0 = h + 8u * G8;
+    if (t < T - tail0) one(tail0 + t);
   };
   // (wave 0) step q's AGG: the group's count from the 16 ranges (lanes 0..15), their exclusive prefixes
   auto publish_agg = [&](uint32_t q) {
@@ -2587,7 +2684,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       sh.tot[s] = total;
       st_desc(&A.desc[sh.grp[q % kLineGrpQ]], pack_count(kStatAgg, total) | A.epoch);
     }
-    agg_next = q + 1;
+    sh.agg_next = q + 1;
   };
   // (wave 0) a resolved prefix: LDS tag for the other waves, PREFIX descriptor for the other workgroups
   auto resolved = [&](uint32_t q, uint64_t P) {
@@ -2596,32 +2693,33 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     if (lane < (int)kMapWaves) sh.pw[s][lane] = P + sh.ex[s][lane];   // every range's launch prefix
     cbar();
     if (lane == 0) {
+      sh.rstep[s] = cur_it;
       lds_st(&sh.res[s], u + 1u);
       st_desc(&A.desc[u], pack_count(kStatPrefix, P + sh.tot[s]) | A.epoch);
     }
-    res_next = q + 1;
+    sh.res_next = q + 1;
   };
   // (wave 0) resolve every step up to q in the foreground (compiler-waited look-back loads)
   auto resolve_upto = [&](uint32_t q) {
-    if (lb_step != 0xFFFFFFFFu) {                    // a hand-waited look-back in flight: let it land
+    if (sh.lb_step != 0xFFFFFFFFu) {                    // a hand-waited look-back in flight: let it land
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lb_step = 0xFFFFFFFFu;
+      sh.lb_step = 0xFFFFFFFFu;
     }
     uint64_t t0 = 0;
     uint32_t spins = 0;
-    while (res_next <= q) {
-      const uint32_t u = sh.grp[res_next % kLineGrpQ];
+    while (sh.res_next <= q) {
+      const uint32_t u = sh.grp[sh.res_next % kLineGrpQ];
       const uint32_t W = u < kLbSlots ? u : kLbSlots;
       uint64_t d[kLbPer];
       lb_load(A, u, W, lane, d);
       uint64_t P = 0;
       if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P)) {
-        resolved(res_next, P);
+        resolved(sh.res_next, P);
         continue;
       }
       if (wait_expired(spins++, t0)) {               // give up: flag it and release the waiting waves
         if (lane == 0) atomicOr(A.err, kErrTimeout);
-        resolved(res_next, 0ull);
+        resolved(sh.res_next, 0ull);
         continue;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -2644,7 +2742,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         }
         cbar();
       }
-      place(nb, false);
+      place(nb, true);
     }
   };
 
@@ -2656,6 +2754,15 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t it = 0;
   for (;; ++it) {
     __syncthreads();
+    cur_it = it;
+    // the steps this workgroup places at the end of this step, decided here by every wave alike: resolved in an
+    // earlier step (the barrier above published them), in order, at most two
+    uint32_t nplace = 0;
+    for (uint32_t i = 0; i < 2u && nb + i < it; ++i) {
+      const uint32_t q = nb + i, s_ = q % kLineSlots;
+      if (sh.res[s_] != sh.grp[q % kLineGrpQ] + 1u || sh.rstep[s_] >= it) break;
+      ++nplace;
+    }
     const uint32_t gnext = sh.grp[(it + 1) % kLineGrpQ];
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
     const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD &&
@@ -2670,17 +2777,17 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kLineCap - 1u ? rk : kLineCap - 1u] = (uint16_t)pos; };
     v4u x[kRows];
     // ---- buffer 0
-    wait_buf(b[0]);                                   // the youngest operations in flight: b[1]'s loads
+    wait_buf_n(b[0]);                                 // the youngest operations in flight: b[1]'s loads
     if (do_claim) {
       claim_res = atomic_add_nowait(ticket, run);
       pend = run;
     }
     if (wave == 0) {
-      if (lb_step != 0xFFFFFFFFu) {                   // issued a step ago, older than b[1]'s loads: landed
-        const uint32_t q = lb_step, u = sh.grp[q % kLineGrpQ];
-        lb_step = 0xFFFFFFFFu;
+      if (sh.lb_step != 0xFFFFFFFFu) {                   // issued a step ago, older than b[1]'s loads: landed
+        const uint32_t q = sh.lb_step, u = sh.grp[q % kLineGrpQ];
+        sh.lb_step = 0xFFFFFFFFu;
         uint64_t d[kLbPer];
-        lb_window_read(sh.win, lb_base, u, lane, d);
+        lb_window_read(sh.win, sh.win_base, u, lane, d);
         uint64_t P = 0;
         if (lb_count_window(A, u, d, lane, P)) resolved(q, P);
       }
@@ -2691,23 +2798,23 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     for (int i = 0; i < kRows; ++i) x[i] = b[0].x[i];
     if (interior) delim_rows<true>(x, 0, lo, hi, key, lane, nev, keep);
     else delim_rows<false>(x, 0, lo, hi, key, lane, nev, keep);
-    load_buf(b[0], A, gn, 0, lane, 0);
+    load_buf_n(b[0], A, gn, lane, 0);
     // Every wave issues the window's kLineWinLoads LDS-DMA loads every step, so the wait below has one count on
     // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
     // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
     // (other waves, or no such group) land in the wave's own dummy area and are never read.
     {
-      const bool want = wave == 0 && res_next < agg_next;
-      const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
+      const bool want = wave == 0 && sh.res_next < sh.agg_next;
+      const uint32_t u = want ? sh.grp[sh.res_next % kLineGrpQ] : 0u;
       const uint64_t base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
       if (want) {
-        lb_base = base;
-        lb_step = res_next;
+        sh.win_base = base;
+        sh.lb_step = sh.res_next;
       }
     }
     // ---- buffer 1
-    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsPerBuf + kLineWinLoads) : "memory");   // b[0] + window in flight
-    touch_buf(b[1]);
+    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsPerBufN + kLineWinLoads) : "memory");   // b[0] + window in flight
+    touch_buf_n(b[1]);
     __builtin_amdgcn_sched_barrier(0);
     if (pend) {                                       // the wait above covered the claim: its value is back
       asm volatile("" : "+v"(claim_res) :: "memory");
@@ -2730,39 +2837,23 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
                                      ((g.fl & kGeoLast) ? kLineLast : 0u) | (r + 1u == nranges ? kLineEnd : 0u) |
                                      (g.hi_u << 16),
                                  g.c};
+      sh.b16[slot][wave] = (uint32_t)(A.obj_base - A.shift + g.ubase) & 0xFFFFu;
     }
     // the next step fills the slot of step it + 1 - kLineSlots: this wave must have placed it.  Blocking here
     // (only b[0]'s loads in flight, so the registers are free) holds back this workgroup's AGG of step it, its
     // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
-#if DP_LINE_EARLY
-    if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
-    // b[1]'s reload goes out before this step's placements, so both buffers' loads travel during them
-    load_buf(b[kBufs - 1], A, gn, 0, lane, kBufs - 1);
-    // place every older step whose prefix is known (wave-local order); a dense range waits for the full path
-    while (nb < it) {
-      const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
-      if (lds_ld(&sh.res[nb % kLineSlots]) != want) break;
-      cbar();
-      if (!place(nb, true)) break;
-      ++nb;
-    }
-#else
-    while (nb < it) {
-      const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
-      if (lds_ld(&sh.res[nb % kLineSlots]) != want) break;
-      cbar();
-      place(nb, false);
-      ++nb;
+    for (uint32_t i = 0; i < nplace; ++i, ++nb) {
+      if constexpr (OUT64 == 2 && DP_LINE_GROUP) place_group(nb);
+      else place(nb, true);
     }
     if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
-    load_buf(b[kBufs - 1], A, gn, 0, lane, kBufs - 1);
-#endif
+    load_buf_n(b[kBufs - 1], A, gn, lane, kBufs - 1);
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
   }
-  drain_bufs(b);                                      // (and a look-back window still in flight)
-  lb_step = 0xFFFFFFFFu;
+  drain_bufs_n(b);                                    // (and a look-back window still in flight)
+  if (wave == 0) sh.lb_step = 0xFFFFFFFFu;
   __syncthreads();                                    // every wave's last count is in LDS
   if (wave == 0) publish_agg(it);
   place_upto(it);
@@ -3813,6 +3904,7 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
     ntab = last > first ? ((last - 1) >> 16) - j0 + 1 : 1;
     tab = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(d_out) + ((2 * cap + 15) & ~15ull));
     if (!d_out) return fail(DP_ERR_INVALID, "out_mode 3 needs an output buffer (entries + block table)");
+    if (((uintptr_t)d_out) & 15u) return fail(DP_ERR_INVALID, "out_mode 3 needs a 16-byte aligned output buffer");
   }
   const uint64_t nr = rg.size() / 2;
   uint64_t units = 0, span = 0;

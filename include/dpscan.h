@@ -122,7 +122,7 @@ int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
  *       object offset (j0 + j) << 16, so entry i's full offset is ((j0 + j) << 16) + low word for the j
  *       with tab[j] <= i < tab[j + 1] (tab is non-decreasing).  When `first` is not a multiple of 64 KiB,
  *       tab[0] stands for a boundary below the first byte and is not written: read it as 0.
- *     - d_out must hold (2 * cap + 15) & ~15 + 8 * J bytes;
+ *     - d_out must be 16-byte aligned and hold (2 * cap + 15) & ~15 + 8 * J bytes;
  *     - ranges must be contiguous (range i + 1 starts where range i ends), and d_buf and buf_base must be
  *       congruent mod 16 (the kernel's 16-byte lanes then sit on object-aligned 64 KiB boundaries).
  *   range_end (host array of nranges, may be NULL): delimiters up to and including range i.
