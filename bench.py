@@ -733,9 +733,7 @@ def delim_worker(args, team, leg, k, world, dev):
     def collect(i):
         return ctxs[i % 2].delim_ranges_result(nr)
 
-    two_max = ctxs[0].forms()[1]
-    kernel = ("map_kernel<DELIM> + delim_place_kernel (one HIP-event span)" if nbytes <= two_max
-              else "scan_kernel<DELIM> (one-pass)")
+    kernel = ScanContext.DELIM_FORMS[ctxs[0].delim_form(nbytes)]
     S = Steps(team, ctxs, launch, collect)
     team.barrier()
     S.warm(args.warmup)
@@ -811,7 +809,9 @@ def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
         sample = obj.bytes_range(b0, min(b1, b0 + (1 << 30)))     # bounded sample: the first GiB scanned
         cpu = cpu_baseline_delim(sample)
         del sample
-    pmc_kernel = "scan_kernel<1" if "one-pass" in allres[0]["kernel"] else "map_kernel<1>,delim_place_kernel"
+    k = allres[0]["kernel"]
+    pmc_kernel = ("line_kernel<" if k.startswith("line_kernel") else "scan_kernel<1" if k.startswith("scan_kernel")
+                  else "map_kernel<1>,delim_place_kernel")
     traffic, traffic_src = (load_traffic(args, leg, allres[0]["scanned"], pmc_kernel, args.index_dtype)
                             if world == 1 else (None, None))
     name = "CSV" if csv_mode else "VCF"

@@ -2445,6 +2445,9 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_GROUP      // the uint16 index's placements as one contiguous run per group (0: one run per range)
 #define DP_LINE_GROUP 1
 #endif
+#ifndef DP_LINE_FASTA      // the FASTA form of line_kernel (DP_FASTA_FORM=line): not yet within the VGPR budget
+#define DP_LINE_FASTA 0    // (its build spills 16-20 B per lane, which the ISA guard refuses)
+#endif
 #ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
 #define DP_LINE_PRIO 0
 #endif
@@ -2478,6 +2481,12 @@ struct LineShared {
   unsigned long long win_base;                     // wave 0: the descriptor index of win[0]
   uint32_t agg_next, res_next, lb_step;            // wave 0: steps with an AGG / resolved; the window's step
   unsigned long long win_dummy[kLineWin];          // every other wave's / step's window loads (never read)
+  // FASTA: the range's record {cF | cT << 16, (first '\n' + 1) | events << 16, sF | sT << 1 | fV << 2, 0}, every
+  // range's exclusive prefix function {cF, cT, sF, sT} and true incoming state, the group's function
+  uint4 frec[kLineSlots][kMapWaves];
+  uint4 wex[kLineSlots][kMapWaves];
+  uint32_t sw[kLineSlots][kMapWaves];
+  uint4 gagg[kLineSlots];
 };
 
 struct LineArgs {
@@ -2532,12 +2541,36 @@ __device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, u
   return lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P);
 }
 
-template <int OUT64>
+// Buffers of the lockstep kernels (BufN: no lookahead dword in flight; FASTA reads it by a scalar load).
+__device__ __forceinline__ void load_bufx(BufN& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf_n(b, A, g, lane, h); }
+__device__ __forceinline__ void wait_bufx(BufN& b) { wait_buf_n(b); }
+__device__ __forceinline__ void touch_bufx(BufN& b) { touch_buf_n(b); }
+__device__ __forceinline__ void drain_bufsx(BufN (&b)[kBufs]) { drain_bufs_n(b); }
+typedef __attribute__((address_space(4))) const uint32_t cu32s;   // constant address space: s_load_dword
+
+// A window of FASTA group functions: the prefix count P and line state S entering group u, once resolvable.
+__device__ __forceinline__ bool lb_func_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P,
+                                               uint32_t& S) {
+  const uint32_t W = u < kLbSlots ? u : kLbSlots;
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+#pragma unroll
+  for (int j = 0; j < kLbPer; ++j) {
+    const uint32_t k = kLbPer * rl + j;
+    d[j] = k < W ? ((d[j] & kEpochMask) == A.epoch ? d[j] : 0ull) : kIdentDesc;
+  }
+  return lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S);
+}
+
+template <int MODE, int OUT64>
 __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, ScanArgs A,
                                                                  const uint64_t* __restrict__ tab_lo,
                                                                  const uint64_t* __restrict__ tab_hi,
                                                                  const uint64_t* __restrict__ tab_r0) {
   static_assert(kMapWaves == 16, "line_kernel: one workgroup of 16 waves per CU");
+  constexpr bool kFa = MODE == kFasta;
+  // no lookahead dword in flight for FASTA either (2 VGPRs): the byte after a buffer comes by a scalar load
+  typedef BufN BufT;
+  constexpr int kLoadsX = kLoadsPerBufN;
   __shared__ __attribute__((aligned(16))) LineShared sh;
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2558,9 +2591,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t r = sh.grp[0] * kMapWaves + (uint32_t)wave;
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
-  BufN b[kBufs];
+  BufT b[kBufs];
 #pragma unroll
-  for (int h = 0; h < kBufs; ++h) load_buf_n(b[h], A, g, lane, h);
+  for (int h = 0; h < kBufs; ++h) load_bufx(b[h], A, g, lane, h);
   if (DP_LINE_PRIO && wave == 0) set_prio(DP_LINE_PRIO);
   bool ovf = false;
   uint32_t cur_it = 0;                               // the step the loop is in
@@ -2587,28 +2620,66 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
     const uint32_t lo_w = gq.z & 15u, hi_w = gq.z >> 16;
     const uint64_t off0 = A.obj_base - A.shift + wbase;
-    if (lane == 0) {
-      if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
-      if (gq.z & kLineEnd) A.total[0] = Pw + n;
-      if constexpr (OUT64 == 2) {
-        // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
-        const uint64_t j = (off0 >> 16) - A.tab_j0;
-        if ((off0 & 0xFFFFull) == 0 && lo_w == 0 && hi_w != 0 && off0 >= (A.tab_j0 << 16) && j < A.tab_n)
-          A.blocktab[j] = Pw;
+    if constexpr (kFa) {
+      // the FASTA fix-up of phase_b / fasta_place_block with the range's true incoming state: drop a start
+      // pending from the previous range, prepend the end of the header pending into it; pairs at 2P - S + i
+      typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
+      const uint4 fr = sh.frec[s][wave];
+      const uint32_t S = sh.sw[s][wave];
+      const uint32_t cF = fr.x & 0xFFFFu, cT = fr.x >> 16, fn = fr.y & 0xFFFFu, fl = fr.z;
+      const uint32_t fV = (fl >> 2) & 1u;
+      if (lane == 0) {
+        const uint64_t P_incl = Pw + (S ? cT : cF);
+        const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
+        if (gq.z & kLineLast) {
+          A.chunk_end[gq.w] = P_incl;
+          A.pending[gq.w] = S_out ? (long long)P_incl - 1 : -1ll;
+        }
+        if (gq.z & kLineEnd) A.total[0] = P_incl;
       }
-    }
+      if (cw & kLineDense) {
+        dense_b<kFasta, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, S, lane);
+        return true;
+      }
+      const uint32_t skip = S & fV;
+      const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
+      const uint32_t m = n - skip + pre;
+      const uint64_t b0 = 2 * Pw - S, last = 2 * A.cap - 1;
+      const bool near4g = OUT64 == 0 && off0 + kWaveBytes + 1 > 0xFFFFFFFFull;
+      const uint16_t* evw = sh.ev[s][wave];
+      for (uint32_t i = (uint32_t)lane; i < m; i += kWave) {
+        const uint32_t e = (pre && i == 0) ? fn - 1u : (uint32_t)evw[i + skip - pre];
+        const uint64_t slot = b0 + i;
+        const uint64_t val = off0 + e + (slot & 1u);
+        if (near4g) ovf |= val > 0xFFFFFFFFull;
+        put<OutT>(A.out, slot < last ? slot : last, val);
+      }
+      (void)list;
+      return true;
+    } else {
+      if (lane == 0) {
+        if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
+        if (gq.z & kLineEnd) A.total[0] = Pw + n;
+        if constexpr (OUT64 == 2) {
+          // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
+          const uint64_t j = (off0 >> 16) - A.tab_j0;
+          if ((off0 & 0xFFFFull) == 0 && lo_w == 0 && hi_w != 0 && off0 >= (A.tab_j0 << 16) && j < A.tab_n)
+            A.blocktab[j] = Pw;
+        }
+      }
 #ifdef DP_LINE_NOPLACE
-    return true;    // timing probe only (wrong results): every step's bookkeeping without the index stores
+      return true;    // timing probe only (wrong results): every step's bookkeeping without the index stores
 #endif
-    if (cw & kLineDense) {
-      dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
+      if (cw & kLineDense) {
+        dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
+        return true;
+      }
+      if (!list) return true;
+      const uint16_t* evw = sh.ev[s][wave];
+      // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
+      ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
       return true;
     }
-    if (!list) return true;
-    const uint16_t* evw = sh.ev[s][wave];
-    // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
-    ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
-    return true;
   };
   // (every thread of the workgroup) step q's uint16 index as ONE contiguous run [P_g, P_g + total) (the
   // best-measured store shape, stream_rw_kernel): thread t stores group entries h + 8t .. h + 8t + 7 as one
@@ -2651,11 +2722,11 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       const uint32_t w0 = find(e0);
       if (w0 == find(e0 + 7u) && !dense(w0)) {        // the common case: one range's 8 consecutive positions
         const uint16_t* ev = sh.ev[s][w0] + (e0 - ex[w0]);
-        const uint32_t b = sh.b16[s][w0];
+        const uint32_t bb = sh.b16[s][w0];
         uint32_t wd[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          wd[i] = (uint32_t)(uint16_t)(b + ev[2 * i]) | ((uint32_t)(uint16_t)(b + ev[2 * i + 1]) << 16);
+          wd[i] = (uint32_t)(uint16_t)(bb + ev[2 * i]) | ((uint32_t)(uint16_t)(bb + ev[2 * i + 1]) << 16);
         const v4u pk = {wd[0], wd[1], wd[2], wd[3]};
 #if DP_NTSTORE
         __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + e0));
@@ -2669,35 +2740,77 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     const uint32_t tail0 = h + 8u * G8;
     if (t < T - tail0) one(tail0 + t);
   };
-  // (wave 0) step q's AGG: the group's count from the 16 ranges (lanes 0..15), their exclusive prefixes
+  // (wave 0) step q's AGG: the group's count (DELIM) or function of the incoming line state (FASTA) from its 16
+  // ranges (lanes 0..15), with every range's exclusive prefix
   auto publish_agg = [&](uint32_t q) {
     const uint32_t s = q % kLineSlots;
-    const uint32_t c = lane < (int)kMapWaves ? (sh.cnt[s][lane] & ~kLineDense) : 0u;
-    uint32_t inc = c;
-    inc += dpp32<kRowShr1, 0xF>(inc, 0u);
-    inc += dpp32<kRowShr2, 0xF>(inc, 0u);
-    inc += dpp32<kRowShr4, 0xF>(inc, 0u);
-    inc += dpp32<kRowShr8, 0xF>(inc, 0u);
-    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kMapWaves - 1);
-    if (lane < (int)kMapWaves) sh.ex[s][lane] = inc - c;
-    if (lane == 0) {
-      sh.tot[s] = total;
-      st_desc(&A.desc[sh.grp[q % kLineGrpQ]], pack_count(kStatAgg, total) | A.epoch);
+    uint64_t agg;
+    if constexpr (kFa) {
+      Func32 w = Func32{0, 0, 0, 1};                   // identity (a range past the end)
+      if (lane < (int)kMapWaves && (sh.geo[s][lane].z & kLineValid)) {
+        const uint4 fr = sh.frec[s][lane];
+        w = Func32{fr.x & 0xFFFFu, fr.x >> 16, fr.z & 1u, (fr.z >> 1) & 1u};
+      }
+      Func32 wi = w;
+      wi = f32_then(f32_dpp<kRowShr1, 0xF>(wi), wi);
+      wi = f32_then(f32_dpp<kRowShr2, 0xF>(wi), wi);
+      wi = f32_then(f32_dpp<kRowShr4, 0xF>(wi), wi);
+      wi = f32_then(f32_dpp<kRowShr8, 0xF>(wi), wi);
+      const Func32 we = f32_dpp<kRowShr1, 0xF>(wi);
+      if (lane < (int)kMapWaves) sh.wex[s][lane] = uint4{we.cF, we.cT, we.sF & 1u, we.sT & 1u};
+      const Func fa{(uint32_t)__builtin_amdgcn_readlane((int)wi.cF, kMapWaves - 1),
+                    (uint32_t)__builtin_amdgcn_readlane((int)wi.cT, kMapWaves - 1),
+                    (uint32_t)__builtin_amdgcn_readlane((int)wi.sF, kMapWaves - 1) & 1u,
+                    (uint32_t)__builtin_amdgcn_readlane((int)wi.sT, kMapWaves - 1) & 1u};
+      if (lane == 0) sh.gagg[s] = uint4{(uint32_t)fa.cF, (uint32_t)fa.cT, fa.sF, fa.sT};
+      agg = pack_agg(fa);
+    } else {
+      const uint32_t c = lane < (int)kMapWaves ? (sh.cnt[s][lane] & ~kLineDense) : 0u;
+      uint32_t inc = c;
+      inc += dpp32<kRowShr1, 0xF>(inc, 0u);
+      inc += dpp32<kRowShr2, 0xF>(inc, 0u);
+      inc += dpp32<kRowShr4, 0xF>(inc, 0u);
+      inc += dpp32<kRowShr8, 0xF>(inc, 0u);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kMapWaves - 1);
+      if (lane < (int)kMapWaves) sh.ex[s][lane] = inc - c;
+      if (lane == 0) sh.tot[s] = total;
+      agg = pack_count(kStatAgg, total);
     }
+    if (lane == 0) st_desc(&A.desc[sh.grp[q % kLineGrpQ]], agg | A.epoch);
     sh.agg_next = q + 1;
   };
-  // (wave 0) a resolved prefix: LDS tag for the other waves, PREFIX descriptor for the other workgroups
-  auto resolved = [&](uint32_t q, uint64_t P) {
+  // (wave 0) a resolved prefix P (and FASTA's incoming line state S): every range's prefix in LDS, the slot's
+  // tag for the other waves, the PREFIX descriptor for the other workgroups
+  auto resolved = [&](uint32_t q, uint64_t P, uint32_t S) {
     const uint32_t s = q % kLineSlots;
     const uint32_t u = sh.grp[q % kLineGrpQ];
-    if (lane < (int)kMapWaves) sh.pw[s][lane] = P + sh.ex[s][lane];   // every range's launch prefix
+    uint64_t pref;
+    if constexpr (kFa) {
+      if (lane < (int)kMapWaves) {
+        const uint4 wx = sh.wex[s][lane];
+        sh.pw[s][lane] = P + (S ? wx.y : wx.x);
+        const uint32_t sw = S ? wx.w : wx.z;
+        sh.sw[s][lane] = (sh.geo[s][lane].z & kLineFirst) ? 0u : sw;   // a chunk's first range starts afresh
+      }
+      const uint4 ga = sh.gagg[s];
+      pref = pack_prefix(P + (S ? ga.y : ga.x), S ? ga.w : ga.z);
+    } else {
+      (void)S;
+      if (lane < (int)kMapWaves) sh.pw[s][lane] = P + sh.ex[s][lane];   // every range's launch prefix
+      pref = pack_count(kStatPrefix, P + sh.tot[s]);
+    }
     cbar();
     if (lane == 0) {
       sh.rstep[s] = cur_it;
       lds_st(&sh.res[s], u + 1u);
-      st_desc(&A.desc[u], pack_count(kStatPrefix, P + sh.tot[s]) | A.epoch);
+      st_desc(&A.desc[u], pref | A.epoch);
     }
     sh.res_next = q + 1;
+  };
+  auto reduce = [&](uint32_t u, uint64_t (&d)[kLbPer], uint64_t& P, uint32_t& S) -> bool {
+    if constexpr (kFa) return lb_func_window(A, u, d, lane, P, S);
+    S = 0;
+    return lb_count_window(A, u, d, lane, P);
   };
   // (wave 0) resolve every step up to q in the foreground (compiler-waited look-back loads)
   auto resolve_upto = [&](uint32_t q) {
@@ -2711,15 +2824,21 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       const uint32_t u = sh.grp[sh.res_next % kLineGrpQ];
       const uint32_t W = u < kLbSlots ? u : kLbSlots;
       uint64_t d[kLbPer];
-      lb_load(A, u, W, lane, d);
+      const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+#pragma unroll
+      for (int j = 0; j < kLbPer; ++j) {
+        const uint32_t k = kLbPer * rl + j;
+        d[j] = ld_desc(&A.desc[k < W ? u - 1 - k : 0u]);
+      }
       uint64_t P = 0;
-      if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P)) {
-        resolved(sh.res_next, P);
+      uint32_t S = 0;
+      if (reduce(u, d, P, S)) {
+        resolved(sh.res_next, P, S);
         continue;
       }
       if (wait_expired(spins++, t0)) {               // give up: flag it and release the waiting waves
         if (lane == 0) atomicOr(A.err, kErrTimeout);
-        resolved(sh.res_next, 0ull);
+        resolved(sh.res_next, 0ull, 0u);
         continue;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -2770,14 +2889,31 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     if (do_claim) run = sh.grp[(claimed - 1) % kLineGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
     const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
     const uint32_t slot = it % kLineSlots;
-    uint32_t nev = 0;
+    FState st{0u, 0u, 0u, -1, 0u, 0u};               // DELIM: st.nev only
     const int lo = (int)g.lo_u, hi = (int)g.hi_u;
     const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
     uint16_t* evw = sh.ev[slot][wave];
     auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kLineCap - 1u ? rk : kLineCap - 1u] = (uint16_t)pos; };
     v4u x[kRows];
+    auto rows = [&](int h) {
+#pragma unroll
+      for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
+      if constexpr (kFa) {
+        // the first dword after this buffer (a scalar load through the constant address space: it waits on
+        // lgkmcnt, never on the hand-counted vmcnt); read only where that byte lies inside the chunk, the
+        // range's own first dword elsewhere (always in the buffer)
+        const bool inb = interior || (h + 1) * kBufBytes < hi;
+        const uint64_t la_at = g.ubase + (inb ? (uint64_t)(h + 1) * kBufBytes : 0ull);
+        const uint32_t la = *(cu32s*)(uintptr_t)(A.base + la_at);
+        if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
+        else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
+      } else {
+        if (interior) delim_rows<true>(x, h, lo, hi, key, lane, st.nev, keep);
+        else delim_rows<false>(x, h, lo, hi, key, lane, st.nev, keep);
+      }
+    };
     // ---- buffer 0
-    wait_buf_n(b[0]);                                 // the youngest operations in flight: b[1]'s loads
+    wait_bufx(b[0]);                                  // the youngest operations in flight: b[1]'s loads
     if (do_claim) {
       claim_res = atomic_add_nowait(ticket, run);
       pend = run;
@@ -2789,20 +2925,18 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         uint64_t d[kLbPer];
         lb_window_read(sh.win, sh.win_base, u, lane, d);
         uint64_t P = 0;
-        if (lb_count_window(A, u, d, lane, P)) resolved(q, P);
+        uint32_t S = 0;
+        if (reduce(u, d, P, S)) resolved(q, P, S);
       }
-      // every wave wrote step it - 1's count before the barrier: its AGG goes out before anything blocks
+      // every wave wrote step it - 1's summary before the barrier: its AGG goes out before anything blocks
       if (it > 0) publish_agg(it - 1);
     }
-#pragma unroll
-    for (int i = 0; i < kRows; ++i) x[i] = b[0].x[i];
-    if (interior) delim_rows<true>(x, 0, lo, hi, key, lane, nev, keep);
-    else delim_rows<false>(x, 0, lo, hi, key, lane, nev, keep);
-    load_buf_n(b[0], A, gn, lane, 0);
+    rows(0);
+    load_bufx(b[0], A, gn, lane, 0);
     // Every wave issues the window's kLineWinLoads LDS-DMA loads every step, so the wait below has one count on
     // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
     // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
-    // (other waves, or no such group) land in the wave's own dummy area and are never read.
+    // (other waves, or no such group) land in a dummy area and are never read.
     {
       const bool want = wave == 0 && sh.res_next < sh.agg_next;
       const uint32_t u = want ? sh.grp[sh.res_next % kLineGrpQ] : 0u;
@@ -2813,8 +2947,8 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       }
     }
     // ---- buffer 1
-    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsPerBufN + kLineWinLoads) : "memory");   // b[0] + window in flight
-    touch_buf_n(b[1]);
+    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsX + kLineWinLoads) : "memory");   // b[0] + window in flight
+    touch_bufx(b[1]);
     __builtin_amdgcn_sched_barrier(0);
     if (pend) {                                       // the wait above covered the claim: its value is back
       asm volatile("" : "+v"(claim_res) :: "memory");
@@ -2824,37 +2958,44 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       claimed += pend;
       pend = 0;
     }
-#pragma unroll
-    for (int i = 0; i < kRows; ++i) x[i] = b[1].x[i];
-    if (interior) delim_rows<true>(x, 1, lo, hi, key, lane, nev, keep);
-    else delim_rows<false>(x, 1, lo, hi, key, lane, nev, keep);
+    rows(1);
     cbar();
     if (lane == 0) {
       const bool valid = (g.fl & kGeoValid) != 0u;
-      sh.cnt[slot][wave] = valid ? (nev | (nev > kLineCap ? kLineDense : 0u)) : 0u;
+      sh.cnt[slot][wave] = valid ? (st.nev | (st.nev > kLineCap ? kLineDense : 0u)) : 0u;
       sh.geo[slot][wave] = uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32),
                                  g.lo_u | (valid ? kLineValid : 0u) | ((g.fl & kGeoFirst) ? kLineFirst : 0u) |
                                      ((g.fl & kGeoLast) ? kLineLast : 0u) | (r + 1u == nranges ? kLineEnd : 0u) |
                                      (g.hi_u << 16),
                                  g.c};
-      sh.b16[slot][wave] = (uint32_t)(A.obj_base - A.shift + g.ubase) & 0xFFFFu;
+      if constexpr (kFa) {
+        // the range's function of its incoming line state (phase_a_rec / map_kernel's record)
+        if (!st.nlseen) st.fV = st.S;
+        uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
+        if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }   // chunk start: the incoming state is reset
+        sh.frec[slot][wave] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16),
+                                    st.S | (sT << 1) | (st.fV << 2), 0u};
+      } else {
+        sh.b16[slot][wave] = (uint32_t)(A.obj_base - A.shift + g.ubase) & 0xFFFFu;
+      }
     }
-    // the next step fills the slot of step it + 1 - kLineSlots: this wave must have placed it.  Blocking here
-    // (only b[0]'s loads in flight, so the registers are free) holds back this workgroup's AGG of step it, its
-    // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+    // this step's placements (decided at its start); then, if the next step's slot still holds an unplaced
+    // step, block for it here (only b[0]'s loads in flight, so the registers are free).  Blocking holds back
+    // this workgroup's AGG of step it, its newest group, while it waits for an older one: the lowest waiting
+    // group never depends on a held AGG.
     for (uint32_t i = 0; i < nplace; ++i, ++nb) {
-      if constexpr (OUT64 == 2 && DP_LINE_GROUP) place_group(nb);
+      if constexpr (!kFa && OUT64 == 2 && DP_LINE_GROUP) place_group(nb);
       else place(nb, true);
     }
     if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
-    load_buf_n(b[kBufs - 1], A, gn, lane, kBufs - 1);
+    load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
   }
-  drain_bufs_n(b);                                    // (and a look-back window still in flight)
+  drain_bufsx(b);                                     // (and a look-back window still in flight)
   if (wave == 0) sh.lb_step = 0xFFFFFFFFu;
-  __syncthreads();                                    // every wave's last count is in LDS
+  __syncthreads();                                    // every wave's last summary is in LDS
   if (wave == 0) publish_agg(it);
   place_upto(it);
   if (ovf) atomicOr(A.err, kErrOverflow);
@@ -3090,6 +3231,7 @@ struct dp_ctx {
   uint16_t* d_spill = nullptr;
   uint64_t rec_cap = 0;               // ranges
   bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
+  int fasta_form = 0;                 // 0: map + placement kernels, 1: line_kernel (DP_FASTA_FORM = line | two)
   uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
   int delim_form = 0;                 // newline kernels: 0 auto (by size), 1 line_kernel, 2 two kernels, 3 one-pass
   uint32_t line_launches = 0;         // line_kernel launches (ticket parity)
@@ -3522,8 +3664,9 @@ int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   return scan_leave(c, ss);
 }
 
-// The lockstep one-pass newline index (line_kernel), over the same 16 KiB-range staging as launch_delim2.
-int launch_line(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
+// The lockstep one-pass kernel (line_kernel) of either index, over the same 16 KiB-range staging as launch_delim2:
+// the newline index (mode kDelim, kind = out_mode's element form) or the FASTA pairs (kFasta, kind = out_u64).
+int launch_line(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
                 int kind, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
                 uint32_t wrap32, unsigned long long* blocktab, uint64_t tab_j0, uint64_t tab_n) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
@@ -3546,7 +3689,7 @@ int launch_line(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, 
   a.desc = c->d_desc;
   a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
   if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
-    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
+    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B: one uint64 pair)
     cap = 1;
   }
   a.out = d_out;
@@ -3584,12 +3727,21 @@ int launch_line(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, 
   hipEvent_t e0;
   rc = ev_begin(c, &e0, ss);
   if (rc) return rc;
-  if (kind == 1)
-    hipLaunchKernelGGL((line_kernel<1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
-  else if (kind == 2)
-    hipLaunchKernelGGL((line_kernel<2>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+#if DP_LINE_FASTA
+  if (mode == kFasta && kind)
+    hipLaunchKernelGGL((line_kernel<kFasta, 1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  else if (mode == kFasta)
+    hipLaunchKernelGGL((line_kernel<kFasta, 0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
   else
-    hipLaunchKernelGGL((line_kernel<0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+#else
+  if (mode == kFasta) return fail(DP_ERR_INVALID, "the FASTA line_kernel is not built (DP_LINE_FASTA=0)");
+#endif
+  if (kind == 1)
+    hipLaunchKernelGGL((line_kernel<kDelim, 1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  else if (kind == 2)
+    hipLaunchKernelGGL((line_kernel<kDelim, 2>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  else
+    hipLaunchKernelGGL((line_kernel<kDelim, 0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   rc = ev_end(c, ss);
   if (rc) return rc;
@@ -3666,6 +3818,8 @@ int dp_ctx_create(int device, dp_ctx** out) {
   if (c->grid > 256) c->grid = 256;   // one look-back window (G <= 256) per unit
   const char* onepass = getenv("DP_FASTA_ONEPASS");
   c->fasta_onepass = onepass && atoi(onepass) != 0;
+  const char* fform = getenv("DP_FASTA_FORM");
+  c->fasta_form = fform && !strcmp(fform, "line") ? 1 : 0;
   // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
   const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
   c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
@@ -3784,6 +3938,11 @@ int dp_fasta_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint
     rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units);
     if (rc) return rc;
     rc = launch_scan(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0);
+  } else if (c->fasta_form == 1) {                   // the lockstep one-pass kernel
+    rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units, kWaveBytes);
+    if (rc) return rc;
+    rc = launch_line(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0, 0, 0, nullptr,
+                     0, 0);
   } else {
     rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units, kWaveBytes);
     if (rc) return rc;
@@ -3913,7 +4072,7 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   if (c->delim_form == 1) {                           // the lockstep one-pass kernel
     rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
     if (rc) return rc;
-    rc = launch_line(c, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
+    rc = launch_line(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
                      out_mode == 2, tab, j0, ntab);
   } else if (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) {   // two kernels
     rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
@@ -4089,6 +4248,12 @@ int dp_scan_forms(dp_ctx* c, int* fasta_two_kernel, uint64_t* delim_two_kernel_m
   if (!c) return fail(DP_ERR_INVALID, "null");
   if (fasta_two_kernel) *fasta_two_kernel = c->fasta_onepass ? 0 : 1;
   if (delim_two_kernel_max) *delim_two_kernel_max = c->delim_twopass_max;
+  return DP_OK;
+}
+
+int dp_scan_delim_form(dp_ctx* c, uint64_t span, int* form) {
+  if (!c || !form) return fail(DP_ERR_INVALID, "null");
+  *form = c->delim_form == 1 ? 1 : (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) ? 2 : 3;
   return DP_OK;
 }
 

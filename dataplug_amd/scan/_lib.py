@@ -66,6 +66,7 @@ SIGNATURES = [
     ("dp_debug_profile", _c.c_int, [_p, _u64p, _u64, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
     ("dp_alloc_counts", _c.c_int, [_u64p, _u64p]),
     ("dp_scan_forms", _c.c_int, [_p, _c.POINTER(_c.c_int), _u64p]),
+    ("dp_scan_delim_form", _c.c_int, [_p, _u64, _c.POINTER(_c.c_int)]),
     ("dp_scan_geometry", _c.c_int, [_p, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
 ]
 

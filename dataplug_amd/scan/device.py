@@ -339,6 +339,16 @@ class ScanContext:
         check(self.lib.dp_scan_forms(self.handle, ctypes.byref(f), ctypes.byref(d)))
         return int(f.value), int(d.value)
 
+    DELIM_FORMS = {1: "line_kernel<DELIM> (lockstep one pass)",
+                   2: "map_kernel<DELIM> + delim_place_kernel (one HIP-event span)",
+                   3: "scan_kernel<DELIM> (one-pass look-back)"}
+
+    def delim_form(self, span: int) -> int:
+        """The kernels a newline launch of ``span`` bytes takes (dp_scan_delim_form: 1 line, 2 two, 3 one-pass)."""
+        f = ctypes.c_int(0)
+        check(self.lib.dp_scan_delim_form(self.handle, int(span), ctypes.byref(f)))
+        return int(f.value)
+
     def geometry(self) -> Tuple[int, int]:
         g = ctypes.c_int(0)
         u = ctypes.c_int(0)
