@@ -2442,9 +2442,9 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_CAP
 #define DP_LINE_CAP 640
 #endif
-#ifndef DP_LINE_GROUP      // the uint16 index's placements as one contiguous run per group (0: one run per range)
-#define DP_LINE_GROUP 1
-#endif
+#ifndef DP_LINE_GROUP      // the uint16 index's placements as one contiguous run per group (0, default: one run per
+#define DP_LINE_GROUP 0    // range; 1 measured no faster: 951-957 vs 951 us per 4 GiB CSV, and it needs the VGPRs
+#endif                     // that keep wave 0's bookkeeping in registers)
 #ifndef DP_LINE_FASTA      // the FASTA form of line_kernel (DP_FASTA_FORM=line): not yet within the VGPR budget
 #define DP_LINE_FASTA 0    // (its build spills 16-20 B per lane, which the ISA guard refuses)
 #endif
@@ -2478,8 +2478,6 @@ struct LineShared {
   uint32_t rstep[kLineSlots];                      // the step in which wave 0 set res
   uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
   unsigned long long win[kLineWin];                // wave 0: a look-back window's descriptors, by LDS-DMA
-  unsigned long long win_base;                     // wave 0: the descriptor index of win[0]
-  uint32_t agg_next, res_next, lb_step;            // wave 0: steps with an AGG / resolved; the window's step
   unsigned long long win_dummy[kLineWin];          // every other wave's / step's window loads (never read)
   // FASTA: the range's record {cF | cT << 16, (first '\n' + 1) | events << 16, sF | sT << 1 | fV << 2, 0}, every
   // range's exclusive prefix function {cF, cT, sF, sT} and true incoming state, the group's function
@@ -2599,13 +2597,10 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t cur_it = 0;                               // the step the loop is in
   uint32_t nb = 0;                                   // (every wave) the next step to place
   // (wave 0) steps with a published AGG / a resolved prefix, the step of the look-back window in flight and its
-  // first descriptor: kept in LDS, not in registers (every wave would carry them; SGPRs are at their limit)
-  if (threadIdx.x == 0) {
-    sh.agg_next = 0;
-    sh.res_next = 0;
-    sh.lb_step = 0xFFFFFFFFu;
-    sh.win_base = 0;
-  }
+  // first descriptor (in registers: kept in LDS they cost wave 0 ~10 dependent LDS round trips per step, and the
+  // barrier made every wave wait for them: 956 vs 849 us per 4 GiB CSV)
+  uint32_t agg_next = 0, res_next = 0, lb_step = 0xFFFFFFFFu;
+  uint64_t win_base = 0;
 
   // phase B of step q for this wave's range
   // ``list``: also copy the range's LDS list to the output (false: the group run does; see place_group)
@@ -2777,7 +2772,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       agg = pack_count(kStatAgg, total);
     }
     if (lane == 0) st_desc(&A.desc[sh.grp[q % kLineGrpQ]], agg | A.epoch);
-    sh.agg_next = q + 1;
+    agg_next = q + 1;
   };
   // (wave 0) a resolved prefix P (and FASTA's incoming line state S): every range's prefix in LDS, the slot's
   // tag for the other waves, the PREFIX descriptor for the other workgroups
@@ -2805,7 +2800,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       lds_st(&sh.res[s], u + 1u);
       st_desc(&A.desc[u], pref | A.epoch);
     }
-    sh.res_next = q + 1;
+    res_next = q + 1;
   };
   auto reduce = [&](uint32_t u, uint64_t (&d)[kLbPer], uint64_t& P, uint32_t& S) -> bool {
     if constexpr (kFa) return lb_func_window(A, u, d, lane, P, S);
@@ -2814,14 +2809,14 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   };
   // (wave 0) resolve every step up to q in the foreground (compiler-waited look-back loads)
   auto resolve_upto = [&](uint32_t q) {
-    if (sh.lb_step != 0xFFFFFFFFu) {                    // a hand-waited look-back in flight: let it land
+    if (lb_step != 0xFFFFFFFFu) {                    // a hand-waited look-back in flight: let it land
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sh.lb_step = 0xFFFFFFFFu;
+      lb_step = 0xFFFFFFFFu;
     }
     uint64_t t0 = 0;
     uint32_t spins = 0;
-    while (sh.res_next <= q) {
-      const uint32_t u = sh.grp[sh.res_next % kLineGrpQ];
+    while (res_next <= q) {
+      const uint32_t u = sh.grp[res_next % kLineGrpQ];
       const uint32_t W = u < kLbSlots ? u : kLbSlots;
       uint64_t d[kLbPer];
       const uint32_t rl = (uint32_t)(kWave - 1 - lane);
@@ -2833,12 +2828,12 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       uint64_t P = 0;
       uint32_t S = 0;
       if (reduce(u, d, P, S)) {
-        resolved(sh.res_next, P, S);
+        resolved(res_next, P, S);
         continue;
       }
       if (wait_expired(spins++, t0)) {               // give up: flag it and release the waiting waves
         if (lane == 0) atomicOr(A.err, kErrTimeout);
-        resolved(sh.res_next, 0ull, 0u);
+        resolved(res_next, 0ull, 0u);
         continue;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -2919,11 +2914,11 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       pend = run;
     }
     if (wave == 0) {
-      if (sh.lb_step != 0xFFFFFFFFu) {                   // issued a step ago, older than b[1]'s loads: landed
-        const uint32_t q = sh.lb_step, u = sh.grp[q % kLineGrpQ];
-        sh.lb_step = 0xFFFFFFFFu;
+      if (lb_step != 0xFFFFFFFFu) {                   // issued a step ago, older than b[1]'s loads: landed
+        const uint32_t q = lb_step, u = sh.grp[q % kLineGrpQ];
+        lb_step = 0xFFFFFFFFu;
         uint64_t d[kLbPer];
-        lb_window_read(sh.win, sh.win_base, u, lane, d);
+        lb_window_read(sh.win, win_base, u, lane, d);
         uint64_t P = 0;
         uint32_t S = 0;
         if (reduce(u, d, P, S)) resolved(q, P, S);
@@ -2938,12 +2933,12 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
     // (other waves, or no such group) land in a dummy area and are never read.
     {
-      const bool want = wave == 0 && sh.res_next < sh.agg_next;
-      const uint32_t u = want ? sh.grp[sh.res_next % kLineGrpQ] : 0u;
+      const bool want = wave == 0 && res_next < agg_next;
+      const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
       const uint64_t base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
       if (want) {
-        sh.win_base = base;
-        sh.lb_step = sh.res_next;
+        win_base = base;
+        lb_step = res_next;
       }
     }
     // ---- buffer 1
@@ -2994,7 +2989,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     g = gn;
   }
   drain_bufsx(b);                                     // (and a look-back window still in flight)
-  if (wave == 0) sh.lb_step = 0xFFFFFFFFu;
+  if (wave == 0) lb_step = 0xFFFFFFFFu;
   __syncthreads();                                    // every wave's last summary is in LDS
   if (wave == 0) publish_agg(it);
   place_upto(it);

@@ -102,7 +102,11 @@ def load():
     except OSError as e:  # pragma: no cover - depends on the ROCm runtime being present
         raise DPScanUnavailable(f"cannot load {LIB_PATH}: {e}") from e
     for name, res, args in SIGNATURES:
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if "DPSCAN_LIB" in os.environ:     # an older build loaded for a same-box A/B: it lacks newer entry points
+                continue
+            raise DPScanUnavailable(f"{LIB_PATH} does not export {name}: rebuild it")
         fn.restype = res
         fn.argtypes = args
     _lib = lib
