@@ -2448,6 +2448,9 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_FASTA      // the FASTA form of line_kernel (DP_FASTA_FORM=line): not yet within the VGPR budget
 #define DP_LINE_FASTA 0    // (its build spills 16-20 B per lane, which the ISA guard refuses)
 #endif
+#ifndef DP_LINE_LA         // A/B: the input buffers with their lookahead dword (map_kernel's Buf)
+#define DP_LINE_LA 0
+#endif
 #ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
 #define DP_LINE_PRIO 0
 #endif
@@ -2544,6 +2547,12 @@ __device__ __forceinline__ void load_bufx(BufN& b, const ScanArgs& A, const Geo&
 __device__ __forceinline__ void wait_bufx(BufN& b) { wait_buf_n(b); }
 __device__ __forceinline__ void touch_bufx(BufN& b) { touch_buf_n(b); }
 __device__ __forceinline__ void drain_bufsx(BufN (&b)[kBufs]) { drain_bufs_n(b); }
+#if DP_LINE_LA
+__device__ __forceinline__ void load_bufx(Buf& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf(b, A, g, 0, lane, h); }
+__device__ __forceinline__ void wait_bufx(Buf& b) { wait_buf(b); }
+__device__ __forceinline__ void touch_bufx(Buf& b) { touch_buf(b); }
+__device__ __forceinline__ void drain_bufsx(Buf (&b)[kBufs]) { drain_bufs(b); }
+#endif
 typedef __attribute__((address_space(4))) const uint32_t cu32s;   // constant address space: s_load_dword
 
 // A window of FASTA group functions: the prefix count P and line state S entering group u, once resolvable.
@@ -2567,8 +2576,13 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   static_assert(kMapWaves == 16, "line_kernel: one workgroup of 16 waves per CU");
   constexpr bool kFa = MODE == kFasta;
   // no lookahead dword in flight for FASTA either (2 VGPRs): the byte after a buffer comes by a scalar load
+#if DP_LINE_LA
+  typedef Buf BufT;
+  constexpr int kLoadsX = kLoadsPerBuf;
+#else
   typedef BufN BufT;
   constexpr int kLoadsX = kLoadsPerBufN;
+#endif
   __shared__ __attribute__((aligned(16))) LineShared sh;
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
