@@ -2883,14 +2883,17 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   for (;; ++it) {
     __syncthreads();
     cur_it = it;
-    // the steps this workgroup places at the end of this step, decided here by every wave alike: resolved in an
-    // earlier step (the barrier above published them), in order, at most two
+#if DP_LINE_GROUP
+    // the group runs need every thread: the steps placed at the end of this step are decided here by every wave
+    // alike (resolved in an earlier step, which the barrier above published), in order, at most two.  (This
+    // places a step a step later than the per-wave check below: 951 vs 849 us per 4 GiB CSV, its slots fill.)
     uint32_t nplace = 0;
     for (uint32_t i = 0; i < 2u && nb + i < it; ++i) {
       const uint32_t q = nb + i, s_ = q % kLineSlots;
       if (sh.res[s_] != sh.grp[q % kLineGrpQ] + 1u || sh.rstep[s_] >= it) break;
       ++nplace;
     }
+#endif
     const uint32_t gnext = sh.grp[(it + 1) % kLineGrpQ];
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
     const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD &&
@@ -2992,10 +2995,20 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     // step, block for it here (only b[0]'s loads in flight, so the registers are free).  Blocking holds back
     // this workgroup's AGG of step it, its newest group, while it waits for an older one: the lowest waiting
     // group never depends on a held AGG.
+#if DP_LINE_GROUP
     for (uint32_t i = 0; i < nplace; ++i, ++nb) {
-      if constexpr (!kFa && OUT64 == 2 && DP_LINE_GROUP) place_group(nb);
+      if constexpr (!kFa && OUT64 == 2) place_group(nb);
       else place(nb, true);
     }
+#else
+    // every older step whose prefix is known, as soon as this wave sees it (wave-local order)
+    while (nb < it) {
+      if (lds_ld(&sh.res[nb % kLineSlots]) != sh.grp[nb % kLineGrpQ] + 1u) break;
+      cbar();
+      place(nb, true);
+      ++nb;
+    }
+#endif
     if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
     load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
