@@ -22,8 +22,7 @@ Workloads (synthetic bytes of the named shapes, resident in HBM before any timed
 One step = on every GPU, one scan call over its bytes: FASTA = dp_fasta_index_async + dp_fasta_result (the
 chunk-table check, the two scan kernels -- map_kernel<FASTA> over 16 KiB ranges, then fasta_place_kernel --,
 the split-header resolve kernel, the read-back of count / pending / chunk ends); newline = dp_delim_ranges
-(two kernels up to 512 MiB per launch, the one-pass look-back kernel above: a 32 GiB CSV or a 64/N GiB VCF
-part is one-pass).  The index stays in HBM (the H2D/D2H-inclusive end-to-end rate is DESIGN.md §6).  Steps
+(round 4: one launch of the lockstep line_kernel at every size).  The index stays in HBM (the H2D/D2H-inclusive end-to-end rate is DESIGN.md §6).  Steps
 alternate between two contexts and step k + 1 is enqueued before step k's result is collected; the library
 runs one scan at a time per GPU (its scan stream), so ``value`` is this pipelined rate provided
 ``ms_per_step`` >= the scan's own average span (checked; else the ``serialized`` rate, always reported).

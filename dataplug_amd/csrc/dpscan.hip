@@ -3255,7 +3255,8 @@ struct dp_ctx {
   bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
   int fasta_form = 0;                 // 0: map + placement kernels, 1: line_kernel (DP_FASTA_FORM = line | two)
   uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
-  int delim_form = 0;                 // newline kernels: 0 auto (by size), 1 line_kernel, 2 two kernels, 3 one-pass
+  int delim_form = 1;                 // newline kernels: 1 line_kernel (default), 0 by size (round 3: two kernels up
+                                      // to kDelimTwoPassMax, one-pass above), 2 two kernels, 3 one-pass
   uint32_t line_launches = 0;         // line_kernel launches (ticket parity)
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
@@ -3845,9 +3846,11 @@ int dp_ctx_create(int device, dp_ctx** out) {
   // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
   const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
   c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
-  // newline kernels (A/B): DP_DELIM_FORM = line | two | one (default: by launch size)
+  // newline kernels (A/B): DP_DELIM_FORM = line (default) | auto (round 3's choice by size) | two | one.  Round 4
+  // same box, CSV / VCF / FASTA bytes (profiles/r04/line/): line_kernel 67 / 64 / 66 us at 256 MiB (one-pass 82 /
+  // 81 / 80), 219 / 210 / 216 us at 1 GiB (239 / 229 / 226), 830 / 803 / 822 us at 4 GiB (877 / 802 / 822)
   const char* form = getenv("DP_DELIM_FORM");
-  c->delim_form = !form ? 0 : (!strcmp(form, "line") ? 1 : (!strcmp(form, "two") ? 2 : (!strcmp(form, "one") ? 3 : 0)));
+  c->delim_form = !form ? 1 : (!strcmp(form, "auto") ? 0 : (!strcmp(form, "two") ? 2 : (!strcmp(form, "one") ? 3 : 1)));
   *out = c;
   return DP_OK;
 }

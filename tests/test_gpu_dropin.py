@@ -351,7 +351,7 @@ def test_bench_default_line_carries_the_newline_legs():
         rf = sub["roofline"]
         assert rf["frac"] > 0 and rf["measured_peak"] > 0 and rf["measured_mixed_ref"] > 0
         assert sub["cpu_baseline"]["value"] > 0 and sub["cpu_baseline"]["cores"] >= 1
-        assert rf["kernel"].startswith("map_kernel<DELIM>")          # <= 512 MiB: the two-kernel form
+        assert rf["kernel"].startswith("line_kernel<DELIM>")         # the default newline form
     assert line["bench_wall_s"] > 0
 
 

@@ -489,23 +489,28 @@ def test_repeated_launches_and_sizes():
         c.close()
 
 
-def _delim_ctx(twopass_max):
+def _delim_ctx(twopass_max, form="auto"):
+    """A context pinned to round 3's size-based newline forms (form "auto": two kernels up to twopass_max bytes,
+    the one-pass kernel above) or, form "line", to the default lockstep line_kernel."""
     from dataplug_amd.scan import ScanContext
     os.environ["DP_DELIM_TWOPASS_MAX"] = str(twopass_max)
+    os.environ["DP_DELIM_FORM"] = form
     try:
         c = ScanContext(0)
     finally:
         del os.environ["DP_DELIM_TWOPASS_MAX"]
+        del os.environ["DP_DELIM_FORM"]
     assert c.forms()[1] == twopass_max
     return c
 
 
 @pytest.mark.parametrize("size", [1, 5_000, 64 * 16384 - 3, 64 * 16384 + 16385, (7 << 20) + 11, (70 << 20) + 5])
 def test_newline_forms_equal(size):
-    """The newline index's two forms (map + 64-range placement blocks, the default up to 512 MiB per launch, and
-    the one-pass kernel) give the oracle's offsets in every output form, with every_k / emit_add / carry, on CSV
-    rows (some ranges over the 512-entry spill slot: dense rescans), a run of newlines and newline-free spans."""
-    two, one = _delim_ctx(1 << 62), _delim_ctx(0)
+    """The newline index's three forms (line_kernel, the default; map + 64-range placement blocks; the one-pass
+    look-back kernel) give the oracle's offsets in every output form, with every_k / emit_add / carry, on CSV
+    rows (some ranges over the 512-entry spill slot and line_kernel's 640-entry LDS list: dense rescans), a run
+    of newlines and newline-free spans; all three write the same block table."""
+    two, one, line = _delim_ctx(1 << 62), _delim_ctx(0), _delim_ctx(0, "line")
     try:
         a = synth.csv(size, seed=size % 89) if size > 4096 else np.full(size, 10, np.uint8)
         if size > (1 << 20):
@@ -516,6 +521,8 @@ def test_newline_forms_equal(size):
         two.h2d(d.ptr + 3, a)
         d1 = one.workspace("t_in", n + 64)
         one.h2d(d1.ptr + 3, a)
+        d2 = line.workspace("t_in", n + 64)
+        line.h2d(d2.ptr + 3, a)
         base = 3
         full = dpref.delim(a, 0, n)[0] + np.uint64(base)
         for k, add, carry in ((1, 0, 0), (4, 1, 2), (3, 0, 7)):
@@ -523,7 +530,7 @@ def test_newline_forms_equal(size):
             exp = full[(sel % np.uint64(k)) == np.uint64(k - 1)] + np.uint64(add)
             for mode in (1, 0, 3):
                 outs = []
-                for c, dp in ((two, d.ptr + 3), (one, d1.ptr + 3)):
+                for c, dp in ((two, d.ptr + 3), (one, d1.ptr + 3), (line, d2.ptr + 3)):
                     if mode == 3 and (k != 1 or add != 0):
                         # the block table counts delimiters: an entry index only when every delimiter is one
                         with pytest.raises(DPScanError, match="out_mode 3 needs every_k == 1"):
@@ -543,13 +550,15 @@ def test_newline_forms_equal(size):
                         assert np.array_equal(r[0].astype(np.uint64), exp), (k, add, carry, mode)
                 if not outs:
                     continue
-                assert np.array_equal(outs[0][0], outs[1][0]) and outs[0][1] == outs[1][1]
-                assert np.array_equal(np.asarray(outs[0][2]), np.asarray(outs[1][2]))
-                if mode == 3:                                     # the two forms' block tables too
-                    assert np.array_equal(outs[0][3], outs[1][3])
+                for o in outs[1:]:
+                    assert np.array_equal(outs[0][0], o[0]) and outs[0][1] == o[1]
+                    assert np.array_equal(np.asarray(outs[0][2]), np.asarray(o[2]))
+                    if mode == 3:                                 # the forms' block tables too
+                        assert np.array_equal(outs[0][3], o[3])
     finally:
         two.close()
         one.close()
+        line.close()
 
 
 def test_forms_alternate_on_one_context():

@@ -56,7 +56,8 @@ def main():
     sizes = [int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")]
     top = max(sizes)
     makers = {"onepass": lambda: make_ctx(0, "one"), "twokernel": lambda: make_ctx(1 << 62, "two"),
-              "line": lambda: make_ctx(None, "line"), "default": lambda: make_ctx()}
+              "line": lambda: make_ctx(None, "line"), "auto": lambda: make_ctx(None, "auto"),
+              "default": lambda: make_ctx()}
     forms = {k: makers[k]() for k in args.forms.split(",")}
     ctx0 = next(iter(forms.values()))
     d = ctx0.workspace("in", top + 64)
