@@ -2593,12 +2593,18 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   unsigned int* ticket = L.ticket + L.parity;
   if (blockIdx.x == 0 && threadIdx.x == 0) L.ticket[L.parity ^ 1u] = 0u;   // the next launch's ticket
   uint32_t claimed = 2, run = 0, pend = 0, claim_res = 0;
+  // Every group is claimed from the ticket, the first two as well (one atomic), never assigned by blockIdx: a
+  // group then only ever waits on lower groups that running workgroups hold, so a grid need not be resident
+  // all at once (two processes' grids sharing a GPU: with static first groups each grid's running workgroups
+  // waited on its own unstarted ones, which waited for the other grid's CUs).
   if (threadIdx.x == 0) {
-    sh.grp[0] = blockIdx.x;                          // (the host launches at most one workgroup per group)
-    sh.grp[1] = G + blockIdx.x;
+    const uint32_t u0 = atomicAdd(ticket, 2u);
+    sh.grp[0] = u0;
+    sh.grp[1] = u0 + 1u;
   }
   if (threadIdx.x < kLineSlots) sh.res[threadIdx.x] = 0u;
   __syncthreads();
+  if (sh.grp[0] >= ngroups) return;                  // (uniform) every group went to another workgroup
   const uint32_t key = A.delim ^ kSel12;
   uint32_t r = sh.grp[0] * kMapWaves + (uint32_t)wave;
   Cursor cur{0, 0, 0, 0, 0, 0};
@@ -2964,7 +2970,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     __builtin_amdgcn_sched_barrier(0);
     if (pend) {                                       // the wait above covered the claim: its value is back
       asm volatile("" : "+v"(claim_res) :: "memory");
-      const uint32_t u = 2u * G + rfl(claim_res);
+      const uint32_t u = rfl(claim_res);
       if (lane == 0)
         for (uint32_t i = 0; i < pend; ++i) sh.grp[(claimed + i) % kLineGrpQ] = u + i;
       claimed += pend;

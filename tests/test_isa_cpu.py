@@ -16,8 +16,8 @@ from dataplug_amd.scan import _lib
 
 SHIPPED = ["scan_kernel<0,0>", "scan_kernel<0,1>", "scan_kernel<1,0>", "scan_kernel<1,1>", "scan_kernel<1,2>",
            "map_kernel<0>", "map_kernel<1>", "fasta_place_kernel<0>", "fasta_place_kernel<1>",
-           "delim_place_kernel<0>", "delim_place_kernel<1>", "delim_place_kernel<2>", "line_kernel<0>",
-           "line_kernel<1>", "line_kernel<2>", "fasta_resolve_kernel",
+           "delim_place_kernel<0>", "delim_place_kernel<1>", "delim_place_kernel<2>", "line_kernel<1,0>",
+           "line_kernel<1,1>", "line_kernel<1,2>", "fasta_resolve_kernel",
            "find_kernel", "stream_kernel", "stream_rw_kernel"]
 
 
