@@ -2458,8 +2458,11 @@ constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workg
 constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
 static_assert(kLineSlots >= 3 && kLineSlots <= 6, "line slots: phase A, resolution, placement + slack");
 static_assert(kLineCap % 8 == 0 && kLineCap <= 1024, "line cap");
-constexpr uint32_t kLineGrpQ = 8;                  // claimed groups by step (>= slots + claim-ahead + 1)
-static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + 1, "group queue spans the pending and claimed steps");
+#ifndef DP_LINE_RUN        // consecutive groups per claim (one returning atomic on one address each)
+#define DP_LINE_RUN 1
+#endif
+constexpr uint32_t kLineGrpQ = 16;                 // claimed groups by step (>= slots + claim-ahead + run)
+static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + DP_LINE_RUN, "group queue spans the pending and claimed steps");
 constexpr uint32_t kLineDense = 0x80000000u;
 constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
 constexpr uint32_t kLineEnd = 128u;                // geo.z: the launch's last range (writes the total)
@@ -2904,7 +2907,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
     const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD &&
                           sh.grp[(claimed - 1) % kLineGrpQ] < ngroups;
-    if (do_claim) run = sh.grp[(claimed - 1) % kLineGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
+    if (do_claim) run = sh.grp[(claimed - 1) % kLineGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_LINE_RUN;
     const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
     const uint32_t slot = it % kLineSlots;
     FState st{0u, 0u, 0u, -1, 0u, 0u};               // DELIM: st.nev only
