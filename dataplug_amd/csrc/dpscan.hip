@@ -3214,6 +3214,13 @@ thread_local std::string g_err;
 // form is 4-24 % faster up to 512 MiB (the one-pass kernel's ~35-40 us start and tail), the one-pass kernel
 // 2-28 % faster from 1 GiB (the two-kernel form moves every delimiter through the spill: 4 more bytes each).
 constexpr uint64_t kDelimTwoPassMax = 512ull << 20;
+// Round 4: the default newline form is line_kernel up to this many bytes per launch and the one-pass look-back
+// kernel above.  Same boxes, CSV / VCF (profiles/r04/line*, big*): line_kernel's fixed cost is ~5-15 us against
+// the one-pass kernel's ~30 us, so it is faster up to 1-2 GiB (256 MiB: 67 / 64 us vs 82 / 81; 1 GiB: 219 / 210
+// vs 239 / 229), but its steady state stays at ~5.0-5.2 TB/s of input (one group claim per 256 KiB step and the
+// group look-back chain per round) where the one-pass kernel streams at 5.3-5.9: at 4 GiB 830-906 vs 765-877 us
+// depending on the box, at 16 GiB CSV 3,607 vs 3,401 us, at 32 GiB 7,082 vs 5,855 us.
+constexpr uint64_t kDelimLineMax = 2ull << 30;
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -3264,8 +3271,9 @@ struct dp_ctx {
   bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
   int fasta_form = 0;                 // 0: map + placement kernels, 1: line_kernel (DP_FASTA_FORM = line | two)
   uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
-  int delim_form = 1;                 // newline kernels: 1 line_kernel (default), 0 by size (round 3: two kernels up
-                                      // to kDelimTwoPassMax, one-pass above), 2 two kernels, 3 one-pass
+  int delim_form = 4;                 // newline kernels: 4 (default) line_kernel up to kDelimLineMax bytes, one-pass
+                                      // above; 0 round 3's rule (two kernels up to kDelimTwoPassMax, one-pass above);
+                                      // 1 line_kernel, 2 two kernels, 3 one-pass at every size
   uint32_t line_launches = 0;         // line_kernel launches (ticket parity)
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
@@ -3855,11 +3863,10 @@ int dp_ctx_create(int device, dp_ctx** out) {
   // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
   const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
   c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
-  // newline kernels (A/B): DP_DELIM_FORM = line (default) | auto (round 3's choice by size) | two | one.  Round 4
-  // same box, CSV / VCF / FASTA bytes (profiles/r04/line/): line_kernel 67 / 64 / 66 us at 256 MiB (one-pass 82 /
-  // 81 / 80), 219 / 210 / 216 us at 1 GiB (239 / 229 / 226), 830 / 803 / 822 us at 4 GiB (877 / 802 / 822)
+  // newline kernels (A/B): DP_DELIM_FORM = hybrid (default) | line | auto (round 3's choice by size) | two | one
   const char* form = getenv("DP_DELIM_FORM");
-  c->delim_form = !form ? 1 : (!strcmp(form, "auto") ? 0 : (!strcmp(form, "two") ? 2 : (!strcmp(form, "one") ? 3 : 1)));
+  c->delim_form = !form ? 4 : !strcmp(form, "line") ? 1 : !strcmp(form, "auto") ? 0 : !strcmp(form, "two") ? 2
+                : !strcmp(form, "one") ? 3 : 4;
   *out = c;
   return DP_OK;
 }
@@ -4103,7 +4110,8 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   uint64_t units = 0, span = 0;
   for (uint64_t i = 0; i < nr; ++i) span += rg[2 * i + 1] - rg[2 * i];
   const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
-  if (c->delim_form == 1) {                           // the lockstep one-pass kernel
+  const bool line = c->delim_form == 1 || (c->delim_form == 4 && span <= kDelimLineMax);
+  if (line) {                                         // the lockstep one-pass kernel
     rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
     if (rc) return rc;
     rc = launch_line(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
@@ -4287,7 +4295,8 @@ int dp_scan_forms(dp_ctx* c, int* fasta_two_kernel, uint64_t* delim_two_kernel_m
 
 int dp_scan_delim_form(dp_ctx* c, uint64_t span, int* form) {
   if (!c || !form) return fail(DP_ERR_INVALID, "null");
-  *form = c->delim_form == 1 ? 1 : (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) ? 2 : 3;
+  *form = (c->delim_form == 1 || (c->delim_form == 4 && span <= kDelimLineMax)) ? 1
+          : (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) ? 2 : 3;
   return DP_OK;
 }
 
