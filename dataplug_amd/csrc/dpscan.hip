@@ -1079,7 +1079,9 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
           w[e] = a | (b << 16);
         }
         const v4u pk = {w[0], w[1], w[2], w[3]};
-#if DP_NTSTORE
+#if defined(DP_PROBE_NOSTORE)
+        ovf |= (pk.x ^ pk.y ^ pk.z ^ pk.w) == 0x9E3779B9u;   // timing probe (wrong results): the gathers, no store
+#elif DP_NTSTORE
         __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + i));
 #else
         *reinterpret_cast<v4u*>(o + i) = pk;
