@@ -22,7 +22,9 @@ Workloads (synthetic bytes of the named shapes, resident in HBM before any timed
 One step = on every GPU, one scan call over its bytes: FASTA = dp_fasta_index_async + dp_fasta_result (the
 chunk-table check, the two scan kernels -- map_kernel<FASTA> over 16 KiB ranges, then fasta_place_kernel --,
 the split-header resolve kernel, the read-back of count / pending / chunk ends); newline = dp_delim_ranges
-(round 4: one launch of the lockstep line_kernel at every size).  The index stays in HBM (the H2D/D2H-inclusive end-to-end rate is DESIGN.md §6).  Steps
+(one launch: the lockstep line_kernel up to 2 GiB, the one-pass look-back scan_kernel above, dp_scan_delim_form;
+the kernel that ran is named in each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
+rate is DESIGN.md §6).  Steps
 alternate between two contexts and step k + 1 is enqueued before step k's result is collected; the library
 runs one scan at a time per GPU (its scan stream), so ``value`` is this pipelined rate provided
 ``ms_per_step`` >= the scan's own average span (checked; else the ``serialized`` rate, always reported).

@@ -2214,7 +2214,20 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
 // are coalesced 16-byte groups.  Ranges with more than kSpillCap delimiters ("dense") are rescanned from the
 // input by dense_b.  every_k / emit_add / carry and the four output forms are those of the one-pass kernel.
 __device__ __forceinline__ uint64_t pack_count(uint64_t st, uint64_t count) { return st | (count & 0xFFFFFFFFFFFFull); }
-__device__ __forceinline__ bool lb_reduce_count(uint64_t (&d)[kLbPer], uint32_t W, uint64_t basedesc, int lane, uint64_t& P) {
+// the 64-bit sum over the wave (two 32-bit halves through DPP), uniform
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t sum) {
+  sum += dpp64<kRowShr1, 0xF>(sum, 0ull);
+  sum += dpp64<kRowShr2, 0xF>(sum, 0ull);
+  sum += dpp64<kRowShr4, 0xF>(sum, 0ull);
+  sum += dpp64<kRowShr8, 0xF>(sum, 0ull);
+  sum += dpp64<kRowBcast15, 0xA>(sum, 0ull);
+  sum += dpp64<kRowBcast31, 0xC>(sum, 0ull);
+  return readlane64(sum, kWave - 1);
+}
+// ``all`` (optional): set, with P = the window's total count, when every descriptor is published and none is a
+// PREFIX (the look-back can go on past the window)
+__device__ __forceinline__ bool lb_reduce_count(uint64_t (&d)[kLbPer], uint32_t W, uint64_t basedesc, int lane, uint64_t& P,
+                                                bool* all = nullptr) {
   const uint32_t rl = (uint32_t)(kWave - 1 - lane);
   uint32_t seen = 0, bad = 0;
 #pragma unroll
@@ -2226,7 +2239,16 @@ __device__ __forceinline__ bool lb_reduce_count(uint64_t (&d)[kLbPer], uint32_t 
   }
   const uint64_t PB = __ballot(seen);
   const uint64_t BB = __ballot(bad);
-  if (PB == 0ull) return false;
+  if (PB == 0ull) {
+    if (all != nullptr && BB == 0ull) {
+      uint64_t s = 0;
+#pragma unroll
+      for (int j = 0; j < kLbPer; ++j) s += d[j] & 0xFFFFFFFFFFFFull;
+      P = wave_sum64(s);
+      *all = true;
+    }
+    return false;
+  }
   const int Lp = 63 - __builtin_clzll(PB);            // nearest lane holding a prefix
   const uint64_t need = ~((1ull << Lp) - 1ull);
   if (BB & need) return false;
@@ -2242,16 +2264,7 @@ __device__ __forceinline__ bool lb_reduce_count(uint64_t (&d)[kLbPer], uint32_t 
     if (k < kP) sum += d[j] & 0xFFFFFFFFFFFFull;
     if (k == kP) pv = d[j] & 0xFFFFFFFFFFFFull;
   }
-  // wave sum (64-bit, two 32-bit halves through DPP)
-  uint32_t lo = (uint32_t)sum, hi = (uint32_t)(sum >> 32);
-  sum = ((uint64_t)hi << 32) | lo;
-  sum += dpp64<kRowShr1, 0xF>(sum, 0ull);
-  sum += dpp64<kRowShr2, 0xF>(sum, 0ull);
-  sum += dpp64<kRowShr4, 0xF>(sum, 0ull);
-  sum += dpp64<kRowShr8, 0xF>(sum, 0ull);
-  sum += dpp64<kRowBcast15, 0xA>(sum, 0ull);
-  sum += dpp64<kRowBcast31, 0xC>(sum, 0ull);
-  P = readlane64(pv, Lp) + readlane64(sum, kWave - 1);
+  P = readlane64(pv, Lp) + wave_sum64(sum);
   return true;
 }
 
@@ -2456,6 +2469,27 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
 #define DP_LINE_PRIO 0
 #endif
+#ifndef DP_LINE_DUMMY      // A/B: dummy look-back windows loaded by all 64 lanes (0: by lane 0 only)
+#define DP_LINE_DUMMY 0
+#endif
+#ifndef DP_LINE_PUBW       // the wave that publishes each group's AGG (wave 0 resolves the prefixes)
+#define DP_LINE_PUBW 0
+#endif
+constexpr int kPubWave = DP_LINE_PUBW;
+// timing probe only (wrong results): the lockstep scan and its LDS records without any look-back, publication,
+// placement or stall (every step's window loads, descriptor stores and index stores left out)
+#ifdef DP_LINE_SCANONLY
+constexpr bool kScanOnly = true;
+#else
+constexpr bool kScanOnly = false;
+#endif
+// DP_LINE_LATE 1: a step's look-back window is issued at its end (after b[1]'s reload) and reduced after the next
+// step's second buffer wait, so it sees the AGGs the other workgroups published half a step later; 0: issued
+// after b[0]'s reload, reduced at the next step's start
+#ifndef DP_LINE_LATE
+#define DP_LINE_LATE 1
+#endif
+constexpr bool kLineLate = DP_LINE_LATE != 0;
 constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
 constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
 static_assert(kLineSlots >= 3 && kLineSlots <= 6, "line slots: phase A, resolution, placement + slack");
@@ -2468,11 +2502,22 @@ static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + DP_LINE_RUN, "group queue
 constexpr uint32_t kLineDense = 0x80000000u;
 constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
 constexpr uint32_t kLineEnd = 128u;                // geo.z: the launch's last range (writes the total)
-// A look-back window (kLbSlots descriptors before a group) arrives by LDS-DMA: kLineWinLoads 16-byte-per-lane
-// loads from an even descriptor index, so 384 descriptors cover any 256 before the group.
-constexpr uint32_t kLineWinLoads = 3;
+// A look-back window (kLineSpan descriptors before a group) arrives by LDS-DMA: kLineWinLoads 16-byte-per-lane
+// loads from an even descriptor index, so 128 descriptors per load cover any kLineSpan before the group.
+// Two parts (DELIM): the nearest kLbSlots groups (~one round of the grid's claims) are reduced first; when all of
+// them are published and none is resolved, the kLbSlots before them.  So a group's prefix does not wait for the
+// round before it to be resolved, only for its AGGs (published without any dependency): a look-back limited to the
+// round before chained every round's resolution to the last one's, and one late workgroup delayed all later ones.
+#ifndef DP_LINE_LBPARTS
+#define DP_LINE_LBPARTS 2
+#endif
+constexpr uint32_t kLineLbParts = DP_LINE_LBPARTS;
+constexpr uint32_t kLineSpan = kLbSlots * kLineLbParts;
+constexpr uint32_t kLineWinLoads = (kLineSpan + 2 + 2 * kWave - 1) / (2 * kWave);
 constexpr uint32_t kLineWin = kLineWinLoads * kWave * 2;
-static_assert(kLineWin >= kLbSlots + 2 + 126, "window loads cover kLbSlots descriptors from an even start");
+static_assert(kLineLbParts == 1 || kLineLbParts == 2, "look-back window parts");
+static_assert(kLineWin >= kLineSpan + 2, "window loads cover kLineSpan descriptors from an even start");
+constexpr int kWinN = kScanOnly ? 0 : (int)kLineWinLoads;   // window loads per wave and step
 
 struct LineShared {
   uint16_t ev[kLineSlots][kMapWaves][kLineCap];    // per slot and wave: the range's positions
@@ -2508,11 +2553,11 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 // Look-back window of group u into LDS by LDS-DMA, hand-waited (inline asm: the compiler adds no wait, and no
-// VGPR is held while the loads travel): descriptors [base, base + kLineWin) of which [u - kLbSlots, u) matter.
+// VGPR is held while the loads travel): descriptors [base, base + kLineWin) of which [u - kLineSpan, u) matter.
 // Relaxed agent-scope reads (sc1), as ld_desc.  Returns base.
 __device__ __forceinline__ uint64_t lb_window_dma(const ScanArgs& A, uint64_t desc_cap, uint32_t u, unsigned long long* win,
                                                   int lane) {
-  uint64_t base = u > kLbSlots ? ((uint64_t)(u - kLbSlots) & ~1ull) : 0ull;
+  uint64_t base = u > kLineSpan ? ((uint64_t)(u - kLineSpan) & ~1ull) : 0ull;
   if (base + kLineWin > desc_cap) base = desc_cap - kLineWin;      // (desc_cap: a multiple of 1024 >= kLineWin)
   const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr(win));
 #pragma unroll
@@ -2536,7 +2581,8 @@ __device__ __forceinline__ void lb_window_read(const unsigned long long* win, ui
   }
 }
 // Reduce a loaded window of group u: true with the group's launch prefix P once resolvable.
-__device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P) {
+__device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P,
+                                                bool* all = nullptr) {
   const uint32_t W = u < kLbSlots ? u : kLbSlots;
   const uint32_t rl = (uint32_t)(kWave - 1 - lane);
 #pragma unroll
@@ -2544,7 +2590,7 @@ __device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, u
     const uint32_t k = kLbPer * rl + j;
     d[j] = k < W ? ((d[j] & kEpochMask) == A.epoch ? d[j] : 0ull) : kIdentDesc;
   }
-  return lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P);
+  return lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P, all);
 }
 
 // Buffers of the lockstep kernels (BufN: no lookahead dword in flight; FASTA reads it by a scalar load).
@@ -2889,7 +2935,48 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   // claim atomic, wave 0's descriptor stores | b0 reload | wave 0's look-back window (LDS-DMA: no VGPRs held) |
   // wait b1 (the b0 reload and the window may stay in flight) | phase-B stores | b1 reload | barrier | wait b0:
   // the window has landed.  So the look-back travels for a whole step and no wait covers a load just issued.
+  // (wave 0) reduce the look-back window that has landed (lb_step: the step of its group)
+  auto consume = [&]() {
+    if (lb_step == 0xFFFFFFFFu) return;
+    const uint32_t q = lb_step, u = sh.grp[q % kLineGrpQ];
+    lb_step = 0xFFFFFFFFu;
+    uint64_t d[kLbPer];
+    lb_window_read(sh.win, win_base, u, lane, d);
+    uint64_t P = 0;
+    uint32_t S = 0;
+    bool ok;
+    if constexpr (!kFa && kLineLbParts == 2) {
+      bool all = false;
+      ok = lb_count_window(A, u, d, lane, P, &all);
+      if (!ok && all) {                               // (u >= kLbSlots) the part before: its prefix + this sum
+        const uint64_t S1 = P;
+        lb_window_read(sh.win, win_base, u - kLbSlots, lane, d);
+        ok = lb_count_window(A, u - kLbSlots, d, lane, P);
+        P += S1;
+      }
+    } else {
+      ok = reduce(u, d, P, S);
+    }
+    if (ok) resolved(q, P, S);
+  };
+  // Every wave issues the window's kLineWinLoads LDS-DMA loads once per step, so the waits have one count on
+  // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
+  // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
+  // (other waves, or no such group) land in a dummy area and are never read.
+  auto issue_window = [&]() {
+    if (kScanOnly) return;
+    const bool want = wave == 0 && res_next < agg_next;
+    const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
+    uint64_t base = 0;
+    // a dummy window is lane 0's 16 bytes per load (the count is per instruction, the bytes per active lane)
+    if (want || lane == 0 || DP_LINE_DUMMY) base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
+    if (want) {
+      win_base = base;
+      lb_step = res_next;
+    }
+  };
   static_assert(kBufs == 2, "line_kernel: two input buffers per range");
+  if (kLineLate) issue_window();                      // (a dummy: the first step's wait counts a window)
   uint32_t it = 0;
   for (;; ++it) {
     __syncthreads();
@@ -2936,43 +3023,33 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       }
     };
     // ---- buffer 0
-    wait_bufx(b[0]);                                  // the youngest operations in flight: b[1]'s loads
+    // the youngest operations in flight: b[1]'s loads (and, kLineLate, the window issued after them)
+    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsX + (kLineLate ? kWinN : 0)) : "memory");
+    touch_bufx(b[0]);
+    __builtin_amdgcn_sched_barrier(0);
     if (do_claim) {
       claim_res = atomic_add_nowait(ticket, run);
       pend = run;
     }
-    if (wave == 0) {
-      if (lb_step != 0xFFFFFFFFu) {                   // issued a step ago, older than b[1]'s loads: landed
-        const uint32_t q = lb_step, u = sh.grp[q % kLineGrpQ];
-        lb_step = 0xFFFFFFFFu;
-        uint64_t d[kLbPer];
-        lb_window_read(sh.win, win_base, u, lane, d);
-        uint64_t P = 0;
-        uint32_t S = 0;
-        if (reduce(u, d, P, S)) resolved(q, P, S);
-      }
+    if (!kScanOnly && wave == 0) {
+      if (!kLineLate) consume();                      // issued a step ago, older than b[1]'s loads: landed
       // every wave wrote step it - 1's summary before the barrier: its AGG goes out before anything blocks
-      if (it > 0) publish_agg(it - 1);
+      if (kPubWave == 0 && it > 0) publish_agg(it - 1);
+      if (kPubWave != 0) agg_next = it;                // published by wave kPubWave in this step
     }
+    if (!kScanOnly && kPubWave != 0 && wave == kPubWave && it > 0) publish_agg(it - 1);
     rows(0);
     load_bufx(b[0], A, gn, lane, 0);
     // Every wave issues the window's kLineWinLoads LDS-DMA loads every step, so the wait below has one count on
     // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
     // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
     // (other waves, or no such group) land in a dummy area and are never read.
-    {
-      const bool want = wave == 0 && res_next < agg_next;
-      const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
-      const uint64_t base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
-      if (want) {
-        win_base = base;
-        lb_step = res_next;
-      }
-    }
+    if (!kLineLate) issue_window();
     // ---- buffer 1
-    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsX + kLineWinLoads) : "memory");   // b[0] + window in flight
+    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsX + (kLineLate ? 0 : kWinN)) : "memory");   // b[0] (+ window) in flight
     touch_bufx(b[1]);
     __builtin_amdgcn_sched_barrier(0);
+    if (kLineLate && !kScanOnly && wave == 0) consume();   // issued at the end of the last step, before b[0]'s reload
     if (pend) {                                       // the wait above covered the claim: its value is back
       asm volatile("" : "+v"(claim_res) :: "memory");
       const uint32_t u = rfl(claim_res);
@@ -3013,15 +3090,16 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
 #else
     // every older step whose prefix is known, as soon as this wave sees it (wave-local order)
-    while (nb < it) {
+    while (!kScanOnly && nb < it) {
       if (lds_ld(&sh.res[nb % kLineSlots]) != sh.grp[nb % kLineGrpQ] + 1u) break;
       cbar();
       place(nb, true);
       ++nb;
     }
 #endif
-    if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
+    if (!kScanOnly && nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
     load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
+    if (kLineLate) issue_window();
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
@@ -3029,7 +3107,12 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   drain_bufsx(b);                                     // (and a look-back window still in flight)
   if (wave == 0) lb_step = 0xFFFFFFFFu;
   __syncthreads();                                    // every wave's last summary is in LDS
-  if (wave == 0) publish_agg(it);
+  if (kScanOnly) return;
+  if (wave == kPubWave) publish_agg(it);
+  if (kPubWave != 0) {
+    __syncthreads();                                  // wave 0 resolves with the group's counts
+    if (wave == 0) agg_next = it + 1;
+  }
   place_upto(it);
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
