@@ -156,6 +156,9 @@ enum Mode { kFasta = 0, kDelim = 1 };
 // accumulated s_memtime deltas; read back with dp_debug_profile().
 // -DDP_PROF2: only the two-kernel form's stamps (map_kernel / fasta_place_kernel), none in scan_kernel, whose
 // DP_PROF accumulators cost registers (its DP_PROF build spills and fails tools/isa_guard.py).
+#if defined(DP_LTL) && !defined(DP_PROF) && !defined(DP_PROF2)
+#define DP_PROF2 1   // -DDP_LTL: line_kernel's per-step timeline (implies the two-kernel form's stamps)
+#endif
 #if defined(DP_PROF) && defined(DP_PROF2)
 #error "DP_PROF and DP_PROF2 are exclusive"
 #endif
@@ -164,7 +167,16 @@ enum Mode { kFasta = 0, kDelim = 1 };
 constexpr int kProfSlots = 8;
 constexpr int kProfWaves = 16;
 constexpr int kProfMaxGrid = 1024;
-__device__ unsigned long long g_prof[kProfMaxGrid * kProfWaves * kProfSlots];
+#ifdef DP_LTL
+// line_kernel timeline (realtime clock, 100 MHz) past the per-wave slots: [256 workgroups][64 steps][waves 0, 1, 8,
+// 15][8 events] (tools/line_timeline.py names them)
+constexpr uint64_t kLtlBase = (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;
+constexpr uint32_t kLtlSteps = 64, kLtlWaves = 4;
+constexpr uint64_t kProfWords = kLtlBase + 256ull * kLtlSteps * kLtlWaves * 8;
+#else
+constexpr uint64_t kProfWords = (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;
+#endif
+__device__ unsigned long long g_prof[kProfWords];
 #endif
 #ifdef DP_PROF
 #define PROF_DECL uint64_t prof_acc[kProfSlots] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t prof_t = __builtin_amdgcn_s_memtime()
@@ -2457,9 +2469,9 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #ifndef DP_LINE_CAP
 #define DP_LINE_CAP 640
 #endif
-#ifndef DP_LINE_GROUP      // the uint16 index's placements as one contiguous run per group (0, default: one run per
-#define DP_LINE_GROUP 0    // range; 1 measured no faster: 951-957 vs 951 us per 4 GiB CSV, and it needs the VGPRs
-#endif                     // that keep wave 0's bookkeeping in registers)
+#ifndef DP_LINE_SHARE      // 1: a step's 16 ranges are placed by whichever waves reach the placement first (claimed
+#define DP_LINE_SHARE 1    // from an LDS counter); 0: every wave places its own range
+#endif
 #ifndef DP_LINE_FASTA      // the FASTA form of line_kernel (DP_FASTA_FORM=line): not yet within the VGPR budget
 #define DP_LINE_FASTA 0    // (its build spills 16-20 B per lane, which the ISA guard refuses)
 #endif
@@ -2476,20 +2488,51 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #define DP_LINE_PUBW 0
 #endif
 constexpr int kPubWave = DP_LINE_PUBW;
+constexpr bool kLineShare = DP_LINE_SHARE != 0;
+// DP_LINE_B1EARLY (A/B): b[1]'s reload before the step's placements instead of after them; the placement stores
+// are then younger than it, so the next step's first wait also waits for as many of b[1]'s loads (correct, slower
+// the more stores a step has)
+#ifndef DP_LINE_B1EARLY
+#define DP_LINE_B1EARLY 0
+#endif
+constexpr bool kLineB1Early = DP_LINE_B1EARLY != 0;
 // timing probe only (wrong results): the lockstep scan and its LDS records without any look-back, publication,
 // placement or stall (every step's window loads, descriptor stores and index stores left out)
 #ifdef DP_LINE_SCANONLY
 constexpr bool kScanOnly = true;
+constexpr bool kScanDma = DP_LINE_SCANONLY == 2;    // (2: with the look-back window loads of every step)
 #else
 constexpr bool kScanOnly = false;
+constexpr bool kScanDma = false;
 #endif
+#ifndef DP_LINE_W0DMA      // 1: only wave 0 issues window loads (every other wave's waits count none)
+#define DP_LINE_W0DMA 0
+#endif
+constexpr bool kW0Dma = DP_LINE_W0DMA != 0;
+#ifdef DP_LTL
+#define LTL(step, e) do { const int lw_ = wave == 0 ? 0 : wave == 1 ? 1 : wave == 8 ? 2 : wave == 15 ? 3 : -1; \
+    if (lw_ >= 0 && lane == 0 && blockIdx.x < 256 && (uint32_t)(step) < kLtlSteps) \
+      g_prof[kLtlBase + (((uint64_t)blockIdx.x * kLtlSteps + (uint32_t)(step)) * kLtlWaves + lw_) * 8 + (e)] = \
+          __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define LTL(step, e) do {} while (0)
+#endif
+// s_waitcnt vmcnt with the count of wave 0 (first) or of every other wave
+template <int A0, int B0>
+__device__ __forceinline__ void vm_wait2(bool first) {
+  if (A0 == B0 || first) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(A0) : "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" :: "i"(B0) : "memory");
+}
 // DP_LINE_LATE 1: a step's look-back window is issued at its end (after b[1]'s reload) and reduced after the next
 // step's second buffer wait, so it sees the AGGs the other workgroups published half a step later; 0: issued
 // after b[0]'s reload, reduced at the next step's start
 #ifndef DP_LINE_LATE
 #define DP_LINE_LATE 1
 #endif
-constexpr bool kLineLate = DP_LINE_LATE != 0;
+// DP_LINE_LATE 2: issued at the step end before b[1]'s reload, reduced after the next step's b[0] reload and a
+// wait for the window alone (b[1]'s loads may still be in flight: the reduction overlaps them)
+constexpr int kLineLate = DP_LINE_LATE;
+static_assert(kLineLate >= 0 && kLineLate <= 2, "DP_LINE_LATE");
 constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
 constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
 static_assert(kLineSlots >= 3 && kLineSlots <= 6, "line slots: phase A, resolution, placement + slack");
@@ -2517,7 +2560,8 @@ constexpr uint32_t kLineWinLoads = (kLineSpan + 2 + 2 * kWave - 1) / (2 * kWave)
 constexpr uint32_t kLineWin = kLineWinLoads * kWave * 2;
 static_assert(kLineLbParts == 1 || kLineLbParts == 2, "look-back window parts");
 static_assert(kLineWin >= kLineSpan + 2, "window loads cover kLineSpan descriptors from an even start");
-constexpr int kWinN = kScanOnly ? 0 : (int)kLineWinLoads;   // window loads per wave and step
+constexpr int kWinN = (kScanOnly && !kScanDma) ? 0 : (int)kLineWinLoads;   // window loads per step (wave 0)
+constexpr int kWinO = kW0Dma ? 0 : kWinN;                                      // (every other wave)
 
 struct LineShared {
   uint16_t ev[kLineSlots][kMapWaves][kLineCap];    // per slot and wave: the range's positions
@@ -2528,7 +2572,7 @@ struct LineShared {
   unsigned long long tot[kLineSlots];              // the group's delimiters
   uint32_t b16[kLineSlots][kMapWaves];             // low 16 bits of the range's first object offset
   uint32_t res[kLineSlots];
-  uint32_t rstep[kLineSlots];                      // the step in which wave 0 set res
+  uint32_t pclaim[kLineSlots];                     // DP_LINE_SHARE: ranges of the slot's step claimed for placement
   uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
   unsigned long long win[kLineWin];                // wave 0: a look-back window's descriptors, by LDS-DMA
   unsigned long long win_dummy[kLineWin];          // every other wave's / step's window loads (never read)
@@ -2673,14 +2717,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t agg_next = 0, res_next = 0, lb_step = 0xFFFFFFFFu;
   uint64_t win_base = 0;
 
-  // phase B of step q for this wave's range
-  // ``list``: also copy the range's LDS list to the output (false: the group run does; see place_group)
-  auto place = [&](uint32_t q, bool list) -> bool {
+  // phase B of range w of step q (its geometry, count and prefix already read from the slot)
+  auto place_v = [&](uint32_t q, uint32_t w, const uint4 gq, const uint32_t cw, const uint64_t Pw) -> bool {
     const uint32_t s = q % kLineSlots;
-    // every LDS read up front (one round trip: the branches below would otherwise serialize them)
-    const uint4 gq = sh.geo[s][wave];
-    const uint32_t cw = sh.cnt[s][wave];
-    const uint64_t Pw = sh.pw[s][wave];
     if (!(gq.z & kLineValid)) return true;
     const uint32_t n = cw & ~kLineDense;
     const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
@@ -2690,8 +2729,8 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       // the FASTA fix-up of phase_b / fasta_place_block with the range's true incoming state: drop a start
       // pending from the previous range, prepend the end of the header pending into it; pairs at 2P - S + i
       typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
-      const uint4 fr = sh.frec[s][wave];
-      const uint32_t S = sh.sw[s][wave];
+      const uint4 fr = sh.frec[s][w];
+      const uint32_t S = sh.sw[s][w];
       const uint32_t cF = fr.x & 0xFFFFu, cT = fr.x >> 16, fn = fr.y & 0xFFFFu, fl = fr.z;
       const uint32_t fV = (fl >> 2) & 1u;
       if (lane == 0) {
@@ -2712,7 +2751,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       const uint32_t m = n - skip + pre;
       const uint64_t b0 = 2 * Pw - S, last = 2 * A.cap - 1;
       const bool near4g = OUT64 == 0 && off0 + kWaveBytes + 1 > 0xFFFFFFFFull;
-      const uint16_t* evw = sh.ev[s][wave];
+      const uint16_t* evw = sh.ev[s][w];
       for (uint32_t i = (uint32_t)lane; i < m; i += kWave) {
         const uint32_t e = (pre && i == 0) ? fn - 1u : (uint32_t)evw[i + skip - pre];
         const uint64_t slot = b0 + i;
@@ -2720,7 +2759,6 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         if (near4g) ovf |= val > 0xFFFFFFFFull;
         put<OutT>(A.out, slot < last ? slot : last, val);
       }
-      (void)list;
       return true;
     } else {
       if (lane == 0) {
@@ -2740,71 +2778,19 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
         return true;
       }
-      if (!list) return true;
-      const uint16_t* evw = sh.ev[s][wave];
+      const uint16_t* evw = sh.ev[s][w];
       // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
       ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
       return true;
     }
   };
-  // (every thread of the workgroup) step q's uint16 index as ONE contiguous run [P_g, P_g + total) (the
-  // best-measured store shape, stream_rw_kernel): thread t stores group entries h + 8t .. h + 8t + 7 as one
-  // aligned 16-byte store, gathering each entry from the LDS list of the range holding it (the largest w with
-  // ex[w] <= e); ranges too dense for LDS are rescanned by their own wave (dense_b) and left out of the run.
-  // Every delimiter an entry (out_mode 3 implies every_k == 1) and the output 16-byte aligned (both checked by the
-  // host); entries at or past the capacity are not stored (the launch then reports DP_ERR_CAPACITY).
-  auto place_group = [&](uint32_t q) {
+  // range w of step q (every LDS read up front: one round trip, the branches would otherwise serialize them)
+  auto place = [&](uint32_t q, uint32_t w) -> bool {
     const uint32_t s = q % kLineSlots;
-    const uint32_t Tg = (uint32_t)sh.tot[s];
-    const uint64_t Pg = sh.pw[s][0];                   // (ex[0] == 0)
-    place(q, false);                                   // this wave's range: its bookkeeping, or its rescan
-#ifdef DP_LINE_NOPLACE
-    return;
-#endif
-    if (Pg >= A.cap) return;
-    const uint32_t T = A.cap - Pg < (uint64_t)Tg ? (uint32_t)(A.cap - Pg) : Tg;
-    uint16_t* o = reinterpret_cast<uint16_t*>(A.out) + Pg;
-    const uint32_t* ex = sh.ex[s];
-    auto find = [&](uint32_t e) {
-      uint32_t w = 0;
-#pragma unroll
-      for (uint32_t st = kMapWaves / 2; st; st >>= 1)
-        if (ex[w + st] <= e) w += st;
-      return w;
-    };
-    auto dense = [&](uint32_t w) { return (sh.cnt[s][w] & kLineDense) != 0u; };
-    auto value = [&](uint32_t e, uint32_t w) { return (uint16_t)(sh.b16[s][w] + sh.ev[s][w][e - ex[w]]); };
-    auto one = [&](uint32_t e) {
-      const uint32_t w = find(e);
-      if (!dense(w)) o[e] = value(e, w);
-    };
-    const uint32_t t = threadIdx.x;
-    const uint32_t hh = (uint32_t)((8u - (uint32_t)(Pg & 7u)) & 7u);
-    const uint32_t h = hh < T ? hh : T;
-    if (t < h) one(t);
-    const uint32_t G8 = (T - h) >> 3;
-    for (uint32_t jg = t; jg < G8; jg += kWave * kMapWaves) {
-      const uint32_t e0 = h + 8u * jg;
-      const uint32_t w0 = find(e0);
-      if (w0 == find(e0 + 7u) && !dense(w0)) {        // the common case: one range's 8 consecutive positions
-        const uint16_t* ev = sh.ev[s][w0] + (e0 - ex[w0]);
-        const uint32_t bb = sh.b16[s][w0];
-        uint32_t wd[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          wd[i] = (uint32_t)(uint16_t)(bb + ev[2 * i]) | ((uint32_t)(uint16_t)(bb + ev[2 * i + 1]) << 16);
-        const v4u pk = {wd[0], wd[1], wd[2], wd[3]};
-#if DP_NTSTORE
-        __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + e0));
-#else
-        *reinterpret_cast<v4u*>(o + e0) = pk;
-#endif
-      } else {
-        for (uint32_t i = 0; i < 8u; ++i) one(e0 + i);
-      }
-    }
-    const uint32_t tail0 = h + 8u * G8;
-    if (t < T - tail0) one(tail0 + t);
+    const uint4 gq = sh.geo[s][w];
+    const uint32_t cw = sh.cnt[s][w];
+    const uint64_t Pw = sh.pw[s][w];
+    return place_v(q, w, gq, cw, Pw);
   };
   // (wave 0) step q's AGG: the group's count (DELIM) or function of the incoming line state (FASTA) from its 16
   // ranges (lanes 0..15), with every range's exclusive prefix
@@ -2867,7 +2853,6 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
     cbar();
     if (lane == 0) {
-      sh.rstep[s] = cur_it;
       lds_st(&sh.res[s], u + 1u);
       st_desc(&A.desc[u], pref | A.epoch);
     }
@@ -2910,24 +2895,55 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       __builtin_amdgcn_s_sleep(1);
     }
   };
-  // (every wave) place steps nb .. q, waiting for their prefixes
-  auto place_upto = [&](uint32_t q) {
-    for (; nb <= q; ++nb) {
-      if (wave == 0) {
-        resolve_upto(nb);
-      } else {
-        const uint32_t want = sh.grp[nb % kLineGrpQ] + 1u;
-        uint64_t t0 = 0;
-        for (uint32_t spins = 0; lds_ld(&sh.res[nb % kLineSlots]) != want; ++spins) {
-          if (wait_expired(spins, t0)) {
-            if (lane == 0) atomicOr(A.err, kErrTimeout);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
+  auto resolved_tag = [&](uint32_t q) { return lds_ld(&sh.res[q % kLineSlots]) == sh.grp[q % kLineGrpQ] + 1u; };
+  // (every wave) block until step q's prefix is known (wave 0 resolves it in the foreground)
+  auto wait_resolved = [&](uint32_t q) {
+    if (wave == 0) {
+      resolve_upto(q);
+    } else {
+      uint64_t t0 = 0;
+      for (uint32_t spins = 0; !resolved_tag(q); ++spins) {
+        if (wait_expired(spins, t0)) {
+          if (lane == 0) atomicOr(A.err, kErrTimeout);
+          break;
         }
-        cbar();
+        __builtin_amdgcn_s_sleep(1);
       }
-      place(nb, true);
+    }
+    cbar();
+  };
+  // (DP_LINE_SHARE) claim and place ranges of the resolved steps nb .. lim - 1, in order, without blocking: a
+  // claim is one LDS add on the slot's counter; a step whose 16 ranges are all claimed is left behind (nb + 1).
+  // A wave places what it claims before it reaches the next barrier, so a step whose ranges are all claimed
+  // before the barrier is placed after it; the slot stall makes every wave see its next slot's old step all
+  // claimed, and the slot's counter is reset after that barrier, so no claim ever reaches a reused slot.
+  auto help = [&](uint32_t lim) {
+    while (nb < lim) {
+      const uint32_t s0 = nb % kLineSlots;
+      if (!resolved_tag(nb)) break;
+      cbar();
+      uint32_t w = 0;
+      if (lane == 0) w = lds_add(&sh.pclaim[s0], 1u);
+      w = rfl(w);
+      if (w >= kMapWaves) {
+        ++nb;
+        continue;
+      }
+      place(nb, w);
+    }
+  };
+  // (every wave) place steps nb .. q, waiting for their prefixes (DP_LINE_SHARE: until all their ranges are claimed)
+  auto place_upto = [&](uint32_t q) {
+    if constexpr (kLineShare) {
+      while (nb <= q) {
+        wait_resolved(nb);
+        help(q + 1u);
+      }
+    } else {
+      for (; nb <= q; ++nb) {
+        wait_resolved(nb);
+        place(nb, (uint32_t)wave);
+      }
     }
   };
 
@@ -2964,12 +2980,13 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
   // (other waves, or no such group) land in a dummy area and are never read.
   auto issue_window = [&]() {
-    if (kScanOnly) return;
-    const bool want = wave == 0 && res_next < agg_next;
-    const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
+    if (kScanOnly && !kScanDma) return;
+    const bool want = wave == 0 && (kScanDma || res_next < agg_next);
+    const uint32_t u = want ? sh.grp[(kScanDma ? cur_it : res_next) % kLineGrpQ] : 0u;
     uint64_t base = 0;
     // a dummy window is lane 0's 16 bytes per load (the count is per instruction, the bytes per active lane)
-    if (want || lane == 0 || DP_LINE_DUMMY) base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
+    if ((!kW0Dma || wave == 0) && (want || lane == 0 || DP_LINE_DUMMY))
+      base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
     if (want) {
       win_base = base;
       lb_step = res_next;
@@ -2981,17 +2998,8 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   for (;; ++it) {
     __syncthreads();
     cur_it = it;
-#if DP_LINE_GROUP
-    // the group runs need every thread: the steps placed at the end of this step are decided here by every wave
-    // alike (resolved in an earlier step, which the barrier above published), in order, at most two.  (This
-    // places a step a step later than the per-wave check below: 951 vs 849 us per 4 GiB CSV, its slots fill.)
-    uint32_t nplace = 0;
-    for (uint32_t i = 0; i < 2u && nb + i < it; ++i) {
-      const uint32_t q = nb + i, s_ = q % kLineSlots;
-      if (sh.res[s_] != sh.grp[q % kLineGrpQ] + 1u || sh.rstep[s_] >= it) break;
-      ++nplace;
-    }
-#endif
+    LTL(it, 0);
+    if (kLineShare && threadIdx.x == 0) sh.pclaim[it % kLineSlots] = 0u;   // its old step: placed (last stall)
     const uint32_t gnext = sh.grp[(it + 1) % kLineGrpQ];
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
     const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD &&
@@ -3024,9 +3032,10 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     };
     // ---- buffer 0
     // the youngest operations in flight: b[1]'s loads (and, kLineLate, the window issued after them)
-    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsX + (kLineLate ? kWinN : 0)) : "memory");
+    vm_wait2<kLoadsX + (kLineLate ? kWinN : 0), kLoadsX + (kLineLate ? kWinO : 0)>(wave == 0);
     touch_bufx(b[0]);
     __builtin_amdgcn_sched_barrier(0);
+    LTL(it, 1);
     if (do_claim) {
       claim_res = atomic_add_nowait(ticket, run);
       pend = run;
@@ -3038,18 +3047,24 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       if (kPubWave != 0) agg_next = it;                // published by wave kPubWave in this step
     }
     if (!kScanOnly && kPubWave != 0 && wave == kPubWave && it > 0) publish_agg(it - 1);
+    LTL(it, 2);
     rows(0);
     load_bufx(b[0], A, gn, lane, 0);
     // Every wave issues the window's kLineWinLoads LDS-DMA loads every step, so the wait below has one count on
     // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
     // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
     // (other waves, or no such group) land in a dummy area and are never read.
-    if (!kLineLate) issue_window();
+    if (kLineLate == 0) issue_window();
+    if (kLineLate == 2) {                             // in flight: b[1]'s loads, the claim, b[0]'s reload
+      asm volatile("s_waitcnt vmcnt(%0)" :: "i"(2 * kLoadsX) : "memory");
+      if (!kScanOnly && wave == 0) consume();
+    }
     // ---- buffer 1
-    asm volatile("s_waitcnt vmcnt(%0)" :: "i"(kLoadsX + (kLineLate ? 0 : kWinN)) : "memory");   // b[0] (+ window) in flight
+    LTL(it, 3);
+    vm_wait2<kLoadsX + (kLineLate ? 0 : kWinN), kLoadsX + (kLineLate ? 0 : kWinO)>(wave == 0);   // b[0] (+ window) in flight
     touch_bufx(b[1]);
     __builtin_amdgcn_sched_barrier(0);
-    if (kLineLate && !kScanOnly && wave == 0) consume();   // issued at the end of the last step, before b[0]'s reload
+    if (kLineLate == 1 && !kScanOnly && wave == 0) consume();   // issued at the end of the last step, before b[0]'s reload
     if (pend) {                                       // the wait above covered the claim: its value is back
       asm volatile("" : "+v"(claim_res) :: "memory");
       const uint32_t u = rfl(claim_res);
@@ -3058,6 +3073,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       claimed += pend;
       pend = 0;
     }
+    LTL(it, 4);
     rows(1);
     cbar();
     if (lane == 0) {
@@ -3079,27 +3095,31 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         sh.b16[slot][wave] = (uint32_t)(A.obj_base - A.shift + g.ubase) & 0xFFFFu;
       }
     }
-    // this step's placements (decided at its start); then, if the next step's slot still holds an unplaced
-    // step, block for it here (only b[0]'s loads in flight, so the registers are free).  Blocking holds back
-    // this workgroup's AGG of step it, its newest group, while it waits for an older one: the lowest waiting
-    // group never depends on a held AGG.
-#if DP_LINE_GROUP
-    for (uint32_t i = 0; i < nplace; ++i, ++nb) {
-      if constexpr (!kFa && OUT64 == 2) place_group(nb);
-      else place(nb, true);
+    // this step's placements: the ranges of every older step whose prefix is known (DP_LINE_SHARE: any of
+    // them, claimed, so the waves that finish their rows first place most of them; else this wave's own, in
+    // order); then, if the next step's slot still holds an unplaced step, block for it here (only b[0]'s loads
+    // in flight, so the registers are free).  Blocking holds back this workgroup's AGG of step it, its newest
+    // group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+    LTL(it, 5);
+    if (kLineB1Early) load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
+    if constexpr (kLineShare) {
+      if (!kScanOnly) help(it);
+    } else {
+      while (!kScanOnly && nb < it) {
+        if (!resolved_tag(nb)) break;
+        cbar();
+        place(nb, (uint32_t)wave);
+        ++nb;
+      }
     }
-#else
-    // every older step whose prefix is known, as soon as this wave sees it (wave-local order)
-    while (!kScanOnly && nb < it) {
-      if (lds_ld(&sh.res[nb % kLineSlots]) != sh.grp[nb % kLineGrpQ] + 1u) break;
-      cbar();
-      place(nb, true);
-      ++nb;
-    }
-#endif
+    LTL(it, 6);
+#ifndef DP_LINE_NOSTALL   // (DP_LINE_NOSTALL: timing probe only, wrong results: never block for a slot)
     if (!kScanOnly && nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
-    load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
-    if (kLineLate) issue_window();
+#endif
+    if (kLineLate == 2) issue_window();
+    if (!kLineB1Early) load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
+    if (kLineLate == 1) issue_window();
+    LTL(it, 7);
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
@@ -3107,6 +3127,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   drain_bufsx(b);                                     // (and a look-back window still in flight)
   if (wave == 0) lb_step = 0xFFFFFFFFu;
   __syncthreads();                                    // every wave's last summary is in LDS
+  LTL(it + 1, 0);
   if (kScanOnly) return;
   if (wave == kPubWave) publish_agg(it);
   if (kPubWave != 0) {
@@ -3114,6 +3135,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     if (wave == 0) agg_next = it + 1;
   }
   place_upto(it);
+  LTL(it + 1, 1);
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
 
@@ -4351,8 +4373,7 @@ int dp_timing_read(dp_ctx* c, double* total_ms, uint64_t* launches) {
 int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slots, int* waves) {
 #ifdef DP_STAMPS
   if (!c || !host_words) return fail(DP_ERR_INVALID, "dp_debug_profile: null argument");
-  const uint64_t n = n_words < (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots ? n_words
-                                                                                 : (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;
+  const uint64_t n = n_words < kProfWords ? n_words : kProfWords;
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipStreamSynchronize(c->stream));
   HIPCHK(hipMemcpyFromSymbol(host_words, HIP_SYMBOL(g_prof), n * 8, 0, hipMemcpyDeviceToHost));
