@@ -705,6 +705,11 @@ __device__ __forceinline__ void drain_bufs(Buf (&b)[kBufs]) {
 
 // The same buffers without the lookahead dword (a FASTA row needs the byte after it; a delimiter row does not):
 // kRows loads per buffer, 2 VGPRs fewer per wave (line_kernel runs at the 128-VGPR limit).
+// the map kernel's input buffers: DP_MAP_BUFN 1 = BufN (no lookahead dword load; FASTA reads it by a scalar
+// load), 0 = Buf (the lookahead dword as a ninth vector load per buffer)
+#ifndef DP_MAP_BUFN
+#define DP_MAP_BUFN 1
+#endif
 struct BufN {
   v4u x[kRows];
 };
@@ -731,6 +736,33 @@ __device__ __forceinline__ void drain_bufs_n(BufN (&b)[kBufs]) {
   for (int h = 0; h < kBufs; ++h) touch_buf_n(b[h]);
   __builtin_amdgcn_sched_barrier(0);
 }
+// Buffers of the lockstep kernels, either kind (BufN: no lookahead dword in flight; FASTA reads it by a scalar load).
+__device__ __forceinline__ void load_bufx(BufN& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf_n(b, A, g, lane, h); }
+__device__ __forceinline__ void wait_bufx(BufN& b) { wait_buf_n(b); }
+__device__ __forceinline__ void touch_bufx(BufN& b) { touch_buf_n(b); }
+__device__ __forceinline__ void drain_bufsx(BufN (&b)[kBufs]) { drain_bufs_n(b); }
+__device__ __forceinline__ void load_bufx(Buf& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf(b, A, g, 0, lane, h); }
+__device__ __forceinline__ void wait_bufx(Buf& b) { wait_buf(b); }
+__device__ __forceinline__ void touch_bufx(Buf& b) { touch_buf(b); }
+__device__ __forceinline__ void drain_bufsx(Buf (&b)[kBufs]) { drain_bufs(b); }
+typedef __attribute__((address_space(4))) const uint32_t cu32s;   // constant address space: s_load_dword
+// the first dword after buffer h of a wave range (FASTA's next-byte lookahead) by a scalar load through the
+// constant address space (it waits on lgkmcnt, never on the hand-counted vmcnt); read only where that byte lies
+// inside the chunk, the range's own first dword elsewhere (always in the buffer)
+__device__ __forceinline__ uint32_t lookahead_s(const uint8_t* base, const Geo& g, int h, bool interior, int hi) {
+  const bool inb = interior || (h + 1) * kBufBytes < hi;
+  const uint64_t at = g.ubase + (inb ? (uint64_t)(h + 1) * kBufBytes : 0ull);
+  return *(cu32s*)(uintptr_t)(base + at);
+}
+__device__ __forceinline__ uint32_t lookahead(const Buf& b, const uint8_t*, const Geo&, int, bool, int) { return b.la; }
+__device__ __forceinline__ uint32_t lookahead(const BufN&, const uint8_t* base, const Geo& g, int h, bool interior, int hi) {
+  return lookahead_s(base, g, h, interior, hi);
+}
+#if DP_MAP_BUFN
+typedef BufN MapBuf;
+#else
+typedef Buf MapBuf;
+#endif
 
 // ------------------------------------------------------------------------------------------ LDS state
 struct WaveRec {                   // one data wave's phase-A result for one unit (written by its lane 0)
@@ -1781,9 +1813,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
 #endif
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
-  Buf b[kBufs];
+  MapBuf b[kBufs];
 #pragma unroll
-  for (int h = 0; h < kBufs; ++h) load_buf(b[h], ScanArgs{M.base}, g, 0, lane, h);
+  for (int h = 0; h < kBufs; ++h) load_bufx(b[h], ScanArgs{M.base}, g, lane, h);
 #if DP_MAP_SYNC == 2 && !DP_MAP_DYN
   // soft lockstep: a wave starts step it only once every wave of the workgroup has finished step
   // it - DP_MAP_LEAD - 1 (monotonic per-slot completion counts, no reset), and trails-the-front issue priority
@@ -1835,7 +1867,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     const uint32_t key = M.delim ^ kSel12;
 #pragma unroll
     for (int h = 0; h < kBufs; ++h) {
-      wait_buf(b[h]);                                 // this buffer landed; the other stays in flight
+      wait_bufx(b[h]);                                // this buffer landed; the other stays in flight
 #if DP_MAP_DYN
       if (h == 0 && do_claim) {                       // the youngest vector-memory operation until the next wait
         claim_res = atomic_add_nowait(M.ticket, run);
@@ -1855,8 +1887,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
       for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
       if constexpr (MODE == kFasta) {
 #ifndef DP_MAP_NOSCAN
-        if (interior) fasta_rows<true>(x, b[h].la, h, lo, hi, lane, st, keep);
-        else fasta_rows<false>(x, b[h].la, h, lo, hi, lane, st, keep);
+        const uint32_t la = lookahead(b[h], M.base, g, h, interior, hi);
+        if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
+        else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
 #else
         // timing probe (wrong results): the map's loads, barriers, claims and stores without the row scan
         uint32_t xs = 0;
@@ -1868,7 +1901,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         if (interior) delim_rows<true>(x, h, lo, hi, key, lane, st.nev, keep);
         else delim_rows<false>(x, h, lo, hi, key, lane, st.nev, keep);
       }
-      if (h + 1 < kBufs) load_buf(b[h], ScanArgs{M.base}, gn, 0, lane, h);
+      if (h + 1 < kBufs) load_bufx(b[h], ScanArgs{M.base}, gn, lane, h);
     }
     const bool dense = st.nev > kSpillCap;
     const uint32_t n = dense ? 0u : st.nev;
@@ -1901,7 +1934,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
       }
     }
-    load_buf(b[kBufs - 1], ScanArgs{M.base}, gn, 0, lane, kBufs - 1);
+    load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
 #ifdef DP_STAMPS
     n_done += (g.fl & kGeoValid) ? 1u : 0u;
 #endif
@@ -1918,7 +1951,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     r = rn;
     g = gn;
   }
-  drain_bufs(b);
+  drain_bufsx(b);
 #ifdef DP_STAMPS
   // per wave: start and end (100 MHz realtime clock), ranges scanned, the XCC it ran on
   if (lane == 0 && blockIdx.x < kProfMaxGrid) {
@@ -2535,7 +2568,7 @@ constexpr int kLineLate = DP_LINE_LATE;
 static_assert(kLineLate >= 0 && kLineLate <= 2, "DP_LINE_LATE");
 constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
 constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
-static_assert(kLineSlots >= 3 && kLineSlots <= 6, "line slots: phase A, resolution, placement + slack");
+static_assert(kLineSlots >= 3 && kLineSlots <= 8, "line slots: phase A, resolution, placement + slack");
 static_assert(kLineCap % 8 == 0 && kLineCap <= 1024, "line cap");
 #ifndef DP_LINE_RUN        // consecutive groups per claim (one returning atomic on one address each)
 #define DP_LINE_RUN 1
@@ -2637,18 +2670,6 @@ __device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, u
   return lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P, all);
 }
 
-// Buffers of the lockstep kernels (BufN: no lookahead dword in flight; FASTA reads it by a scalar load).
-__device__ __forceinline__ void load_bufx(BufN& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf_n(b, A, g, lane, h); }
-__device__ __forceinline__ void wait_bufx(BufN& b) { wait_buf_n(b); }
-__device__ __forceinline__ void touch_bufx(BufN& b) { touch_buf_n(b); }
-__device__ __forceinline__ void drain_bufsx(BufN (&b)[kBufs]) { drain_bufs_n(b); }
-#if DP_LINE_LA
-__device__ __forceinline__ void load_bufx(Buf& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf(b, A, g, 0, lane, h); }
-__device__ __forceinline__ void wait_bufx(Buf& b) { wait_buf(b); }
-__device__ __forceinline__ void touch_bufx(Buf& b) { touch_buf(b); }
-__device__ __forceinline__ void drain_bufsx(Buf (&b)[kBufs]) { drain_bufs(b); }
-#endif
-typedef __attribute__((address_space(4))) const uint32_t cu32s;   // constant address space: s_load_dword
 
 // A window of FASTA group functions: the prefix count P and line state S entering group u, once resolvable.
 __device__ __forceinline__ bool lb_func_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P,
@@ -3020,9 +3041,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         // the first dword after this buffer (a scalar load through the constant address space: it waits on
         // lgkmcnt, never on the hand-counted vmcnt); read only where that byte lies inside the chunk, the
         // range's own first dword elsewhere (always in the buffer)
-        const bool inb = interior || (h + 1) * kBufBytes < hi;
-        const uint64_t la_at = g.ubase + (inb ? (uint64_t)(h + 1) * kBufBytes : 0ull);
-        const uint32_t la = *(cu32s*)(uintptr_t)(A.base + la_at);
+        const uint32_t la = lookahead_s(A.base, g, h, interior, hi);
         if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
         else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
       } else {
