@@ -2522,11 +2522,12 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 #endif
 constexpr int kPubWave = DP_LINE_PUBW;
 constexpr bool kLineShare = DP_LINE_SHARE != 0;
-// DP_LINE_B1EARLY (A/B): b[1]'s reload before the step's placements instead of after them; the placement stores
-// are then younger than it, so the next step's first wait also waits for as many of b[1]'s loads (correct, slower
-// the more stores a step has)
+// DP_LINE_B1EARLY 1: b[1]'s reload before the step's placements instead of after them, so the placements run
+// with both buffers in flight; the placement stores are then younger than it, so the next step's first wait also
+// waits for as many of b[1]'s loads (a conservative wait).  With DP_LINE_W0DMA: CSV / VCF 1-4 GiB 1.6-2.1 %
+// faster, a sparse index ('>' in FASTA bytes, uint64) 1-3.7 % slower (profiles/r04/ab/w0b1)
 #ifndef DP_LINE_B1EARLY
-#define DP_LINE_B1EARLY 0
+#define DP_LINE_B1EARLY 1
 #endif
 constexpr bool kLineB1Early = DP_LINE_B1EARLY != 0;
 // timing probe only (wrong results): the lockstep scan and its LDS records without any look-back, publication,
@@ -2538,8 +2539,9 @@ constexpr bool kScanDma = DP_LINE_SCANONLY == 2;    // (2: with the look-back wi
 constexpr bool kScanOnly = false;
 constexpr bool kScanDma = false;
 #endif
-#ifndef DP_LINE_W0DMA      // 1: only wave 0 issues window loads (every other wave's waits count none)
-#define DP_LINE_W0DMA 0
+#ifndef DP_LINE_W0DMA      // 1: only wave 0 issues window loads (every other wave's waits count none: one wait per
+                           // wave role, in uniform branches; 0: every wave issues them, lane 0 only but wave 0)
+#define DP_LINE_W0DMA 1
 #endif
 constexpr bool kW0Dma = DP_LINE_W0DMA != 0;
 #ifdef DP_LTL
@@ -2566,6 +2568,8 @@ __device__ __forceinline__ void vm_wait2(bool first) {
 // wait for the window alone (b[1]'s loads may still be in flight: the reduction overlaps them)
 constexpr int kLineLate = DP_LINE_LATE;
 static_assert(kLineLate >= 0 && kLineLate <= 2, "DP_LINE_LATE");
+static_assert(!(kLineB1Early && kLineLate == 2), "DP_LINE_LATE=2 reduces the window at a wait that counts on the window "
+                                                 "being older than b[1]'s reload");
 constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
 constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
 static_assert(kLineSlots >= 3 && kLineSlots <= 8, "line slots: phase A, resolution, placement + slack");
