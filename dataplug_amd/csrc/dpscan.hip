@@ -710,6 +710,9 @@ __device__ __forceinline__ void drain_bufs(Buf (&b)[kBufs]) {
 #ifndef DP_MAP_BUFN
 #define DP_MAP_BUFN 1
 #endif
+#ifndef DP_MAP_B1EARLY     // A/B: the map kernel's last buffer reloaded before the range's stores (see map_kernel)
+#define DP_MAP_B1EARLY 0
+#endif
 struct BufN {
   v4u x[kRows];
 };
@@ -1905,6 +1908,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     }
     const bool dense = st.nev > kSpillCap;
     const uint32_t n = dense ? 0u : st.nev;
+    // DP_MAP_B1EARLY: the last buffer's reload before the range's record and spill stores (the next step's first
+    // wait then also waits for as many of its loads as there were stores: conservative)
+    if (DP_MAP_B1EARLY) load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
     cbar();
     if constexpr (MODE == kFasta) {
       // the range's summary (phase_a_rec of a one-range unit) and its events, word-major
@@ -1934,7 +1940,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
       }
     }
-    load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
+    if (!DP_MAP_B1EARLY) load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
 #ifdef DP_STAMPS
     n_done += (g.fl & kGeoValid) ? 1u : 0u;
 #endif
@@ -2486,12 +2492,14 @@ __global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlac
 // spilling them to HBM, and places them itself once the group's prefix is known:
 //   * step k: phase A of group g_k -> LDS slot k % kLineSlots (positions, count, geometry per wave);
 //   * step k + 1: wave 0 publishes g_k's delimiter count as an AGG descriptor right after the barrier (every
-//     wave wrote its count before it), then resolves g_k's prefix by a decoupled look-back over the group
-//     descriptors with hand-waited loads: issued after one buffer wait, reduced after the next (no stall);
-//     a resolved group gets its PREFIX descriptor and its LDS slot's `res` tag;
-//   * the step after: every wave copies its range's positions to their final index (place_delims).
-// A wave only blocks when the slot it is about to overwrite is still unplaced (its group's predecessors
-// are late); wave 0 then resolves in the foreground.  No spill round trip (the two-kernel form moves every
+//     wave wrote its count before it), and at the step's end loads the look-back window of its oldest
+//     unresolved group (512 group descriptors, by LDS-DMA: no VGPR held in flight);
+//   * step k + 2: wave 0 reduces that window after its second buffer wait (no stall); a resolved group gets its
+//     PREFIX descriptor, every range's launch prefix in LDS and the slot's `res` tag; after their rows, the
+//     waves claim the resolved step's 16 ranges from an LDS counter and copy each range's positions to their
+//     final index (place_delims), so the waves that finish first place most of them.
+// A wave only blocks when the slot it is about to overwrite still holds unclaimed ranges (its group's
+// predecessors are late); wave 0 then resolves in the foreground.  No spill round trip (the two-kernel form moves every
 // delimiter through HBM twice more), no coordinator wave and no placement launch (the one-pass look-back
 // kernel's start and tail).  Deadlock-free: a workgroup publishes the AGG of every group it has scanned before
 // it blocks, groups are claimed in increasing order by running workgroups, and a group's prefix depends only
@@ -2972,10 +2980,12 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
   };
 
-  // Vector-memory order per step (vmcnt counts in issue order): [b1 reload of the previous step] | wait b0 |
-  // claim atomic, wave 0's descriptor stores | b0 reload | wave 0's look-back window (LDS-DMA: no VGPRs held) |
-  // wait b1 (the b0 reload and the window may stay in flight) | phase-B stores | b1 reload | barrier | wait b0:
-  // the window has landed.  So the look-back travels for a whole step and no wait covers a load just issued.
+  // Vector-memory order per step (vmcnt counts in issue order; shipped knobs DP_LINE_LATE=1, B1EARLY, W0DMA):
+  // [b1 reload, placement stores, wave 0's window loads of the last step] | barrier | wait b0 (b1, those stores
+  // and the window may stay in flight: a conservative count when there were stores) | claim atomic, wave 0's
+  // AGG store | rows(0) | b0 reload | wait b1 (only b0's reload in flight: the claim and the window have landed)
+  // | window reduction (wave 0) | rows(1) | b1 reload | placements | window loads (wave 0).  So a window travels
+  // for half a step and no wait covers a load just issued.
   // (wave 0) reduce the look-back window that has landed (lb_step: the step of its group)
   auto consume = [&]() {
     if (lb_step == 0xFFFFFFFFu) return;
@@ -3000,10 +3010,11 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
     if (ok) resolved(q, P, S);
   };
-  // Every wave issues the window's kLineWinLoads LDS-DMA loads once per step, so the waits have one count on
-  // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
-  // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
-  // (other waves, or no such group) land in a dummy area and are never read.
+  // Wave 0 (every wave with DP_LINE_W0DMA=0) issues the window's kLineWinLoads LDS-DMA loads once per step, so
+  // its waits have one count on every path (a count per path inside one branch made the compiler merge b[1]'s
+  // registers through copies above the wait; one count per wave role, in uniform branches, does not).  Only the
+  // window of wave 0's oldest unresolved group with a published AGG is read; the other loads (no such group, or
+  // the other waves) land in a dummy area and are never read.
   auto issue_window = [&]() {
     if (kScanOnly && !kScanDma) return;
     const bool want = wave == 0 && (kScanDma || res_next < agg_next);
@@ -3073,10 +3084,6 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     LTL(it, 2);
     rows(0);
     load_bufx(b[0], A, gn, lane, 0);
-    // Every wave issues the window's kLineWinLoads LDS-DMA loads every step, so the wait below has one count on
-    // every path (a count per path made the compiler merge b[1]'s registers through copies above the wait).
-    // Only wave 0's window of its oldest unresolved group with a published AGG is read; the other loads
-    // (other waves, or no such group) land in a dummy area and are never read.
     if (kLineLate == 0) issue_window();
     if (kLineLate == 2) {                             // in flight: b[1]'s loads, the claim, b[0]'s reload
       asm volatile("s_waitcnt vmcnt(%0)" :: "i"(2 * kLoadsX) : "memory");
@@ -3120,9 +3127,9 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
     // this step's placements: the ranges of every older step whose prefix is known (DP_LINE_SHARE: any of
     // them, claimed, so the waves that finish their rows first place most of them; else this wave's own, in
-    // order); then, if the next step's slot still holds an unplaced step, block for it here (only b[0]'s loads
-    // in flight, so the registers are free).  Blocking holds back this workgroup's AGG of step it, its newest
-    // group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+    // order); then, if the next step's slot still holds an unclaimed range, block for it here (a claimed range is
+    // placed before its wave reaches the next barrier).  Blocking holds back this workgroup's AGG of step it, its
+    // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
     LTL(it, 5);
     if (kLineB1Early) load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
     if constexpr (kLineShare) {
