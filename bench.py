@@ -22,8 +22,8 @@ Workloads (synthetic bytes of the named shapes, resident in HBM before any timed
 One step = on every GPU, one scan call over its bytes: FASTA = dp_fasta_index_async + dp_fasta_result (the
 chunk-table check, the two scan kernels -- map_kernel<FASTA> over 16 KiB ranges, then fasta_place_kernel --,
 the split-header resolve kernel, the read-back of count / pending / chunk ends); newline = dp_delim_ranges
-(one launch: the lockstep line_kernel up to 2 GiB, the one-pass look-back scan_kernel above, dp_scan_delim_form;
-the kernel that ran is named in each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
+(one launch: the lockstep line_kernel up to 2 GiB and above it for CSV-dense input, the one-pass look-back
+scan_kernel otherwise, dp_scan_delim_form; the kernel that ran is named in each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
 rate is DESIGN.md §6).  Steps
 alternate between two contexts and step k + 1 is enqueued before step k's result is collected; the library
 runs one scan at a time per GPU (its scan stream), so ``value`` is this pipelined rate provided
@@ -734,10 +734,12 @@ def delim_worker(args, team, leg, k, world, dev):
     def collect(i):
         return ctxs[i % 2].delim_ranges_result(nr)
 
-    kernel = ScanContext.DELIM_FORMS[ctxs[0].delim_form(nbytes)]
     S = Steps(team, ctxs, launch, collect)
     team.barrier()
     S.warm(args.warmup)
+    # the kernel the timed launches take (above 2 GiB it follows each context's previous launch's delimiter
+    # density, dp_scan_delim_form: known after the warm-up)
+    kernel = " / ".join(ScanContext.DELIM_FORMS[f] for f in sorted({c.delim_form(nbytes) for c in ctxs}))
     dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
     dt, _, _ = S.timed(args.steps)                                         # serialized (secondary)
     dt_ov, _, (n_out, _, ends) = S.timed(args.steps, serialize=False)      # pipelined (`value`), verified

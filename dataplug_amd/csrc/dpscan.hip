@@ -3358,6 +3358,14 @@ constexpr uint64_t kDelimTwoPassMax = 512ull << 20;
 // group look-back chain per round) where the one-pass kernel streams at 5.3-5.9: at 4 GiB 830-906 vs 765-877 us
 // depending on the box, at 16 GiB CSV 3,607 vs 3,401 us, at 32 GiB 7,082 vs 5,855 us.
 constexpr uint64_t kDelimLineMax = 2ull << 30;
+// Above kDelimLineMax the choice follows the delimiter density of the ctx's previous newline launch (round 4, final
+// kernels, bench sizes, same box: CSV (~28 newlines per KiB) 32 GiB line 5,755 vs one-pass 5,896 us; VCF (~12.5 per
+// KiB) 64 GiB line 11,326 vs one-pass 10,838 us, profiles/r04/ab/form_bench2).  Both kernels couple a workgroup's
+// progress to its predecessors' counts through the look-back; the one-pass kernel buffers up to 16 units and
+// 4,096 positions per wave, so its slack shrinks as the density grows, while line_kernel's 4 slots of 640
+// positions per range hold 4 steps at any density: dense input runs line_kernel at every size.  A ctx's first
+// launch (no density yet) takes the one-pass kernel above kDelimLineMax.
+constexpr uint64_t kLineDenseMilli = 20000;     // delimiters per KiB x 1000
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -3412,6 +3420,9 @@ struct dp_ctx {
                                       // above; 0 round 3's rule (two kernels up to kDelimTwoPassMax, one-pass above);
                                       // 1 line_kernel, 2 two kernels, 3 one-pass at every size
   uint32_t line_launches = 0;         // line_kernel launches (ticket parity)
+  uint64_t delim_line_max = kDelimLineMax;   // DP_DELIM_LINE_MAX (tests): the hybrid form's size split
+  uint64_t delim_density_milli = 0;   // delimiters per KiB x 1000 of the last newline launch (0: none yet)
+  uint64_t delim_span = 0;            // bytes scanned by the newline launch in flight
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
   uint64_t nchunks = 0, cap = 0;
@@ -3433,6 +3444,18 @@ struct dp_ctx {
 };
 
 std::atomic<uint64_t> g_dev_allocs{0}, g_host_allocs{0};
+
+// The newline kernels for a launch scanning `span` bytes (1 line_kernel, 2 two kernels, 3 one-pass; see
+// kDelimLineMax and kLineDenseMilli for the default's rule)
+static int delim_form_for(const dp_ctx* c, uint64_t span) {
+  switch (c->delim_form) {
+    case 1: return 1;
+    case 2: return 2;
+    case 3: return 3;
+    case 0: return span <= c->delim_twopass_max ? 2 : 3;
+    default: return (span <= c->delim_line_max || c->delim_density_milli >= kLineDenseMilli) ? 1 : 3;
+  }
+}
 
 namespace {
 
@@ -4004,6 +4027,8 @@ int dp_ctx_create(int device, dp_ctx** out) {
   const char* form = getenv("DP_DELIM_FORM");
   c->delim_form = !form ? 4 : !strcmp(form, "line") ? 1 : !strcmp(form, "auto") ? 0 : !strcmp(form, "two") ? 2
                 : !strcmp(form, "one") ? 3 : 4;
+  const char* lmax = getenv("DP_DELIM_LINE_MAX");    // the hybrid form's size split (tests)
+  if (lmax) c->delim_line_max = strtoull(lmax, nullptr, 10);
   *out = c;
   return DP_OK;
 }
@@ -4247,13 +4272,14 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   uint64_t units = 0, span = 0;
   for (uint64_t i = 0; i < nr; ++i) span += rg[2 * i + 1] - rg[2 * i];
   const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
-  const bool line = c->delim_form == 1 || (c->delim_form == 4 && span <= kDelimLineMax);
-  if (line) {                                         // the lockstep one-pass kernel
+  const int dform = delim_form_for(c, span);
+  c->delim_span = span;
+  if (dform == 1) {                                   // the lockstep one-pass kernel
     rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
     if (rc) return rc;
     rc = launch_line(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
                      out_mode == 2, tab, j0, ntab);
-  } else if (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) {   // two kernels
+  } else if (dform == 2) {                            // two kernels
     rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
     if (rc) return rc;
     rc = launch_delim2(c, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
@@ -4292,6 +4318,7 @@ int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint6
     if (range_end) range_end[c->range_map.empty() ? i : c->range_map[i]] = nd;
   }
   const uint64_t nout = (carry + nd) / k - carry / k;
+  if (c->delim_span) c->delim_density_milli = (nd * 1024000ull) / c->delim_span;
   if (n_delims) *n_delims = nd;
   if (n_out) *n_out = nout;
   if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out");
@@ -4431,8 +4458,7 @@ int dp_scan_forms(dp_ctx* c, int* fasta_two_kernel, uint64_t* delim_two_kernel_m
 
 int dp_scan_delim_form(dp_ctx* c, uint64_t span, int* form) {
   if (!c || !form) return fail(DP_ERR_INVALID, "null");
-  *form = (c->delim_form == 1 || (c->delim_form == 4 && span <= kDelimLineMax)) ? 1
-          : (c->delim_form == 2 || (c->delim_form == 0 && span <= c->delim_twopass_max)) ? 2 : 3;
+  *form = delim_form_for(c, span);
   return DP_OK;
 }
 

@@ -165,10 +165,12 @@ int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
  * look-back kernel, DP_FASTA_ONEPASS=1), and the largest newline launch (bytes scanned) that runs as two
  * kernels -- larger ones run the one-pass kernel (default 512 MiB; DP_DELIM_TWOPASS_MAX sets it). */
 int dp_scan_forms(dp_ctx* ctx, int* fasta_two_kernel, uint64_t* delim_two_kernel_max);
-/* The kernels a newline launch scanning `span` bytes takes on this ctx: 1 = line_kernel (lockstep one pass),
- * 2 = map + placement kernels, 3 = the one-pass look-back kernel.  Default: line_kernel up to 2 GiB per launch,
- * the one-pass kernel above (DP_DELIM_FORM = hybrid | line | auto | two | one; auto: round 3's rule, two kernels
- * up to delim_two_kernel_max bytes, one-pass above). */
+/* The kernels the ctx's next newline launch scanning `span` bytes takes: 1 = line_kernel (lockstep one pass),
+ * 2 = map + placement kernels, 3 = the one-pass look-back kernel.  Default: line_kernel up to 2 GiB per launch
+ * (DP_DELIM_LINE_MAX sets the split), and above it too when the ctx's previous newline launch had at least 20
+ * delimiters per KiB (CSV-like density); otherwise the one-pass kernel above 2 GiB.  DP_DELIM_FORM = hybrid |
+ * line | auto | two | one overrides (auto: round 3's rule, two kernels up to delim_two_kernel_max bytes, one-pass
+ * above).  Every form writes the same output. */
 int dp_scan_delim_form(dp_ctx* ctx, uint64_t span, int* form);
 
 /* Launch geometry (for tests/tuning): workgroups of the persistent scan grid, and unit size in bytes. */

@@ -595,3 +595,34 @@ def test_forms_alternate_on_one_context():
                 assert (pending == -1).all() and np.array_equal(pairs.astype(np.uint64), fexp)
     finally:
         c.close()
+
+
+@pytest.mark.gpu
+def test_form_follows_delimiter_density():
+    """Above the hybrid form's size split a newline launch takes line_kernel when the context's previous launch
+    was CSV-dense (>= 20 delimiters per KiB), else the one-pass kernel (dp_scan_delim_form); a context's first
+    launch has no density yet.  Every launch, whichever kernel, equals the oracle (the split set to 1 MiB so
+    small launches exercise both sides)."""
+    from dataplug_amd.scan import ScanContext
+    os.environ["DP_DELIM_LINE_MAX"] = str(1 << 20)
+    try:
+        c = ScanContext(0)
+    finally:
+        del os.environ["DP_DELIM_LINE_MAX"]
+    try:
+        objs = {"csv": synth.csv((5 << 20) + 77, seed=12), "vcf": synth.vcf((5 << 20) + 91, seed=13)}
+        dens = {k: len(dpref.delim(a, 0, len(a))[0]) * 1024 / len(a) for k, a in objs.items()}
+        assert dens["csv"] >= 20 > dens["vcf"], dens
+        span = 4 << 20
+        assert c.delim_form(span) == 3 and c.delim_form(1 << 20) == 1      # no density yet
+        for name, want_next in (("csv", 1), ("csv", 1), ("vcf", 3), ("vcf", 3), ("csv", 1)):
+            a = objs[name]
+            n = len(a)
+            d = c.workspace("t_" + name, n + 64)
+            c.h2d(d.ptr, a)
+            ran = c.delim_form(n)
+            r = c.delim_ranges(d.ptr, n, 0, [(0, n)], out_mode=1)
+            assert np.array_equal(r[0], dpref.delim(a, 0, n)[0]), (name, ran)
+            assert c.delim_form(span) == want_next, (name, ran)
+    finally:
+        c.close()
