@@ -713,6 +713,14 @@ __device__ __forceinline__ void drain_bufs(Buf (&b)[kBufs]) {
 #ifndef DP_MAP_B1EARLY     // A/B: the map kernel's last buffer reloaded before the range's stores (see map_kernel)
 #define DP_MAP_B1EARLY 0
 #endif
+#ifndef DP_FASTA_REC16     // FASTA range records of 16 bytes (1: the placement derives the range's geometry from the
+#define DP_FASTA_REC16 1   // chunk table) or 32 (0: summary + geometry).  The map kernel's record and spill stores cost
+#endif                     // ~21 and ~26 us per 4 GiB (timing probes without them), far above their bytes' share
+                           // of the bus: halving the records measured 657-660 vs 667-670 us (profiles/r04/ab/rec16)
+constexpr bool kRec16 = DP_FASTA_REC16 != 0;
+#ifndef DP_MAP_BATCHREC    // FASTA map kernel: a group's 16 range records and spill words stored by one wave (1), or
+#define DP_MAP_BATCHREC 0  // each range's by its own wave (0)
+#endif
 struct BufN {
   v4u x[kRows];
 };
@@ -1705,6 +1713,9 @@ struct MapArgs {
   unsigned int* ticket;        // (DP_MAP_DYN) next group to claim; zeroed by the placement kernel
   unsigned int* place_ticket;  // [2] the placement kernel's block ticket, zeroed here
   uint32_t delim;              // DELIM: the delimiter byte x4
+#ifdef DP_MAP_NOREC
+  uint32_t skip_rec;           // timing probe: skip the record / spill stores (a repeat of the ctx's last launch)
+#endif
 };
 
 // Range r of the chunk table (ranges of kWaveBytes in each chunk's aligned coordinates): the Geo of a
@@ -1761,12 +1772,31 @@ __device__ __forceinline__ uint32_t atomic_add_nowait(unsigned int* p, uint32_t 
 __device__ __forceinline__ uint4 range_geo_rec(const Geo& g) {
   return uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32), g.lo_u | (g.hi_u << 16), 0u};
 }
+// (kRec16) the same from the chunk table: range r of chunk c (range_geo without the search)
+__device__ __forceinline__ uint4 range_geo_rec_tab(const Tab& T, uint32_t c, uint64_t r) {
+  const uint64_t lo = T.lo[c], hi = T.hi[c], u0 = T.u0[c];
+  const uint64_t ub = (lo & ~15ull) + (r - u0) * (uint64_t)kWaveBytes;
+  const uint32_t lo_u = lo > ub ? (uint32_t)(lo - ub) : 0u;
+  const uint64_t hu = hi - ub;
+  const uint32_t hi_u = hu < (uint64_t)(kWaveBytes + 16) ? (uint32_t)hu : (uint32_t)(kWaveBytes + 16);
+  return uint4{(uint32_t)ub, (uint32_t)(ub >> 32), lo_u | (hi_u << 16), 0u};
+}
+// FASTA range record r's summary word
+__device__ __forceinline__ uint64_t fasta_rec_at(uint64_t r) { return kRec16 ? r : 2 * r; }
 
 template <int MODE>
 __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
                                                                 const uint64_t* __restrict__ tab_hi,
                                                                 const uint64_t* __restrict__ tab_r0) {
-  __shared__ __attribute__((aligned(16))) uint16_t sev[kMapWaves][kSpillCap];
+  // DP_MAP_BATCHREC (FASTA): a step's events, records and counts stay in LDS (two step parities) and one wave per
+  // step stores the previous step's group as a few coalesced stores: 16 waves x 3 scattered stores per step cost
+  // ~29 us per 4 GiB (a timing probe without them: 640-648 vs 671-677 us)
+  constexpr bool kBatch = MODE == kFasta && DP_MAP_DYN && DP_MAP_BATCHREC;
+  constexpr int kPar = kBatch ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) uint16_t sev[kPar][kMapWaves][kSpillCap];
+  __shared__ uint4 s_rec[kPar][kMapWaves][2];
+  __shared__ uint32_t s_nw[kPar][kMapWaves];           // events kept | valid bit (0: no record)
+  __shared__ uint32_t s_r0[kPar];                     // the group's first range
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
@@ -1774,7 +1804,25 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
 #if !DP_MAP_DYN
   const uint32_t NW = gridDim.x * kMapWaves;
 #endif
-  uint16_t* evw = sev[wave];
+  constexpr uint32_t kNwValid = 0x80000000u;
+  // (kBatch, one wave) the group of step parity `par`: 32 lanes store its 16 record pairs, then 16 lanes per word
+  // index its spill words (word-major: word k of its 16 ranges is one contiguous 256-byte run)
+  auto write_batch = [&](uint32_t par) {
+    const uint32_t r0 = s_r0[par];
+    if (kRec16 ? lane < 16 : lane < 32) {
+      const uint32_t w = kRec16 ? (uint32_t)lane : (uint32_t)lane >> 1, h = kRec16 ? 0u : (uint32_t)lane & 1u;
+      if (s_nw[par][w] & kNwValid) M.rec[(kRec16 ? 1 : 2) * (uint64_t)(r0 + w) + h] = s_rec[par][w][h];
+    }
+    const uint32_t w = (uint32_t)lane & 15u;
+    const uint32_t nw = s_nw[par][w];
+    const uint32_t n = (nw & kNwValid) ? (nw & 0xFFFFu) : 0u;
+    for (uint32_t k0 = 0; __ballot(8u * (k0 + ((uint32_t)lane >> 4)) < n) != 0ull; k0 += 4u) {
+      const uint32_t k = k0 + ((uint32_t)lane >> 4);
+      if (8u * k < n)
+        reinterpret_cast<v4u*>(M.spill)[spill_word(k, r0 + w, M.nranges)] =
+            *reinterpret_cast<const v4u*>(&sev[par][w][8u * k]);
+    }
+  };
   // the placement kernel that follows claims its blocks from this ticket: it starts from zero (no memset
   // launch, no end-of-kernel counter; the placement kernel zeroes this kernel's own ticket in turn)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1866,6 +1914,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     FState st{0u, 0u, 0u, -1, 0u, 0u};
     const int lo = (int)g.lo_u, hi = (int)g.hi_u;
     const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
+    uint16_t* evw = sev[kBatch ? (it & 1u) : 0u][wave];
     auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kSpillCap - 1u ? rk : kSpillCap - 1u] = (uint16_t)pos; };
     const uint32_t key = M.delim ^ kSel12;
 #pragma unroll
@@ -1912,20 +1961,43 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     // wait then also waits for as many of its loads as there were stores: conservative)
     if (DP_MAP_B1EARLY) load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
     cbar();
-    if constexpr (MODE == kFasta) {
+#ifdef DP_MAP_NOREC
+    // (probe) DP_MAP_NOREC=1: no record stores, 2: no spill stores, 3: neither; the last launch's data stand
+    const bool probe_norec = M.skip_rec && (DP_MAP_NOREC & 1), probe_nospill = M.skip_rec && (DP_MAP_NOREC & 2);
+#else
+    constexpr bool probe_norec = false, probe_nospill = false;
+#endif
+    if constexpr (kBatch) {
+      // this range's record and count to LDS (its events are there already); the previous step's group, whose
+      // LDS data every wave completed before this step's barrier, to HBM by one wave (rotating)
+      if (!st.nlseen) st.fV = st.S;
+      uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
+      if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
+      const uint32_t par = it & 1u;
+      if (lane == 0) {
+        const bool valid = (g.fl & kGeoValid) != 0u;
+        const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
+                            ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
+        s_nw[par][wave] = valid ? (n | kNwValid) : 0u;
+        s_rec[par][wave][0] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+        s_rec[par][wave][1] = range_geo_rec(g);
+        if (wave == 0) s_r0[par] = r;                  // (wave 0's range is the group's first)
+      }
+      if (it > 0 && (uint32_t)wave == ((it - 1u) & 15u)) write_batch(par ^ 1u);
+    } else if constexpr (MODE == kFasta) {
       // the range's summary (phase_a_rec of a one-range unit) and its events, word-major
       if (!st.nlseen) st.fV = st.S;
       uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
       if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
-      if ((uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
+      if (!probe_nospill && (uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
         const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
         reinterpret_cast<v4u*>(M.spill)[spill_word((uint32_t)lane, r, M.nranges)] = v;   // re-read soon: cacheable
       }
-      if (lane == 0 && (g.fl & kGeoValid)) {
+      if (!probe_norec && lane == 0 && (g.fl & kGeoValid)) {
         const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
                             ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
-        M.rec[2 * (uint64_t)r] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
-        M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
+        M.rec[fasta_rec_at(r)] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+        if (!kRec16) M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
       }
     } else {
       // the range's delimiter count and positions, range-major (the placement gathers consecutive events)
@@ -1948,7 +2020,13 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     if (lane == 0) lds_add(&s_done[it % 8u], 1u);
 #endif
 #if DP_MAP_DYN
-    if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
+    if (gnext >= ngroups) {                           // uniform (LDS value read after the barrier)
+      if constexpr (kBatch) {                         // the last step's group
+        __syncthreads();
+        if ((uint32_t)wave == (it & 15u)) write_batch(it & 1u);
+      }
+      break;
+    }
 #elif DP_MAP_SYNC
     if (it + 1 >= steps) break;
 #else
@@ -2006,7 +2084,8 @@ struct PlaceShared {
 // One placement block b (1024 range records): every thread of the workgroup takes part; ends with a barrier,
 // so the caller may reuse `ps` at once.
 template <int OUT64>
-__device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const ScanArgs& A, uint32_t b, PlaceShared& ps) {
+__device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const ScanArgs& A, const Tab& T, uint32_t b,
+                                                  PlaceShared& ps) {
   typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
   constexpr int kPW = kPlaceBlock / kWave;           // 16 waves
   const int lane = __lane_id();
@@ -2032,8 +2111,8 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
   uint4 rc = uint4{0u, 0u, 2u, 0u};                   // identity: no count, state kept
   uint4 rg = uint4{0u, 0u, 0u, 0u};
   if (valid) {
-    rc = PA.rec[2 * r];
-    rg = PA.rec[2 * r + 1];
+    rc = PA.rec[fasta_rec_at(r)];
+    rg = kRec16 ? range_geo_rec_tab(T, rc.w, r) : PA.rec[2 * r + 1];
   }
   const uint32_t cF = rc.x & 0xFFFFu, cT = rc.x >> 16, fl = rc.z;
   // what the placement needs besides the prefix is loaded now, under the scan and the look-back: the
@@ -2232,7 +2311,7 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
     for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
       const uint32_t t = ps.dense[i];
       const uint64_t rr = (uint64_t)b * kPlaceBlock + t;
-      const uint4 rq = PA.rec[2 * rr + 1];
+      const uint4 rq = kRec16 ? range_geo_rec_tab(T, PA.rec[rr].w, rr) : PA.rec[2 * rr + 1];
       dense_b<kFasta, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, ps.dP[t], ps.dS[t], lane);
     }
   }
@@ -2252,7 +2331,8 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
     ps.blk = DP_PLACE_TICKET ? atomicAdd(&A.ticket[0], 1u) : blockIdx.x;   // claim order: a block only waits on lower,
   }                                                   // already running or finished, blocks
   __syncthreads();
-  fasta_place_block<OUT64>(PA, A, ps.blk, ps);
+  const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
+  fasta_place_block<OUT64>(PA, A, T, ps.blk, ps);
 }
 
 // ------------------------------------------------------------------------------------------ DELIM, two kernels
@@ -3742,6 +3822,10 @@ int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n
   m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
   m.place_ticket = a.ticket;
   m.delim = 0;
+#ifdef DP_MAP_NOREC
+  static thread_local uint64_t probe_launches = 0;
+  m.skip_rec = probe_launches++ >= 4;               // (the bench's two contexts: their first launches write)
+#endif
   PlaceArgs pa;
   pa.map_ticket = m.ticket;
   pa.rec = c->d_rec;
