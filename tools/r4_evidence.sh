@@ -13,8 +13,7 @@ timeout -k 10 400 python -u tools/delim_sweep.py --forms default,line,onepass,tw
 grep form $O/delim_sweep.log
 for leg in fasta csv vcf; do
   step prof_$leg
-  K=""; [ $leg != fasta ] && K="scan_kernel<1, 2>"
-  DELIM_KERNEL="$K" timeout -k 10 500 bash tools/r4_prof.sh $leg $O/$leg > $O/prof_$leg.log 2>&1 || { tail -20 $O/prof_$leg.log; exit 1; }
+  timeout -k 10 500 bash tools/r4_prof.sh $leg $O/$leg > $O/prof_$leg.log 2>&1 || { tail -20 $O/prof_$leg.log; exit 1; }
   tail -4 $O/prof_$leg.log
 done
 step bench
