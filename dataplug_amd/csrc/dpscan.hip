@@ -718,6 +718,9 @@ __device__ __forceinline__ void drain_bufs(Buf (&b)[kBufs]) {
 #endif                     // ~21 and ~26 us per 4 GiB (timing probes without them), far above their bytes' share
                            // of the bus: halving the records measured 657-660 vs 667-670 us (profiles/r04/ab/rec16)
 constexpr bool kRec16 = DP_FASTA_REC16 != 0;
+#ifndef DP_MAP_DEFER       // FASTA map kernel: range records and first spill words kept in LDS and stored in bursts
+#define DP_MAP_DEFER 1     // when the buffer fills and at the end (1), or at every step (0)
+#endif
 #ifndef DP_MAP_BATCHREC    // FASTA map kernel: a group's 16 range records and spill words stored by one wave (1), or
 #define DP_MAP_BATCHREC 0  // each range's by its own wave (0)
 #endif
@@ -1823,6 +1826,32 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
             *reinterpret_cast<const v4u*>(&sev[par][w][8u * k]);
     }
   };
+  // DP_MAP_DEFER (FASTA, 16-byte records): every range's record and first kDeferW spill words stay in LDS, kDeferG
+  // groups deep, and the workgroup stores them in one burst when the buffer is full and once at the end (its last
+  // loads drained): the map's scattered stores inside the read stream cost far more than their bytes (§4)
+  constexpr bool kDefer = MODE == kFasta && DP_MAP_DYN && DP_MAP_DEFER && kRec16 && !kBatch;
+  constexpr uint32_t kDeferG = kDefer ? 72u : 1u, kDeferW = 4u;
+  __shared__ uint4 dq_rec[kDeferG][kMapWaves];
+  __shared__ uint4 dq_sp[kDeferG][kDeferW][kMapWaves];
+  __shared__ uint32_t dq_nw[kDeferG][kMapWaves];      // words buffered | kNwValid (0: no record)
+  __shared__ uint32_t dq_r0[kDeferG];
+  uint32_t nbuf = 0;                                  // groups buffered (uniform)
+  // (every thread, after a barrier) the buffered groups to HBM: per group its 16 records (256 contiguous bytes)
+  // and each buffered spill word index (word-major: 256 contiguous bytes)
+  auto flush = [&]() {
+    constexpr uint32_t kPer = 16u * (1u + kDeferW);
+    for (uint32_t e = threadIdx.x; e < nbuf * kPer; e += kWave * kMapWaves) {
+      const uint32_t gq = e / kPer, rem = e - gq * kPer, part = rem >> 4, w = rem & 15u;
+      const uint32_t nw = dq_nw[gq][w];
+      if (!(nw & kNwValid)) continue;
+      const uint64_t rr = (uint64_t)dq_r0[gq] + w;
+      if (part == 0u) M.rec[rr] = dq_rec[gq][w];
+      else if (part - 1u < (nw & 0xFFu))
+        reinterpret_cast<v4u*>(M.spill)[spill_word(part - 1u, rr, M.nranges)] =
+            *reinterpret_cast<const v4u*>(&dq_sp[gq][part - 1u][w]);
+    }
+    nbuf = 0;
+  };
   // the placement kernel that follows claims its blocks from this ticket: it starts from zero (no memset
   // launch, no end-of-kernel counter; the placement kernel zeroes this kernel's own ticket in turn)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -1967,7 +1996,29 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
 #else
     constexpr bool probe_norec = false, probe_nospill = false;
 #endif
-    if constexpr (kBatch) {
+    if constexpr (kDefer) {
+      if (!st.nlseen) st.fV = st.S;
+      uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
+      if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
+      const bool valid = (g.fl & kGeoValid) != 0u;
+      const uint32_t nwords = (n + 7u) >> 3;
+      if (lane == 0) {
+        const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
+                            ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
+        dq_nw[nbuf][wave] = valid ? ((nwords < kDeferW ? nwords : kDeferW) | kNwValid) : 0u;
+        dq_rec[nbuf][wave] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
+        if (wave == 0) dq_r0[nbuf] = r;                // (wave 0's range is the group's first)
+      }
+      if (valid && (uint32_t)lane < nwords) {
+        const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
+        if ((uint32_t)lane < kDeferW) *reinterpret_cast<v4u*>(&dq_sp[nbuf][lane][wave]) = v;
+        else reinterpret_cast<v4u*>(M.spill)[spill_word((uint32_t)lane, r, M.nranges)] = v;   // a rare long list
+      }
+      if (++nbuf == kDeferG) {                        // uniform: the buffer is full
+        __syncthreads();
+        flush();
+      }
+    } else if constexpr (kBatch) {
       // this range's record and count to LDS (its events are there already); the previous step's group, whose
       // LDS data every wave completed before this step's barrier, to HBM by one wave (rotating)
       if (!st.nlseen) st.fV = st.S;
@@ -2036,6 +2087,10 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     g = gn;
   }
   drain_bufsx(b);
+  if constexpr (kDefer) {                             // the last buffered groups, after the last loads
+    __syncthreads();
+    flush();
+  }
 #ifdef DP_STAMPS
   // per wave: start and end (100 MHz realtime clock), ranges scanned, the XCC it ran on
   if (lane == 0 && blockIdx.x < kProfMaxGrid) {
