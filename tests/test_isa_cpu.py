@@ -79,3 +79,32 @@ def test_guard_flags_violations(tmp_path, use, scratch, ok):
     assert (not touches and not spills) == ok
     assert (isa_guard.verify(str(p))["scratch"] == []) == (scratch == 0)
     assert isa_guard.short_name(isa_guard.kernel_names(str(p))[0]) == "map_kernel<0>"
+
+
+_ASM_DMA = """\t.text
+_ZN12_GLOBAL__N_111line_kernelILi1ELi2EEEvNS_8LineArgsE:
+\t;;#ASMSTART
+\tbuffer_load_dwordx4 v[4:7], v1, s[0:3], 0 offen nt
+\t;;#ASMEND
+\t;;#ASMSTART
+\ts_mov_b32 m0, s8
+\tglobal_load_lds_dwordx4 v[8:9], off sc1
+\t;;#ASMEND
+\ts_waitcnt vmcnt({n})
+\tv_add_u32_e32 v10, v4, v5
+\ts_endpgm
+.Lfunc_end0:
+\t.amdhsa_kernel _ZN12_GLOBAL__N_111line_kernelILi1ELi2EEEvNS_8LineArgsE
+\t\t.amdhsa_private_segment_fixed_size 0
+\t.end_amdhsa_kernel
+"""
+
+
+@pytest.mark.parametrize("n,ok", [(0, True), (1, True), (2, False)])
+def test_guard_counts_lds_dma_loads(tmp_path, n, ok):
+    """line_kernel's look-back windows are LDS-DMA loads (no VGPR destination) that still take a vmcnt slot in
+    issue order: after one, `s_waitcnt vmcnt(1)` retires the older buffer load, `vmcnt(2)` does not."""
+    p = tmp_path / "k.s"
+    p.write_text(_ASM_DMA.format(n=n))
+    assert (isa_guard.check(str(p)) == []) == ok
+    assert isa_guard.short_name(isa_guard.kernel_names(str(p))[0]) == "line_kernel<1,2>"
