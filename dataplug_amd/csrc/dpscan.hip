@@ -1679,6 +1679,9 @@ constexpr uint32_t kSpillCap = 512;                 // events kept per range (1 
 __device__ __forceinline__ uint64_t spill_word(uint32_t j, uint64_t r, uint64_t nranges) { return j * nranges + r; }
 constexpr uint32_t kPlaceBlock = 1024;              // range summaries per placement workgroup (one per thread)
 constexpr uint32_t kStageBytes = 128u << 10;        // LDS staging of a placement block's output run
+#ifndef DP_PLACE_SWZ       // the staging area's 16-byte groups XOR-swizzled within runs of 16 (1) or linear (0)
+#define DP_PLACE_SWZ 0
+#endif
 #ifndef DP_MAP_WAVES
 #define DP_MAP_WAVES 16
 #endif
@@ -2146,6 +2149,12 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   OutT* s_stage = reinterpret_cast<OutT*>(ps.stage);
+  // Staging index of output element i (relative to stage0).  DP_PLACE_SWZ: the 16-byte group g = i / kVec goes to
+  // g ^ ((g >> 4) & 15), a bijection inside each run of 16 groups that keeps a group's elements together: the
+  // threads of a wave write their ranges' runs ~32 elements apart, which linearly fall into one or two LDS banks.
+  constexpr uint32_t kVecS = 16u / sizeof(OutT), kVecSh = sizeof(OutT) == 8 ? 1u : 2u;
+  auto swg = [](uint32_t gi) -> uint32_t { return DP_PLACE_SWZ ? gi ^ ((gi >> 4) & 15u) : gi; };
+  auto swz = [&](uint32_t i) -> uint32_t { return (swg(i >> kVecSh) << kVecSh) | (i & (kVecS - 1u)); };
   if (threadIdx.x == 0) {
     ps.ndense = 0;
     ps.lo = 0;
@@ -2277,7 +2286,7 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
         const uint64_t val = obj_off + e + (slot & 1u);
         if (near4g) ovf |= val > 0xFFFFFFFFull;
         if (stage) {
-          if (slot <= last) s_stage[slot - stage0] = (OutT)val;
+          if (slot <= last) s_stage[swz((uint32_t)(slot - stage0))] = (OutT)val;
         } else {
           put<OutT>(A.out, slot < last ? slot : last, val);
         }
@@ -2301,7 +2310,7 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
           for (uint32_t e = 0; e < 8u; ++e) {
             const uint32_t k = k0 + e;
             const uint32_t ev = (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu;
-            if (k >= skip && k < lim) s_stage[sb + k] = o0 + (OutT)(ev + (par ^ (e & 1u)));
+            if (k >= skip && k < lim) s_stage[swz(sb + k)] = o0 + (OutT)(ev + (par ^ (e & 1u)));
           }
         };
         if (nev > 0u) emit8s(sw0, 0u);
@@ -2336,13 +2345,14 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
     OutT* o = reinterpret_cast<OutT*>(A.out);
     const uint64_t v0 = (run_lo + kVec - 1u) & ~(uint64_t)(kVec - 1u), v1 = run_hi & ~(uint64_t)(kVec - 1u);
     if (v0 <= v1) {
-      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[q - stage0];
-      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
-      const v4u* src = reinterpret_cast<const v4u*>(s_stage + (v0 - stage0));
+      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[swz((uint32_t)(q - stage0))];
+      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[swz((uint32_t)(q - stage0))];
+      const v4u* src = reinterpret_cast<const v4u*>(s_stage);
+      const uint32_t g0 = (uint32_t)((v0 - stage0) / kVec);
       v4u* dst = reinterpret_cast<v4u*>(o + v0);
-      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[g];
+      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[swg(g0 + (uint32_t)g)];
     } else {                                          // the run lies inside one 16-byte group
-      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[q - stage0];
+      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[swz((uint32_t)(q - stage0))];
     }
   }
   PLACE_STAMP(5);
