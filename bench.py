@@ -22,8 +22,9 @@ Workloads (synthetic bytes of the named shapes, resident in HBM before any timed
 One step = on every GPU, one scan call over its bytes: FASTA = dp_fasta_index_async + dp_fasta_result (the
 chunk-table check, the two scan kernels -- map_kernel<FASTA> over 16 KiB ranges, then fasta_place_kernel --,
 the split-header resolve kernel, the read-back of count / pending / chunk ends); newline = dp_delim_ranges
-(one launch: the lockstep line_kernel up to 2 GiB and above it for CSV-dense input, the one-pass look-back
-scan_kernel otherwise, dp_scan_delim_form; the kernel that ran is named in each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
+(one launch: the lockstep line_kernel up to 4 GiB, above it the kernel a density probe picks on the device from
+the launch's own bytes -- line_kernel for CSV-dense input, the one-pass look-back scan_kernel for sparser; the kernel
+that ran, dp_last_delim_form, is named in each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
 rate is DESIGN.md §6).  Steps
 alternate between two contexts and step k + 1 is enqueued before step k's result is collected; the library
 runs one scan at a time per GPU (its scan stream), so ``value`` is this pipelined rate provided
@@ -36,6 +37,12 @@ Launch modes (the same worker code in both):
     devices explicitly, e.g. to rehearse the multi-GPU split on one GPU);
   * ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N``: one rank per GPU; barriers and
     the final gather go over a gloo CPU group, RCCL is never initialised (nothing is exchanged).
+
+At N = 1 the line also carries two end-to-end sub-objects (tools/e2e_legs.py; never ``value``): ``e2e`` --
+co.preprocess() of the configs[1] FASTA and of a configs[2]-shaped CSV from host memory to host memory (ranged GETs,
+pinned staging, H2D, scan, D2H, index PUT) over an in-process store and over the loopback HTTP server in its own
+process, with the stage split -- and ``fastq`` -- configs[4], a FASTQ.gz's per-read index end to end; every stored
+index read back and checked.
 
 Also in the line: per leg the scan's average span from HIP events on the device's scan stream (-> roofline:
 algorithmic bytes / span vs 8 TB/s; ``traffic`` from a committed rocprofv3 PMC summary of the same command),
@@ -88,7 +95,13 @@ def parse(argv=None):
                    help="comma-separated device of each worker / local rank (default 0..N-1); e.g. 0,0,0,0 "
                         "rehearses the multi-GPU split on one GPU")
     p.add_argument("--no-strong", action="store_true", help="skip the fixed-total (strong scaling) FASTA point")
+    p.add_argument("--fasta-onepass", action="store_true",
+                   help="A/B: the FASTA index with the one-pass look-back kernel (dp_ctx_set_form) instead of map + placement")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-e2e", action="store_true", help="skip the end-to-end `e2e` and `fastq` sub-objects (N = 1)")
+    p.add_argument("--e2e-fasta-size", type=int, default=4 << 30, help="e2e leg: the configs[1] FASTA's bytes")
+    p.add_argument("--e2e-csv-size", type=int, default=4 << 30, help="e2e leg: the configs[2]-shaped CSV's bytes")
+    p.add_argument("--fastq-tiles", type=int, default=16, help="fastq leg: copies of the 65,536-read tile")
     p.add_argument("--no-verify", action="store_true")
     p.add_argument("--traffic-bytes", type=float, default=None,
                    help="HBM bytes per headline scan launch from a rocprofv3 --pmc pass (overrides --traffic-from)")
@@ -463,10 +476,12 @@ def load_traffic(args, leg, size, kernel, index_dtype=None):
 
 # ------------------------------------------------------------------------------------------ FASTA
 # The FASTA index is two kernels (libdpscan: the map over 16 KiB ranges, then the placement); their HIP-event
-# span is one "launch" (DP_FASTA_ONEPASS=1: round 2's one-pass look-back kernel, for A/B runs)
-_ONEPASS = os.environ.get("DP_FASTA_ONEPASS", "0") not in ("", "0")
-FASTA_KERNEL = "scan_kernel<FASTA>" if _ONEPASS else "map_kernel<FASTA> + fasta_place_kernel (one HIP-event span)"
-FASTA_PMC_KERNELS = "scan_kernel<0" if _ONEPASS else "map_kernel<0>,fasta_place_kernel"
+# span is one "launch" (--fasta-onepass: round 2's one-pass look-back kernel, for A/B runs, dp_ctx_set_form)
+def fasta_kernel_names(args):
+    """(label, rocprof kernel names of one launch) of the FASTA form the run uses."""
+    if args.fasta_onepass:
+        return "scan_kernel<FASTA>", "scan_kernel<0"
+    return "map_kernel<FASTA> + fasta_place_kernel (one HIP-event span)", "map_kernel,fasta_place_kernel"
 
 
 class FastaSpec:
@@ -493,6 +508,9 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
     from dataplug_amd.scan import ScanContext
     out = {"worker": k, "device": dev}
     ctxs = (ScanContext(dev), ScanContext(dev))
+    if args.fasta_onepass:
+        for c in ctxs:
+            c.set_form(fasta=1)
 
     def prepare(sp: FastaSpec, tag: str, gi: int):
         if gi >= len(sp.groups):
@@ -599,7 +617,8 @@ def report_fasta(args, world, team, allres, spec, strong, t_leg):
         host = spec.obj.bytes_range(0, spec.size)        # regenerated: the worker kept no host copy
         cpu = cpu_baseline(host, spec.chunk_size)
         del host
-    traffic, traffic_src = load_traffic(args, "fasta", spec.size, FASTA_PMC_KERNELS) if world == 1 else (None, None)
+    fasta_label, fasta_pmc = fasta_kernel_names(args)
+    traffic, traffic_src = load_traffic(args, "fasta", spec.size, fasta_pmc) if world == 1 else (None, None)
     strong_out = None
     if strong is not None:
         sr = [r["strong"] for r in allres if "strong" in r]
@@ -646,7 +665,7 @@ def report_fasta(args, world, team, allres, spec, strong, t_leg):
         "roofline": {"bound": "hbm", "achieved": round(ach / 1e9, 1), "peak": HBM_PEAK / 1e9,
                      "unit": "GB/s", "frac": round(ach / HBM_PEAK, 4),
                      "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
-                     "kernel": FASTA_KERNEL, "kernel_avg_us": round(kern * 1e6, 2),
+                     "kernel": fasta_label, "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(r0["alg_bytes"]),
                      "alg_bytes_def": "N + 8 * H (N chunk bytes read once, H headers x two uint32 offsets)",
                      "measured_peak": None if peak_meas is None else round(peak_meas / 1e9, 1),
@@ -741,10 +760,10 @@ def delim_worker(args, team, leg, k, world, dev):
     S = Steps(team, ctxs, launch, collect)
     team.barrier()
     S.warm(args.warmup)
-    # the kernel the timed launches take (above 2 GiB it follows each context's previous launch's delimiter
-    # density, dp_scan_delim_form: known after the warm-up)
-    kernel = " / ".join(ScanContext.DELIM_FORMS[f] for f in sorted({c.delim_form(nbytes) for c in ctxs}))
     dt_t, (kms, kn), _ = S.timed(args.steps, timing=True)
+    # the kernel the timed launches ran: line_kernel up to 4 GiB per launch, above it the density probe's pick from
+    # the launch's own bytes (dp_last_delim_form reads it back with each launch's results)
+    kernel = " / ".join(ScanContext.DELIM_FORMS[f] for f in sorted({c.last_delim_form() for c in ctxs}))
     dt, _, _ = S.timed(args.steps)                                         # serialized (secondary)
     dt_ov, _, (n_out, _, ends) = S.timed(args.steps, serialize=False)      # pipelined (`value`), verified
     wpr = item * n_out / max(1, nbytes)
@@ -819,8 +838,7 @@ def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
         cpu = cpu_baseline_delim(sample)
         del sample
     k = allres[0]["kernel"]
-    pmc_kernel = ("line_kernel<" if k.startswith("line_kernel") else "scan_kernel<1" if k.startswith("scan_kernel")
-                  else "map_kernel<1>,delim_place_kernel")
+    pmc_kernel = "line_kernel<" if k.startswith("line_kernel") else "scan_kernel<1"
     traffic, traffic_src = (load_traffic(args, leg, allres[0]["scanned"], pmc_kernel, args.index_dtype)
                             if world == 1 else (None, None))
     name = "CSV" if csv_mode else "VCF"
@@ -910,6 +928,23 @@ def main(argv=None):
                 team._tb.reset()              # a failed worker aborted the threads' barrier
             if head is not None:
                 head[leg] = sub
+        if world == 1 and not args.no_e2e and head is not None:
+            sys.path.insert(0, os.path.join(REPO, "tools"))
+            import e2e_legs
+            budgets = {"e2e": 90.0, "fastq": 45.0}
+            for name, fn in (("e2e", lambda: e2e_legs.e2e_leg(args.e2e_fasta_size, args.e2e_csv_size,
+                                                               verify_blocked=_verify_blocked,
+                                                               verify=not args.no_verify, log=log)),
+                             ("fastq", lambda: e2e_legs.fastq_leg(tiles=args.fastq_tiles, verify=not args.no_verify,
+                                                                  log=log))):
+                try:
+                    sub = fn()
+                    sub["budget_s"] = budgets[name]
+                    sub["fits_in_driver_run"] = bool(sub["leg_s"] <= budgets[name])
+                except Exception as e:        # an end-to-end leg never drops the headline
+                    log(f"leg {name} failed: {type(e).__name__}: {e}")
+                    sub = {"error": f"{type(e).__name__}: {e}"}
+                head[name] = sub
         if head is not None:
             rss = [head.get("rss_gib_max_worker", 0.0)] + [(head.get(x) or {}).get("rss_gib_max_worker", 0.0)
                                                            for x in args.legs[1:]]

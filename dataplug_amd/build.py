@@ -21,7 +21,7 @@ from dataplug_amd import isa_guard
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, "csrc", "dpscan.hip")
 OUT = os.path.join(HERE, "lib", "libdpscan.so")
-OUT_PROF = os.path.join(HERE, "lib", "libdpscan_prof.so")   # diagnostics: in-kernel section timers
+OUT_DIAG = os.path.join(HERE, "lib", "libdpscan_diag.so")   # diagnostics: in-kernel realtime stamps (-DDP_DIAG)
 GZ_SRC = os.path.join(HERE, "csrc", "dpgz.c")
 GZ_PAR_SRC = os.path.join(HERE, "csrc", "dpgz_par.c")     # parallel inflate of one gzip stream
 GZ_OUT = os.path.join(HERE, "lib", "libdpgz.so")            # host-side gzip access-point index (zlib)
@@ -44,15 +44,14 @@ def stamp_path(lib: str) -> str:
     return lib + ".isa.json"
 
 
-def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=SRC, guard=None) -> str:
-    """Compile ``src`` for gfx950, run the ISA guard on its assembly, install it at ``out`` if it passes.
-    ``guard`` defaults to on except for the DP_PROF diagnostics build (whose section timers spill by design:
-    it is never the shipped library, and its stamp records the failed guard)."""
-    out = out or (OUT_PROF if prof else OUT)
-    guard = (not prof) if guard is None else guard
+def build(verbose: bool = False, diag: bool = False, defines=(), out=None, src=SRC) -> str:
+    """Compile ``src`` for gfx950, run the ISA guard on its assembly, install it at ``out`` only if it passes.
+    The shipped library has no defines; ``diag`` builds the diagnostics library (-DDP_DIAG: in-kernel realtime
+    stamps, lib/libdpscan_diag.so), guarded like the shipped one and loaded only through DPSCAN_LIB."""
+    out = out or (OUT_DIAG if diag else OUT)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-    defs = (["DP_PROF"] if prof else []) + list(defines)  # tuning variants, e.g. DP_RING=5 (tools/probe_perf.py)
+    defs = (["DP_DIAG"] if diag else []) + list(defines)
     with tempfile.TemporaryDirectory(prefix="dpscan_build_") as d:
         cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall",
                "-Wno-unused-result", "-save-temps"] + [f"-D{x}" for x in defs] + ["-o", os.path.join(d, "lib.so"),
@@ -65,12 +64,13 @@ def build(verbose: bool = False, prof: bool = False, defines=(), out=None, src=S
         rep = isa_guard.verify(asm)
         print(f"ISA guard: {rep['result']} ({len(rep['kernels'])} kernels, {os.path.basename(out)})",
               file=sys.stderr if rep["result"] != "ok" else sys.stdout, flush=True)
-        if guard and rep["result"] != "ok":
+        if rep["result"] != "ok":
             raise IsaGuardError(f"{out} not installed: the ISA guard failed on its assembly: "
                                 f"{rep['violations'][:3]} {rep['scratch'][:3]} missing {rep['missing_kernels']}")
         shutil.copyfile(os.path.join(d, "lib.so"), out + ".tmp")
         rep.update(so_sha256=sha256_file(out + ".tmp"), asm_sha256=sha256_file(asm), defines=defs, arch=ARCH,
-                   source=os.path.relpath(os.path.abspath(src), os.path.dirname(HERE)), guard_enforced=guard)
+                   source=os.path.relpath(os.path.abspath(src), os.path.dirname(HERE)), src_sha256=sha256_file(src),
+                   guard_enforced=True)
         with open(stamp_path(out) + ".tmp", "w") as f:
             json.dump(rep, f, indent=1)
         os.replace(stamp_path(out) + ".tmp", stamp_path(out))
@@ -89,4 +89,4 @@ def build_gz() -> str:
 
 if __name__ == "__main__":
     print(build_gz())
-    print(build(verbose="-v" in sys.argv, prof="--prof" in sys.argv))
+    print(build(verbose="-v" in sys.argv, diag="--diag" in sys.argv))

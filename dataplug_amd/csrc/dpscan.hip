@@ -1,33 +1,25 @@
 // dpscan.hip — MI355X (gfx950, CDNA4) record-boundary scan kernels + the C ABI of libdpscan.so.
 //
-// What runs here:
-//   * scan_kernel<FASTA>: the FASTA header index of dataplug/formats/genomics/fasta.py:24-63 for a whole
-//     chunk plan in ONE pass over HBM; emits (start, end) offset pairs bit-exact to the reference.
-//   * scan_kernel<DELIM>: sorted offsets of a delimiter byte (CSV/VCF newline index, FASTQ read ends).
-//   * fasta_resolve_kernel / find_kernel: the "header cut by the chunk end" fix-up (fasta.py:45-56).
-//
-// Single pass, memory-bound (no MFMA):
-//   * persistent grid, one 1024-thread workgroup per CU = 15 data waves + 1 coordinator wave.  Workgroups
-//     claim runs of consecutive 240 KiB units from a global ticket while they run; data wave w owns a
-//     16 KiB range of each (16 rows of 64 lanes x 16 B, bounds-checked non-temporal buffer loads into
-//     DP_NBUF VGPR buffers: one scanned while the others are in flight, hand-waited).
-//   * byte classes: v_perm_b32 with all-ones data sources returns 0x00 for selector byte 12 and 0xFF for
-//     every other selector, so perm(-1, -1, w ^ (pattern ^ 0x0C0C0C0C)) flags the pattern bytes of w
-//     exactly (2 VALU per dword); v_dot4_i32_i8 packs 4 flags into a nibble.
-//   * phase A (data wave, per unit): the wave range's events — FASTA header starts/ends under the
-//     hypothesis "no header pending at the range start", DELIM delimiters — go to the wave's circular list
-//     of 16-bit positions in LDS, and the range's summary (count and line state as a function of the
-//     incoming state) to the unit's ring slot.
-//   * coordinator wave: composes the 15 summaries (DPP scan), publishes the unit aggregate, resolves the
-//     unit prefix by a decoupled look-back over 8-byte descriptors (agent-scope relaxed atomics,
-//     cdna_hip_programming.md G16 R2) and hands per-wave prefixes back through LDS flags.  It runs as an
-//     event loop and never blocks on a single unit.
-//   * phase B (same data wave, as soon as the unit's prefix is there): a coalesced copy of the event list
-//     to the output at its final index (+ the state fix-up at the range start).  A data wave only waits for
-//     the coordinator once it is kRing units ahead.  Ranges with more than kDenseMax events ("dense") keep
-//     no list; their phase B rescans the range from the input with the now known state.
-//   * every wait is bounded (DP_ERR_TIMEOUT); units are claimed in increasing order by running workgroups
-//     only, so a unit only ever waits on lower units owned by running (or finished) workgroups.
+// What ships (every kernel memory-bound integer byte work, no MFMA):
+//   * FASTA header index (dataplug/formats/genomics/fasta.py:24-63 for a whole chunk plan, bit-exact):
+//     map_kernel (one 16-wave workgroup per CU streams groups of 16 ranges of 16 KiB claimed from a ticket, a
+//     barrier per step; per range a 16-byte summary of its header count / line state as a function of the
+//     incoming state, and its events, under "no header pending", burst-stored from LDS) + fasta_place_kernel
+//     (blocks of 1024 range summaries: scan, decoupled look-back over block descriptors, the pending-header
+//     fix-up, LDS-staged coalesced output runs), then fasta_resolve_kernel (header ends cut by a chunk end).
+//   * newline index (CSV / VCF lines, FASTQ read ends with every_k = 4): line_kernel (the map kernel's streaming
+//     loop with the positions kept in LDS, a per-group decoupled look-back by LDS-DMA windows and in-kernel
+//     placement) up to 4 GiB per launch and for CSV-dense input above; the one-pass look-back scan_kernel<DELIM>
+//     (persistent grid, 15 data waves + a coordinator wave per workgroup, 240 KiB units) for sparser input above
+//     4 GiB, picked per launch on the device by density_probe_kernel from the launch's own bytes.
+//   * find_kernel (dp_find_delim), and the calibration stream kernels.
+// Shared pieces: bounds-checked non-temporal buffer loads hand-waited with explicit s_waitcnt (checked by the
+// ISA guard, dataplug_amd/isa_guard.py, before a build is installed); byte classes by v_perm_b32 with all-ones
+// sources (perm(-1, -1, w ^ (pattern ^ 0x0C0C0C0C)) flags the pattern bytes exactly, 2 VALU per dword) packed
+// by v_dot4_i32_i8; look-back descriptors tagged with a launch epoch (no per-launch reset); every inter-workgroup
+// wait bounded in time (DP_ERR_TIMEOUT); work that waits on other workgroups claimed from tickets by running
+// workgroups only, so no grid assumes co-residency.  scan_kernel<FASTA> (the one-pass FASTA form) stays for
+// A/B runs (dp_ctx_set_form).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -43,25 +35,18 @@
 
 namespace {
 
+// The shipped geometry and policies (the variants measured against them are in DESIGN.md §4 and git history;
+// round 5 removed their switches: the library is one build).
 constexpr int kWave = 64;
-#ifndef DP_DWAVES
-#define DP_DWAVES 15
-#endif
-constexpr int kDataWaves = DP_DWAVES;              // + 1 coordinator wave
+constexpr int kDataWaves = 15;                     // + 1 coordinator wave (one-pass kernel)
 static_assert(kDataWaves >= 2 && kDataWaves <= 15, "data waves: one DPP row of summaries");
 constexpr int kCoord = kDataWaves;
 constexpr int kWaves = kDataWaves + 1;
-constexpr int kThreads = kWave * kWaves;           // 1024 (default)
+constexpr int kThreads = kWave * kWaves;           // 1024
 constexpr int kRowBytes = kWave * 16;              // one dwordx4 per lane
-#ifndef DP_NBUF
-#define DP_NBUF 2
-#endif
-#ifndef DP_RROWS
-#define DP_RROWS 16
-#endif
-constexpr int kRangeRows = DP_RROWS;               // rows per wave range
+constexpr int kRangeRows = 16;                     // rows per wave range
 static_assert(kRangeRows * 1024 + 64 < 65536, "event positions are 16-bit offsets into a range");
-constexpr int kBufs = DP_NBUF;                     // input buffers per wave range: one scanned, the rest in flight
+constexpr int kBufs = 2;                           // input buffers per wave range: one scanned, one in flight
 constexpr int kRows = kRangeRows / kBufs;          // rows per buffer (one load batch)
 constexpr int kBufBytes = kRowBytes * kRows;
 constexpr int kWaveBytes = kRowBytes * kRangeRows;   // 16 KiB wave range per unit
@@ -69,50 +54,21 @@ constexpr int kUnitBytes = kWaveBytes * kDataWaves;  // 240 KiB look-back unit
 static_assert(kRows * kBufs == kRangeRows && kRows >= 2 && kRows <= 8, "buffers of 2, 4 or 8 rows");
 // In-flight load destinations live in VGPRs (4 per 16-byte row). 1024-lane workgroups have 128 VGPRs per
 // lane; past 64 of them in buffers the compiler spills live destinations to scratch, and a spilled
-// un-waited destination corrupts addresses (DP_RROWS=32 + DP_NBUF=4 = 128 VGPRs faulted the GPU in round 3).
+// un-waited destination corrupts addresses (32-row ranges in 4 buffers = 128 VGPRs faulted the GPU in round 3).
 static_assert(kBufs * kRows * 4 <= 64, "input buffers must leave room in the 128-VGPR budget");
-#ifndef DP_RING
-#define DP_RING 16
-#endif
-#ifndef DP_EVCAP
-#define DP_EVCAP 4096
-#endif
-#ifndef DP_PRIO
-#define DP_PRIO 2
-#endif
-#ifndef DP_LBFAST
-#define DP_LBFAST 1
-#endif
-#ifndef DP_LAGSHIFT    // DP_PRIO 2: issue priority = min(lag << DP_LAGSHIFT, 3)
-#define DP_LAGSHIFT 0
-#endif
-#ifndef DP_PRIO_LEVELS
-#define DP_PRIO_LEVELS 4u
-#endif
-constexpr uint32_t kRing = DP_RING;                // unit slots per workgroup (units in flight)
+constexpr uint32_t kRing = 16;                     // unit slots per workgroup (units in flight)
 // Units are claimed dynamically (a global ticket, by the coordinator, kClaimAhead steps ahead of the
 // workgroup's front data wave): a workgroup only ever claims a unit while it runs, so every unit a wait
 // depends on belongs to a running (or finished) workgroup — no co-residency assumption, and faster CUs
 // take more units.  The queue spans the ring plus the claim-ahead distance.
-#ifndef DP_CLAIM_FASTA
-#define DP_CLAIM_FASTA 4
-#endif
-#ifndef DP_CLAIM_DELIM     // DELIM units per claim once a unit holds more than DP_CLAIM_DENSE delimiters
-#define DP_CLAIM_DELIM 2
-#endif
-#ifndef DP_CLAIM_SPARSE    // ... and while they hold fewer
-#define DP_CLAIM_SPARSE 4
-#endif
-#ifndef DP_CLAIM_DENSE
-#define DP_CLAIM_DENSE 5500
-#endif
-#ifndef DP_CLAIM_AHEAD
-#define DP_CLAIM_AHEAD 3
-#endif
-constexpr uint32_t kClaimAhead = DP_CLAIM_AHEAD;
-constexpr uint32_t kUnitQ = 2 * DP_RING;
+constexpr uint32_t kClaimFasta = 4;                // FASTA units per claim
+constexpr uint32_t kClaimDelimDense = 2;           // DELIM units per claim once a unit holds more than kClaimDense
+constexpr uint32_t kClaimDelimSparse = 4;          // ... and while they hold fewer
+constexpr uint32_t kClaimDense = 5500;
+constexpr uint32_t kClaimAhead = 3;
+constexpr uint32_t kUnitQ = 2 * kRing;
 static_assert(kUnitQ >= kRing + kClaimAhead + 2, "unit queue: ring + claim-ahead");
-constexpr uint32_t kEvCap = DP_EVCAP;              // 16-bit event entries per data wave (circular)
+constexpr uint32_t kEvCap = 4096;                  // 16-bit event entries per data wave (circular)
 constexpr uint32_t kEvMask = kEvCap - 1;
 constexpr uint32_t kDenseMax = 1024;               // events kept per wave range; more = dense
 static_assert((kEvCap & kEvMask) == 0 && kEvCap >= 2 * kDenseMax, "event list: power of two, >= 2 ranges");
@@ -151,57 +107,22 @@ __device__ __forceinline__ bool wait_expired(uint32_t spins, uint64_t& t0) {
 }
 
 enum Mode { kFasta = 0, kDelim = 1 };
+// newline kernels (the codes of dp_scan_delim_form / dp_last_delim_form): lockstep line_kernel, map + placement, one-pass
+constexpr uint32_t kFormLine = 1, kFormOne = 3;   // (2: round 3's map + placement newline form, removed in round 5)
 
-// In-kernel section timers (diagnostics build only: -DDP_PROF).  Per workgroup and wave, kProfSlots
-// accumulated s_memtime deltas; read back with dp_debug_profile().
-// -DDP_PROF2: only the two-kernel form's stamps (map_kernel / fasta_place_kernel), none in scan_kernel, whose
-// DP_PROF accumulators cost registers (its DP_PROF build spills and fails tools/isa_guard.py).
-#if defined(DP_LTL) && !defined(DP_PROF) && !defined(DP_PROF2)
-#define DP_PROF2 1   // -DDP_LTL: line_kernel's per-step timeline (implies the two-kernel form's stamps)
-#endif
-#if defined(DP_PROF) && defined(DP_PROF2)
-#error "DP_PROF and DP_PROF2 are exclusive"
-#endif
-#if defined(DP_PROF) || defined(DP_PROF2)
-#define DP_STAMPS 1
+// Diagnostics build only (-DDP_DIAG; dataplug_amd.build never sets it for the shipped library): realtime stamps
+// (100 MHz) of the two-kernel FASTA form (map_kernel per wave, fasta_place_kernel per block) and line_kernel's
+// per-step timeline, read back with dp_debug_profile() (tools/map_timeline.py, place_timeline.py,
+// line_timeline.py).
+#ifdef DP_DIAG
 constexpr int kProfSlots = 8;
 constexpr int kProfWaves = 16;
 constexpr int kProfMaxGrid = 1024;
-#ifdef DP_LTL
-// line_kernel timeline (realtime clock, 100 MHz) past the per-wave slots: [256 workgroups][64 steps][waves 0, 1, 8,
-// 15][8 events] (tools/line_timeline.py names them)
+// line_kernel timeline past the per-wave slots: [256 workgroups][64 steps][waves 0, 1, 8, 15][8 events]
 constexpr uint64_t kLtlBase = (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;
 constexpr uint32_t kLtlSteps = 64, kLtlWaves = 4;
 constexpr uint64_t kProfWords = kLtlBase + 256ull * kLtlSteps * kLtlWaves * 8;
-#else
-constexpr uint64_t kProfWords = (uint64_t)kProfMaxGrid * kProfWaves * kProfSlots;
-#endif
 __device__ unsigned long long g_prof[kProfWords];
-#endif
-#ifdef DP_PROF
-#define PROF_DECL uint64_t prof_acc[kProfSlots] = {0, 0, 0, 0, 0, 0, 0, 0}; uint64_t prof_t = __builtin_amdgcn_s_memtime()
-#define PROF_MARK(slot) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); prof_acc[slot] += t_ - prof_t; prof_t = t_; } while (0)
-#define PROF_FLUSH(wave) do { if (__lane_id() == 0 && blockIdx.x < kProfMaxGrid) { for (int i_ = 0; i_ < kProfSlots; ++i_) \
-    g_prof[((uint64_t)blockIdx.x * kProfWaves + (wave)) * kProfSlots + i_] = prof_acc[i_]; } } while (0)
-// Per-unit timeline (realtime clock, 100 MHz) in the g_prof words past the first 256 workgroups' slots:
-// [256 workgroups][96 steps][4 words]: 0 AGG published, 1 prefix resolved, 2 phase A of data wave 0 done,
-// 3 the step's unit index (a value, not a time).
-constexpr uint64_t kTlBase = 256ull * kProfWaves * kProfSlots;
-constexpr uint32_t kTlUnits = 96;
-#define TL_STAMP(k, e) do { if (__lane_id() == 0 && blockIdx.x < 256 && (uint32_t)(k) < kTlUnits) \
-    g_prof[kTlBase + ((uint64_t)blockIdx.x * kTlUnits + (uint32_t)(k)) * 4 + (e)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#define TL_PUT(k, e, v) do { if (__lane_id() == 0 && blockIdx.x < 256 && (uint32_t)(k) < kTlUnits) \
-    g_prof[kTlBase + ((uint64_t)blockIdx.x * kTlUnits + (uint32_t)(k)) * 4 + (e)] = (v); } while (0)
-#define PROF_ARG , uint64_t (&prof_acc)[kProfSlots], uint64_t& prof_t
-#define PROF_PASS , prof_acc, prof_t
-#else
-#define PROF_DECL do {} while (0)
-#define PROF_MARK(slot) do {} while (0)
-#define PROF_FLUSH(wave) do {} while (0)
-#define TL_STAMP(k, e) do {} while (0)
-#define TL_PUT(k, e, v) do {} while (0)
-#define PROF_ARG
-#define PROF_PASS
 #endif
 
 struct ScanArgs {
@@ -227,6 +148,7 @@ struct ScanArgs {
   unsigned int* ticket;        // [2]: next unit to claim, workgroups finished (both reset by the last one)
   long long* pending;          // FASTA: [nchunks] pair index whose end is unresolved at chunk end, or -1
   unsigned long long* chunk_end;  // [nchunks] inclusive count at the end of each (non-empty) chunk
+  const uint32_t* pick;        // (auto newline form) the density probe's choice: the one-pass kernel runs only if kFormOne
 };
 
 // ------------------------------------------------------------------------------------------ helpers
@@ -236,30 +158,12 @@ __device__ __forceinline__ uint32_t match4(uint32_t w, uint32_t key) {
 }
 // match4 bytes (0x00 = 0, 0xFF = -1 as i8) of a lane's 4 dwords -> 16-bit mask, bit i = byte i matched.
 // v_dot4_i32_i8 with weights 1, 2, 4, 8 subtracts the non-matching weights of one dword from its
-// accumulator; chained Horner-style (acc << 4 between dwords) it leaves -(non-match mask), and
-// 0xFFFF + that is the match mask.  4 dot4 + 3 shifts + 1 add.
-#ifndef DP_INTERIOR
-#define DP_INTERIOR 1
-#endif
-#ifndef DP_PACK_IND
-#define DP_PACK_IND 1
-#endif
-// DELIM output stores with the non-temporal hint (the index is not re-read by the kernel).  Same-box A/B:
-// CSV/VCF +2%; on FASTA's sparse 4-byte stores the hint measured -1 to -2%, so FASTA keeps plain stores.
-#ifndef DP_NTSTORE
-#define DP_NTSTORE 1
-#endif
-#ifndef DP_PAIRSTORE   // DELIM phase B: 16-byte stores of offset pairs (uint64 output, every_k = 1)
-#define DP_PAIRSTORE 1
-#endif
+// accumulator; combined as four independent dot4s (no accumulator chain: the dependent v_dot4c form needs
+// s_nop 2 per link) by two-level shift-adds, d0 carrying the +0xFFFF: 4 dot4 + 3 shifts + 2 adds.
+// DELIM output stores carry the non-temporal hint (the index is not re-read by the kernel; same-box A/B: CSV/VCF
+// +2%; on FASTA's sparse 4-byte stores it measured -1 to -2%, so FASTA keeps plain stores).
 typedef unsigned long long v2u64 __attribute__((ext_vector_type(2)));
-#ifndef DP_RANKCLAMP
-#define DP_RANKCLAMP 1
-#endif
 __device__ __forceinline__ uint32_t pack16(uint32_t p0, uint32_t p1, uint32_t p2, uint32_t p3) {
-#if DP_PACK_IND
-  // four independent dot4s (no accumulator chain: the dependent v_dot4c form needs s_nop 2 per link),
-  // combined by two-level shift-adds; d0 carries the +0xFFFF
   const int d0 = __builtin_amdgcn_sdot4((int)p0, 0x08040201, 0xFFFF, false);
   const int d1 = __builtin_amdgcn_sdot4((int)p1, 0x08040201, 0, false);
   const int d2 = __builtin_amdgcn_sdot4((int)p2, 0x08040201, 0, false);
@@ -267,13 +171,6 @@ __device__ __forceinline__ uint32_t pack16(uint32_t p0, uint32_t p1, uint32_t p2
   const uint32_t lo = ((uint32_t)d1 << 4) + (uint32_t)d0;
   const uint32_t hi = ((uint32_t)d3 << 4) + (uint32_t)d2;
   return (hi << 8) + lo;
-#else
-  int t = __builtin_amdgcn_sdot4((int)p3, 0x08040201, 0, false);
-  t = __builtin_amdgcn_sdot4((int)p2, 0x08040201, t * 16, false);
-  t = __builtin_amdgcn_sdot4((int)p1, 0x08040201, t * 16, false);
-  t = __builtin_amdgcn_sdot4((int)p0, 0x08040201, t * 16, false);
-  return (uint32_t)(t + 0xFFFF);
-#endif
 }
 __device__ __forceinline__ uint32_t mask16(const uint4& v, uint32_t key) {
   return pack16(match4(v.x, key), match4(v.y, key), match4(v.z, key), match4(v.w, key));
@@ -349,20 +246,16 @@ __device__ __forceinline__ uint32_t lds_add(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ void cbar() { asm volatile("" ::: "memory"); }
 
 // Issue priority (s_setprio takes an immediate).  The 4 data waves sharing a SIMD otherwise get issue
-// slots by age.  DP_PRIO 2 (default): a wave's priority is how far it trails the workgroup's front wave,
-// so the waves a unit's AGG waits for take issue slots from the ones that run ahead (DataWave::step);
-// DP_PRIO 1: the priority rotates per unit; 0: no priorities.
+// slots by age.  A data wave's priority is how far it trails the workgroup's front wave, so the waves a
+// unit's AGG waits for take issue slots from the ones that run ahead (DataWave::step; a per-unit rotation
+// measured -14 % on DELIM, no priorities -9 %).
 __device__ __forceinline__ void set_prio(uint32_t p) {
-#if DP_PRIO
   switch (p & 3u) {
     case 0: __builtin_amdgcn_s_setprio(0); break;
     case 1: __builtin_amdgcn_s_setprio(1); break;
     case 2: __builtin_amdgcn_s_setprio(2); break;
     default: __builtin_amdgcn_s_setprio(3); break;
   }
-#else
-  (void)p;
-#endif
 }
 
 template <typename T, bool NT = false>
@@ -456,10 +349,7 @@ constexpr uint64_t kIdentDesc = kStatMask;   // status 3: "no unit here" (identi
 // between the two (u itself for the workgroup's first unit, whose "previous unit" is the empty prefix).
 // (With the static unit striding W = G - 1 < kLbSlots; a larger W would mean no base: the window then
 // resolves only once it holds an inclusive prefix.)
-#ifndef DP_LBSLOTS
-#define DP_LBSLOTS 4
-#endif
-constexpr int kLbPer = DP_LBSLOTS;                 // descriptors per lane
+constexpr int kLbPer = 4;                          // descriptors per lane (2: FASTA -22 %, 8: -9 to -16 %)
 constexpr uint32_t kLbSlots = kLbPer * kWave;      // descriptors per window (256 >= G)
 constexpr uint32_t kNoUnit = 0xFFFFFFFFu;
 __device__ __forceinline__ uint32_t lb_span(uint32_t u, uint32_t u_prev) {
@@ -507,7 +397,7 @@ __device__ __forceinline__ bool lb_reduce(uint64_t (&d)[kLbPer], uint32_t W, uin
   // not); with only constant maps between the nearest prefix and u, every unit's incoming state is the
   // state bit (bit 48 of AGG and PREFIX descriptors alike) of its farther neighbour, so the prefix is a
   // plain sum of selected counts.  Any identity map in range: the full functional scan below.
-  if (DP_LBFAST) {
+  {
     const int Lp = 63 - __builtin_clzll(PB);          // nearest lane holding a prefix (PB != 0)
     uint32_t jp = kLbPer;
 #pragma unroll
@@ -643,10 +533,8 @@ struct Buf {
 // checks the compiled code never touches a destination while its load can still be in flight.
 constexpr int kLoadsPerBuf = kRows + 1;
 // Input bytes are read once: non-temporal loads (nt) stream them without displacing L2 lines; measured on
-// MI355X the load pattern alone goes from 6.2 to 6.9 TB/s (tools/cmp_variants.sh, DP_LOADONLY).
-#ifndef DP_LDPOL
+// MI355X the load pattern alone goes from 6.2 to 6.9 TB/s (a load-only probe, round 1).
 #define DP_LDPOL "nt"
-#endif
 
 // buffer resource for one wave range: num_records ends at the 16-byte block holding the chunk end
 __device__ __forceinline__ v4i buf_rsrc(const uint8_t* base, uint64_t wbase, int hi_w) {
@@ -704,79 +592,44 @@ __device__ __forceinline__ void drain_bufs(Buf (&b)[kBufs]) {
 }
 
 // The same buffers without the lookahead dword (a FASTA row needs the byte after it; a delimiter row does not):
-// kRows loads per buffer, 2 VGPRs fewer per wave (line_kernel runs at the 128-VGPR limit).
-// the map kernel's input buffers: DP_MAP_BUFN 1 = BufN (no lookahead dword load; FASTA reads it by a scalar
-// load), 0 = Buf (the lookahead dword as a ninth vector load per buffer)
-#ifndef DP_MAP_BUFN
-#define DP_MAP_BUFN 1
-#endif
-#ifndef DP_MAP_B1EARLY     // A/B: the map kernel's last buffer reloaded before the range's stores (see map_kernel)
-#define DP_MAP_B1EARLY 0
-#endif
-#ifndef DP_FASTA_REC16     // FASTA range records of 16 bytes (1: the placement derives the range's geometry from the
-#define DP_FASTA_REC16 1   // chunk table) or 32 (0: summary + geometry).  The map kernel's record and spill stores cost
-#endif                     // ~21 and ~26 us per 4 GiB (timing probes without them), far above their bytes' share
-                           // of the bus: halving the records measured 657-660 vs 667-670 us (profiles/r04/ab/rec16)
-constexpr bool kRec16 = DP_FASTA_REC16 != 0;
-#ifndef DP_MAP_DEFER       // FASTA map kernel: range records and first spill words kept in LDS and stored in bursts
-#define DP_MAP_DEFER 1     // when the buffer fills and at the end (1), or at every step (0)
-#endif
-#ifndef DP_MAP_BATCHREC    // FASTA map kernel: a group's 16 range records and spill words stored by one wave (1), or
-#define DP_MAP_BATCHREC 0  // each range's by its own wave (0)
-#endif
+// kRows loads per buffer, 2 VGPRs fewer per wave (line_kernel runs at the 128-VGPR limit).  The two-kernel and
+// lockstep kernels use these; FASTA reads its lookahead dword by a scalar load (lookahead_s).
 struct BufN {
   v4u x[kRows];
 };
 constexpr int kLoadsPerBufN = kRows;
-__device__ __forceinline__ void load_buf_n(BufN& b, const ScanArgs& A, const Geo& g, int lane, int half) {
+__device__ __forceinline__ void load_bufx(BufN& b, const ScanArgs& A, const Geo& g, int lane, int half) {
   int hb = (g.fl & kGeoValid) ? wave_hi(g, 0) - half * kBufBytes : 0;
   hb = hb < 0 ? 0 : (hb > kBufBytes + 16 ? kBufBytes + 16 : hb);
   const v4i r = buf_rsrc(A.base, g.ubase + (uint64_t)half * kBufBytes, hb);
   Buf& bb = *reinterpret_cast<Buf*>(&b);          // (load_rows writes x[] only)
   load_rows<kRows>(bb, (uint32_t)lane * 16u, r);
 }
-__device__ __forceinline__ void touch_buf_n(BufN& b) {
+__device__ __forceinline__ void touch_bufx(BufN& b) {
 #pragma unroll
   for (int r = 0; r < kRows; ++r) asm volatile("" : "+v"(b.x[r]) :: "memory");
 }
-__device__ __forceinline__ void wait_buf_n(BufN& b) {
+__device__ __forceinline__ void wait_bufx(BufN& b) {
   asm volatile("s_waitcnt vmcnt(%0)" :: "i"((kBufs - 1) * kLoadsPerBufN) : "memory");
-  touch_buf_n(b);
+  touch_bufx(b);
   __builtin_amdgcn_sched_barrier(0);
 }
-__device__ __forceinline__ void drain_bufs_n(BufN (&b)[kBufs]) {
+__device__ __forceinline__ void drain_bufsx(BufN (&b)[kBufs]) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int h = 0; h < kBufs; ++h) touch_buf_n(b[h]);
+  for (int h = 0; h < kBufs; ++h) touch_bufx(b[h]);
   __builtin_amdgcn_sched_barrier(0);
 }
-// Buffers of the lockstep kernels, either kind (BufN: no lookahead dword in flight; FASTA reads it by a scalar load).
-__device__ __forceinline__ void load_bufx(BufN& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf_n(b, A, g, lane, h); }
-__device__ __forceinline__ void wait_bufx(BufN& b) { wait_buf_n(b); }
-__device__ __forceinline__ void touch_bufx(BufN& b) { touch_buf_n(b); }
-__device__ __forceinline__ void drain_bufsx(BufN (&b)[kBufs]) { drain_bufs_n(b); }
-__device__ __forceinline__ void load_bufx(Buf& b, const ScanArgs& A, const Geo& g, int lane, int h) { load_buf(b, A, g, 0, lane, h); }
-__device__ __forceinline__ void wait_bufx(Buf& b) { wait_buf(b); }
-__device__ __forceinline__ void touch_bufx(Buf& b) { touch_buf(b); }
-__device__ __forceinline__ void drain_bufsx(Buf (&b)[kBufs]) { drain_bufs(b); }
 typedef __attribute__((address_space(4))) const uint32_t cu32s;   // constant address space: s_load_dword
 // the first dword after buffer h of a wave range (FASTA's next-byte lookahead) by a scalar load through the
 // constant address space (it waits on lgkmcnt, never on the hand-counted vmcnt); read only where that byte lies
-// inside the chunk, the range's own first dword elsewhere (always in the buffer)
+// inside the chunk, the range's own first dword elsewhere (always in the buffer).  (As a ninth vector load per
+// buffer it measured 669-672 vs 676-678 us per 4 GiB, profiles/r04/ab/map_bufn.)
 __device__ __forceinline__ uint32_t lookahead_s(const uint8_t* base, const Geo& g, int h, bool interior, int hi) {
   const bool inb = interior || (h + 1) * kBufBytes < hi;
   const uint64_t at = g.ubase + (inb ? (uint64_t)(h + 1) * kBufBytes : 0ull);
   return *(cu32s*)(uintptr_t)(base + at);
 }
-__device__ __forceinline__ uint32_t lookahead(const Buf& b, const uint8_t*, const Geo&, int, bool, int) { return b.la; }
-__device__ __forceinline__ uint32_t lookahead(const BufN&, const uint8_t* base, const Geo& g, int h, bool interior, int hi) {
-  return lookahead_s(base, g, h, interior, hi);
-}
-#if DP_MAP_BUFN
-typedef BufN MapBuf;
-#else
-typedef Buf MapBuf;
-#endif
 
 // ------------------------------------------------------------------------------------------ LDS state
 struct WaveRec {                   // one data wave's phase-A result for one unit (written by its lane 0)
@@ -902,9 +755,6 @@ __device__ __forceinline__ void fasta_row(const v4u& xr, uint32_t wn, int r, int
 template <bool INTERIOR, class Store>
 __device__ __forceinline__ void fasta_rows(const v4u (&x)[kRows], uint32_t la, int half, int lo, int hi, int lane,
                                            FState& st, Store&& store) {
-#ifdef DP_NOROWS
-  return;   // perf probe only: the per-unit machinery without any row work
-#endif
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const int R = half * kRows + r;
@@ -932,9 +782,6 @@ __device__ __forceinline__ void delim_row(const v4u& xr, int r, int lo, int hi, 
 template <bool INTERIOR, class Store>
 __device__ __forceinline__ void delim_rows(const v4u (&x)[kRows], int half, int lo, int hi, uint32_t key, int lane,
                                            uint32_t& nev, Store&& store) {
-#ifdef DP_NOROWS
-  return;
-#endif
 #pragma unroll
   for (int r = 0; r < kRows; ++r) {
     const int R = half * kRows + r;
@@ -953,7 +800,7 @@ struct PhaseA {
 };
 template <int MODE, int OUT64>
 __device__ __forceinline__ void phase_a_half(const ScanArgs& A, PhaseA& pa, Buf& b, int half, int wave, int lane,
-                                             Shared& sh, uint32_t ev_head PROF_ARG) {
+                                             Shared& sh, uint32_t ev_head) {
   v4u x[kRows];
 #pragma unroll
   for (int r = 0; r < kRows; ++r) x[r] = b.x[r];
@@ -961,13 +808,9 @@ __device__ __forceinline__ void phase_a_half(const ScanArgs& A, PhaseA& pa, Buf&
   // Ranks past kDenseMax (a dense range: its list is never read) all land on the range's last reserved
   // entry, which the room check keeps free: a clamp instead of a conditional store.
   auto keep = [&](uint32_t rk, uint32_t pos) {
-#if DP_RANKCLAMP
     evw[(ev_head + (rk < kDenseMax - 1u ? rk : kDenseMax - 1u)) & kEvMask] = (uint16_t)pos;
-#else
-    if (rk < kDenseMax) evw[(ev_head + rk) & kEvMask] = (uint16_t)pos;
-#endif
   };
-  const bool interior = DP_INTERIOR && pa.lo == 0 && pa.hi > kWaveBytes;   // wave-uniform
+  const bool interior = pa.lo == 0 && pa.hi > kWaveBytes;   // wave-uniform
   (void)interior;
   if constexpr (MODE == kFasta) {
     if (interior) fasta_rows<true>(x, b.la, half, pa.lo, pa.hi, lane, pa.st, keep);
@@ -977,7 +820,6 @@ __device__ __forceinline__ void phase_a_half(const ScanArgs& A, PhaseA& pa, Buf&
     // the kernel past 128 VGPRs and spills an in-flight load destination, which tools/isa_guard.py flags)
     delim_rows<false>(x, half, pa.lo, pa.hi, A.delim ^ kSel12, lane, pa.st.nev, keep);
   }
-  PROF_MARK(1);
 }
 template <int MODE>
 __device__ __forceinline__ void phase_a_rec(PhaseA& pa, const Geo& g, int wave, uint32_t ev_head, WaveRec& rec) {
@@ -1054,7 +896,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
       const uint64_t q = q0 + t;
       const uint64_t val = add + pos;
       if (near4g) ovf |= val > 0xFFFFFFFFull;
-      put<OutT, DP_NTSTORE != 0>(A.out, q < last ? q : last, val);
+      put<OutT, true>(A.out, q < last ? q : last, val);
     };
     const uint32_t key = A.delim ^ kSel12;
 #pragma unroll 1
@@ -1087,7 +929,6 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
     q0 = (Pc + r0) / k - A.carry / k;
     nq = nev > r0 ? (nev - r0 + k - 1u) / k : 0u;
   }
-#if DP_PAIRSTORE
   if constexpr (OUT64 == 1 && PAIR) {
     // Every delimiter, uint64 output, the whole list in bounds (wave-uniform): two offsets per lane and
     // one 16-byte store, which halves the store instructions that queue behind the input loads.  An odd
@@ -1102,22 +943,14 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
         const uint64_t v0 = add + ev(i);
         if (t + 1u < m) {
           const uint64_t v1 = add + ev(i + 1u);
-#if DP_NTSTORE
           __builtin_nontemporal_store(v2u64{v0, v1}, reinterpret_cast<v2u64*>(o + i));
         } else {
           __builtin_nontemporal_store((uint64_t)v0, o + i);
         }
-#else
-          *reinterpret_cast<v2u64*>(o + i) = v2u64{v0, v1};
-        } else {
-          o[i] = v0;
-        }
-#endif
       }
       return false;
     }
   }
-#endif
   if constexpr (OUT64 == 2) {
     // uint16 low words, every delimiter, whole list in bounds: eight entries per lane, one 16-byte store;
     // the first (8 - q0 % 8) % 8 entries go alone so that the groups are 16-byte aligned
@@ -1137,13 +970,7 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
           w[e] = a | (b << 16);
         }
         const v4u pk = {w[0], w[1], w[2], w[3]};
-#if defined(DP_PROBE_NOSTORE)
-        ovf |= (pk.x ^ pk.y ^ pk.z ^ pk.w) == 0x9E3779B9u;   // timing probe (wrong results): the gathers, no store
-#elif DP_NTSTORE
         __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + i));
-#else
-        *reinterpret_cast<v4u*>(o + i) = pk;
-#endif
       }
       for (uint32_t t = h + 8u * g + (uint32_t)lane; t < nq; t += kWave) o[t] = (uint16_t)(add + ev(t));
       return false;
@@ -1153,7 +980,7 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
     const uint64_t q = q0 + t;
     const uint64_t val = add + ev(r0 + t * k);
     if (near4g) ovf |= val > 0xFFFFFFFFull;
-    put<OutT, DP_NTSTORE != 0>(A.out, q < last ? q : last, val);
+    put<OutT, true>(A.out, q < last ? q : last, val);
   }
   return ovf;
 }
@@ -1278,33 +1105,23 @@ __device__ __forceinline__ Func compose_unit(Shared& sh, uint32_t s, int lane) {
   return unit;
 }
 
-#ifndef DP_LBDEPTH
-#define DP_LBDEPTH 6
-#endif
-#ifndef DP_IDLE_SLEEP    // coordinator back-off (x 64 clocks) after a round without progress
-#define DP_IDLE_SLEEP 1
-#endif
 // Coordinator issue priority.  At 0 it loses every arbitration to the data waves of its SIMD, which
 // (memory permitting) always have an instruction ready: on some XCDs the workgroups' first AGGs came
 // ~100 us late (tools/timeline.py; every look-back waits on them), and FASTA is 2-3 % faster at 3.  The
 // write-heavy CSV newline index is 4 % slower at 3 (its look-back polls then compete with phase B).
-#ifndef DP_COORD_PRIO_FASTA
-#define DP_COORD_PRIO_FASTA 3
-#endif
-#ifndef DP_COORD_PRIO_DELIM
-#define DP_COORD_PRIO_DELIM 0
-#endif
+constexpr uint32_t kCoordPrioFasta = 3, kCoordPrioDelim = 0;
+constexpr uint32_t kIdleSleep = 1;                 // coordinator back-off (x 64 clocks) after a round without progress
 // look-back windows in flight per coordinator attempt: 8 windows (64 VGPRs of descriptors) pushed the
 // coordinator path past the kernel's 128 VGPRs and spilled to scratch (44-52 B/lane); 6 spills nothing
 // (FASTA +1.4-2.3 % same box, DELIM +-1 %)
-constexpr uint32_t kLbDepth = DP_LBDEPTH;
+constexpr uint32_t kLbDepth = 6;
 
 // consecutive units per ticket atomic: one returning atomic on one address per unit caps the grid near
 // 20 units/us (measured: FASTA -16% at 1, -7% at 2, parity at 4); a longer run of consecutive units
 // per workgroup delays the next workgroup's look-back, which an event-dense DELIM scan feels first (its
 // per-wave event lists fill): CSV (~6,900 delimiters per unit) -20% at 4 vs 2, while VCF (~3,100) and
 // FASTQ (~4,300) gain 5% at 4.  DELIM picks the run from the last composed unit's delimiter count.
-template <int MODE> constexpr uint32_t kClaimN = MODE == kFasta ? DP_CLAIM_FASTA : DP_CLAIM_DELIM;
+template <int MODE> constexpr uint32_t kClaimN = MODE == kFasta ? kClaimFasta : kClaimDelimDense;
 
 // Coordinator event loop.  Its descriptor loads queue behind the CU's in-flight input stream (~5 us),
 // so it never waits on one unit: each round it issues the look-back windows of up to kLbDepth composed
@@ -1312,8 +1129,7 @@ template <int MODE> constexpr uint32_t kClaimN = MODE == kFasta ? DP_CLAIM_FASTA
 // workgroups' look-backs wait on those), then resolves the windows in order until one is incomplete.
 template <int MODE>
 __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int lane, Shared& sh) {
-  PROF_DECL;
-  set_prio(MODE == kFasta ? DP_COORD_PRIO_FASTA : DP_COORD_PRIO_DELIM);
+  set_prio(MODE == kFasta ? kCoordPrioFasta : kCoordPrioDelim);
   Cursor cur{0, 0, 0, 0, 0, 0};
   uint64_t prevP = 0;
   uint32_t prevS = 0;
@@ -1334,7 +1150,7 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
       if (nbatch == 0) {
         uint32_t u = 0;
         // DELIM: long runs while the units are event-sparse, short ones once a unit is event-dense
-        uint32_t run = MODE == kFasta ? kClaimN<MODE> : (last_events > (uint32_t)DP_CLAIM_DENSE ? kClaimN<MODE> : (uint32_t)DP_CLAIM_SPARSE);
+        uint32_t run = MODE == kFasta ? kClaimN<MODE> : (last_events > kClaimDense ? kClaimN<MODE> : kClaimDelimSparse);
         // FASTA's first round: one unit per workgroup, so the first prefixes need only the first step's
         // AGGs (FASTA +0.9-2.2 % same box; DELIM -0.4-0.9 %, so it keeps its runs)
         if (MODE == kFasta && claimed == 0) run = 1;
@@ -1352,9 +1168,6 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
         lds_st(&sh.uq_ready[slot], claimed + 1u);
       }
       if (v == kNoUnit) K = claimed;
-#ifdef DP_TL_CLAIM
-      TL_STAMP(claimed, 2);
-#endif
       ++claimed;
       any = true;
     }
@@ -1370,7 +1183,6 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
       const uint32_t up = unit_of(pub);
       if (lane == 0) {
         if (up > 0) st_desc(&A.desc[up], pack_agg(f) | A.epoch);
-        TL_STAMP(pub, 0);
         sh.done[s] = 0;                               // slot's counter free for unit pub + kRing
       }
       ++pub;
@@ -1378,40 +1190,22 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
     }
     return any;
   };
-#ifdef DP_TL_COORD
-  uint32_t it = 0;                                  // coordinator iterations traced into timeline slots 72..95
-#define TL_IT(e) do { if (it < 24u) TL_STAMP(72u + it, e); } while (0)
-#else
-#define TL_IT(e) do {} while (0)
-#endif
   while (res < K) {
-    TL_IT(0);
     bool prog = claim_ahead();
-    TL_IT(1);
     prog |= compose_ready();
-    TL_IT(2);
-    PROF_MARK(0);
     if (res < pub) {
       const uint32_t D = pub - res < kLbDepth ? pub - res : kLbDepth;
-#ifdef DP_PROF
-      prof_acc[4] += 1;                               // look-back attempts (count)
-#endif
       uint64_t d[kLbDepth][kLbPer];
       uint32_t Wj[kLbDepth];
 #pragma unroll
       for (uint32_t j = 0; j < kLbDepth; ++j) {
-#ifndef DP_NOSYNC
         if (j < D) {
           const uint32_t u = unit_of(res + j);
           Wj[j] = lb_span(u, res + j > 0 ? unit_of(res + j - 1) : kNoUnit);
           lb_load(A, u, Wj[j], lane, d[j]);
         }
-#else
-        for (int i = 0; i < kLbPer; ++i) d[j][i] = kIdentDesc;   // perf probe: no cross-workgroup dependency
-#endif
       }
       prog |= compose_ready();                        // while the windows travel
-      PROF_MARK(0);
 #pragma unroll
       for (uint32_t j = 0; j < kLbDepth; ++j) {
         if (j >= D) break;
@@ -1419,14 +1213,8 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
         uint64_t P;
         uint32_t S_in;
         if (!lb_reduce(d[j], Wj[j], pack_prefix(res > 0 ? prevP : 0ull, res > 0 ? prevS : 0u), lane, P, S_in)) {
-#ifdef DP_PROF
-          prof_acc[5] += 1;                           // incomplete windows (count)
-#endif
           break;
         }
-#ifdef DP_PROF
-        prof_acc[6] += 1;                             // resolved units (count)
-#endif
         const uint32_t s = res % kRing;
         const Geo g = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, u, cur);
         const uint32_t usv = sh.us[s];
@@ -1451,17 +1239,10 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
         // LDS ops of one wave complete in order: every lane's P/S write lands before lane 0's flag
         cbar();
         if (lane == 0) lds_st(&sh.ready[s], res + 1u);
-        TL_STAMP(res, 1);
-        TL_PUT(res, 3, u);
         ++res;
         prog = true;
       }
-      PROF_MARK(1);
     }
-    TL_IT(3);
-#ifdef DP_TL_COORD
-    it += prog ? 1u : 0u;
-#endif
     if (prog) {
       idle = 0;
       idle_t0 = 0;
@@ -1470,11 +1251,9 @@ __device__ __forceinline__ void coordinator(const ScanArgs& A, const Tab& T, int
         if (lane == 0) atomicOr(A.err, kErrTimeout);
         break;
       }
-      __builtin_amdgcn_s_sleep(DP_IDLE_SLEEP);
-      PROF_MARK(3);
+      __builtin_amdgcn_s_sleep(kIdleSleep);
     }
   }
-  PROF_FLUSH(kCoord);
 }
 
 // Data wave: phase A of every unit of the workgroup in order (double-buffered loads two units ahead),
@@ -1499,42 +1278,31 @@ struct DataWave {
     return rfl(sh.uq[slot]);
   }
 
-  __device__ __forceinline__ void finish(bool block, int wslot PROF_ARG) {
+  __device__ __forceinline__ void finish(bool block) {
     const uint32_t s = jt % kRing;
     if (block) {
-      PROF_MARK(2);
       lds_wait_eq(&sh.ready[s], jt + 1u, A.err);
-      PROF_MARK(wslot);
     }
     phase_b<MODE, OUT64>(A, sh, s, wave, lane, ev_tail);
     ++jt;
-    PROF_MARK(4);
   }
 
   // Unit k: for each buffer h in order, phase A over it, then (but for the last) its prefetch for unit
   // k + 1; publish; phase B of ready units; prefetch of the last buffer.  While one buffer is scanned the
   // kBufs - 1 others are in flight.
-  __device__ __forceinline__ bool step(uint32_t k, Geo& g, Buf (&b)[kBufs], Cursor& cur PROF_ARG) {
+  __device__ __forceinline__ bool step(uint32_t k, Geo& g, Buf (&b)[kBufs], Cursor& cur) {
     // sh.front = the workgroup's front step (the coordinator claims units ahead of it)
     uint32_t front = 0;
     if (lane == 0) front = __hip_atomic_fetch_max(&sh.front, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     front = rfl(front);
-#if DP_PRIO == 2
     // Issue priority = how many units this wave trails the workgroup's front wave (0..3): a unit's AGG
     // waits for its slowest wave, so the trailing waves take issue slots from the leading ones.
     {
-      const uint32_t lag = front > k ? (front - k) << DP_LAGSHIFT : 0u;
+      const uint32_t lag = front > k ? front - k : 0u;
       set_prio(lag < 3u ? lag : 3u);
     }
-#else
-    set_prio(((uint32_t)(wave >> 2) + k) % DP_PRIO_LEVELS);   // the 4 data waves of a SIMD take turns
-#endif
     const uint32_t s = k % kRing;
     wait_buf(b[0]);
-#ifdef DP_TL_DATA
-    if (wave == 0) TL_STAMP(k, 2);                    // the unit's first buffer landed
-#endif
-    PROF_MARK(0);
     const uint32_t un = unit_of(k + 1u);
     const Geo gn = geo_of(T, (uint32_t)A.nchunks, (uint32_t)A.nunits, un, cur);
     PhaseA pa;
@@ -1546,17 +1314,13 @@ struct DataWave {
     for (int h = 0; h < kBufs; ++h) {
       if (h > 0) {
         wait_buf(b[h]);                               // this buffer landed; the others stay in flight
-        PROF_MARK(0);
       }
-      phase_a_half<MODE, OUT64>(A, pa, b[h], h, wave, lane, sh, ev_head PROF_PASS);
+      phase_a_half<MODE, OUT64>(A, pa, b[h], h, wave, lane, sh, ev_head);
       if (h + 1 < kBufs) load_buf(b[h], A, gn, wave, lane, h);
     }
     WaveRec rec;
     phase_a_rec<MODE>(pa, g, wave, ev_head, rec);
     ev_head += rec.nev;
-#if !defined(DP_TL_CLAIM) && !defined(DP_TL_DATA)
-    if (wave == 0) TL_STAMP(k, 2);
-#endif
     if (lane == 0) {
       sh.rec[s][wave] = rec;
       cbar();
@@ -1570,16 +1334,14 @@ struct DataWave {
       const bool rdy = lds_ld(&sh.ready[jt % kRing]) == jt + 1u;
       if (!rdy && room) break;
       cbar();
-      finish(!rdy, 3 PROF_PASS);
+      finish(!rdy);
     }
     load_buf(b[kBufs - 1], A, gn, wave, lane, kBufs - 1);
     g = gn;
-    PROF_MARK(5);
     return un < (uint32_t)A.nunits;
   }
 
   __device__ __forceinline__ void run() {
-    PROF_DECL;
     Cursor cur{0, 0, 0, 0, 0, 0};
     const uint32_t u0 = unit_of(0);
     if (u0 == kNoUnit) return;                         // every unit was claimed before this workgroup ran
@@ -1588,12 +1350,9 @@ struct DataWave {
 #pragma unroll
     for (int h = 0; h < kBufs; ++h) load_buf(b[h], A, g, wave, lane, h);
     uint32_t K = 0;                                    // the workgroup's step count (>= 1: u0 is a unit)
-    for (bool more = true; more; ++K) more = step(K, g, b, cur PROF_PASS);
+    for (bool more = true; more; ++K) more = step(K, g, b, cur);
     drain_bufs(b);
-    PROF_MARK(6);
-    while (jt < K) finish(true, 7 PROF_PASS);         // the tail: wait for the workgroup's last prefixes
-    PROF_MARK(6);
-    PROF_FLUSH(wave);
+    while (jt < K) finish(true);         // the tail: wait for the workgroup's last prefixes
   }
 };
 
@@ -1601,6 +1360,7 @@ template <int MODE, int OUT64>
 __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64_t* __restrict__ tab_lo,
                                                         const uint64_t* __restrict__ tab_hi,
                                                         const uint64_t* __restrict__ tab_u0) {
+  if (A.pick != nullptr && *(const cu32s*)(uintptr_t)A.pick != kFormOne) return;   // (uniform) the probe chose line_kernel
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __shared__ Shared sh;
@@ -1613,34 +1373,6 @@ __global__ void __launch_bounds__(kThreads) scan_kernel(ScanArgs A, const uint64
   if (threadIdx.x < kUnitQ) sh.uq_ready[threadIdx.x] = 0;
   if (threadIdx.x == 0) sh.front = 0;
   __syncthreads();
-#ifdef DP_LOADONLY
-  // perf probe only (never a shipped build): the data waves' load structure without any compute or
-  // synchronisation — the ceiling this grid/unit geometry can stream at
-  if (wave != kCoord) {
-    const uint32_t nunits = (uint32_t)A.nunits;
-    const uint32_t u0 = blockIdx.x;
-    const uint32_t K = u0 < nunits ? (nunits - u0 + G - 1) / G : 0;
-    Cursor cur{0, 0, 0, 0, 0, 0};
-    Geo g = geo_of(T, (uint32_t)A.nchunks, nunits, u0, cur);
-    Buf b[kBufs];
-#pragma unroll
-    for (int h = 0; h < kBufs; ++h) load_buf(b[h], A, g, wave, lane, h);
-    uint32_t acc = 0;
-    for (uint32_t k = 0; k < K; ++k) {
-      const Geo gn = geo_of(T, (uint32_t)A.nchunks, nunits, u0 + (k + 1) * G, cur);
-#pragma unroll
-      for (int h = 0; h < kBufs; ++h) {
-        wait_buf(b[h]);
-#pragma unroll
-        for (int r = 0; r < kRows; ++r) acc ^= b[h].x[r][0] ^ b[h].x[r][1] ^ b[h].x[r][2] ^ b[h].x[r][3];
-        load_buf(b[h], A, gn, wave, lane, h);
-      }
-    }
-    drain_bufs(b);
-    if (acc == 0x9E3779B9u) atomicOr(A.err, 4u);
-  }
-  return;
-#endif
   if (wave == kCoord) {
     coordinator<MODE>(A, T, lane, sh);
   } else {
@@ -1679,49 +1411,21 @@ constexpr uint32_t kSpillCap = 512;                 // events kept per range (1 
 __device__ __forceinline__ uint64_t spill_word(uint32_t j, uint64_t r, uint64_t nranges) { return j * nranges + r; }
 constexpr uint32_t kPlaceBlock = 1024;              // range summaries per placement workgroup (one per thread)
 constexpr uint32_t kStageBytes = 128u << 10;        // LDS staging of a placement block's output run
-#ifndef DP_PLACE_SWZ       // the staging area's 16-byte groups XOR-swizzled within runs of 16 (1) or linear (0)
-#define DP_PLACE_SWZ 0
-#endif
-#ifndef DP_MAP_WAVES
-#define DP_MAP_WAVES 16
-#endif
-constexpr uint32_t kMapWaves = DP_MAP_WAVES;        // map kernel: 16 data waves per workgroup, no coordinator
-constexpr uint32_t kMapPerCU = 16u / kMapWaves;     // (A/B: 8-wave workgroups, two per CU)
-static_assert(kMapWaves * kMapPerCU == 16u, "map kernel: 16 waves per CU");
+constexpr uint32_t kMapWaves = 16;                  // map kernel: 16 data waves per workgroup, one per CU, no coordinator
 constexpr uint32_t kRecFirst = 16u, kRecLast = 32u; // range record flags (bits 0-3: sF, sT, fV, dense)
-#ifndef DP_MAP_SYNC        // map kernel: a workgroup barrier per step (its waves on adjacent ranges)
-#define DP_MAP_SYNC 1
-#endif
-#ifndef DP_PLACE_TICKET    // placement blocks in ticket order (0: in blockIdx order, A/B only)
-#define DP_PLACE_TICKET 1
-#endif
-#ifndef DP_MAP_LEAD        // DP_MAP_SYNC 2: steps a wave may lead its workgroup's slowest wave by
-#define DP_MAP_LEAD 1
-#endif
-#ifndef DP_MAP_DYN         // map kernel: groups of 16 ranges claimed from a ticket (0: static striding)
-#define DP_MAP_DYN 1
-#endif
-#ifndef DP_MAP_RUN         // groups per claim (1: 677-681 us vs 687-689 us per 4 GiB with 2, same box,
-#define DP_MAP_RUN 1       // profiles/r03/knob_ab/) ...
-#endif
-#ifndef DP_MAP_AHEAD       // steps claimed ahead of the current one (2: step it + 2 has its group by the
-#define DP_MAP_AHEAD 2     // barrier of step it + 1, where its loads are issued)
-#endif
-#ifndef DP_MAP_TAIL        // ... and one group per claim once within DP_MAP_TAIL x G groups of the end
-#define DP_MAP_TAIL 3
-#endif
+// Map kernel policies (each measured against its alternatives): a workgroup barrier per step (its waves on
+// adjacent ranges), groups of 16 ranges claimed from a ticket one per atomic (677-681 us vs 687-689 us per 4 GiB with
+// two, profiles/r03/knob_ab/), two steps ahead (step it + 2 has its group by the barrier of step it + 1, where its
+// loads are issued).
+constexpr uint32_t kMapAhead = 2;
 
 struct MapArgs {
   const uint8_t* base;         // 16-byte aligned; coordinates relative to it
   uint64_t nchunks, nranges;
-  uint4* rec;                  // [2 * nranges]: range r's summary at 2r, its geometry at 2r + 1 (range_geo_rec)
+  uint4* rec;                  // [nranges] 16-byte range records
   uint16_t* spill;             // event positions relative to the range, word-major (spill_word)
-  unsigned int* ticket;        // (DP_MAP_DYN) next group to claim; zeroed by the placement kernel
+  unsigned int* ticket;        // next group to claim; zeroed by the placement kernel
   unsigned int* place_ticket;  // [2] the placement kernel's block ticket, zeroed here
-  uint32_t delim;              // DELIM: the delimiter byte x4
-#ifdef DP_MAP_NOREC
-  uint32_t skip_rec;           // timing probe: skip the record / spill stores (a repeat of the ctx's last launch)
-#endif
 };
 
 // Range r of the chunk table (ranges of kWaveBytes in each chunk's aligned coordinates): the Geo of a
@@ -1773,12 +1477,8 @@ __device__ __forceinline__ uint32_t atomic_add_nowait(unsigned int* p, uint32_t 
   return old;
 }
 
-// The second half of a range record: where the range lies (aligned coordinates) and its chunk bounds relative to
-// it, so the placement needs no chunk-table lookup: {wbase lo, wbase hi, lo_w | hi_w << 16, 0}.
-__device__ __forceinline__ uint4 range_geo_rec(const Geo& g) {
-  return uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32), g.lo_u | (g.hi_u << 16), 0u};
-}
-// (kRec16) the same from the chunk table: range r of chunk c (range_geo without the search)
+// the same from the chunk table: range r of chunk c (range_geo without the search; FASTA's 16-byte records carry no
+// geometry: the placement derives it, which halved the map's record stores, profiles/r04/ab/rec16)
 __device__ __forceinline__ uint4 range_geo_rec_tab(const Tab& T, uint32_t c, uint64_t r) {
   const uint64_t lo = T.lo[c], hi = T.hi[c], u0 = T.u0[c];
   const uint64_t ub = (lo & ~15ull) + (r - u0) * (uint64_t)kWaveBytes;
@@ -1788,52 +1488,20 @@ __device__ __forceinline__ uint4 range_geo_rec_tab(const Tab& T, uint32_t c, uin
   return uint4{(uint32_t)ub, (uint32_t)(ub >> 32), lo_u | (hi_u << 16), 0u};
 }
 // FASTA range record r's summary word
-__device__ __forceinline__ uint64_t fasta_rec_at(uint64_t r) { return kRec16 ? r : 2 * r; }
 
-template <int MODE>
 __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, const uint64_t* __restrict__ tab_lo,
                                                                 const uint64_t* __restrict__ tab_hi,
                                                                 const uint64_t* __restrict__ tab_r0) {
-  // DP_MAP_BATCHREC (FASTA): a step's events, records and counts stay in LDS (two step parities) and one wave per
-  // step stores the previous step's group as a few coalesced stores: 16 waves x 3 scattered stores per step cost
-  // ~29 us per 4 GiB (a timing probe without them: 640-648 vs 671-677 us)
-  constexpr bool kBatch = MODE == kFasta && DP_MAP_DYN && DP_MAP_BATCHREC;
-  constexpr int kPar = kBatch ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) uint16_t sev[kPar][kMapWaves][kSpillCap];
-  __shared__ uint4 s_rec[kPar][kMapWaves][2];
-  __shared__ uint32_t s_nw[kPar][kMapWaves];           // events kept | valid bit (0: no record)
-  __shared__ uint32_t s_r0[kPar];                     // the group's first range
+  __shared__ __attribute__((aligned(16))) uint16_t sev[kMapWaves][kSpillCap];
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   const uint32_t nranges = (uint32_t)M.nranges, nchunks = (uint32_t)M.nchunks;
-#if !DP_MAP_DYN
-  const uint32_t NW = gridDim.x * kMapWaves;
-#endif
   constexpr uint32_t kNwValid = 0x80000000u;
-  // (kBatch, one wave) the group of step parity `par`: 32 lanes store its 16 record pairs, then 16 lanes per word
-  // index its spill words (word-major: word k of its 16 ranges is one contiguous 256-byte run)
-  auto write_batch = [&](uint32_t par) {
-    const uint32_t r0 = s_r0[par];
-    if (kRec16 ? lane < 16 : lane < 32) {
-      const uint32_t w = kRec16 ? (uint32_t)lane : (uint32_t)lane >> 1, h = kRec16 ? 0u : (uint32_t)lane & 1u;
-      if (s_nw[par][w] & kNwValid) M.rec[(kRec16 ? 1 : 2) * (uint64_t)(r0 + w) + h] = s_rec[par][w][h];
-    }
-    const uint32_t w = (uint32_t)lane & 15u;
-    const uint32_t nw = s_nw[par][w];
-    const uint32_t n = (nw & kNwValid) ? (nw & 0xFFFFu) : 0u;
-    for (uint32_t k0 = 0; __ballot(8u * (k0 + ((uint32_t)lane >> 4)) < n) != 0ull; k0 += 4u) {
-      const uint32_t k = k0 + ((uint32_t)lane >> 4);
-      if (8u * k < n)
-        reinterpret_cast<v4u*>(M.spill)[spill_word(k, r0 + w, M.nranges)] =
-            *reinterpret_cast<const v4u*>(&sev[par][w][8u * k]);
-    }
-  };
-  // DP_MAP_DEFER (FASTA, 16-byte records): every range's record and first kDeferW spill words stay in LDS, kDeferG
-  // groups deep, and the workgroup stores them in one burst when the buffer is full and once at the end (its last
-  // loads drained): the map's scattered stores inside the read stream cost far more than their bytes (§4)
-  constexpr bool kDefer = MODE == kFasta && DP_MAP_DYN && DP_MAP_DEFER && kRec16 && !kBatch;
-  constexpr uint32_t kDeferG = kDefer ? 72u : 1u, kDeferW = 4u;
+  // every range's record and first kDeferW spill words stay in LDS, kDeferG groups deep, and the workgroup stores
+  // them in one burst when the buffer is full and once at the end (its last loads drained): the map's scattered
+  // stores inside the read stream cost far more than their bytes (DESIGN.md §4, 644-650 vs 658-662 us)
+  constexpr uint32_t kDeferG = 72u, kDeferW = 4u;
   __shared__ uint4 dq_rec[kDeferG][kMapWaves];
   __shared__ uint4 dq_sp[kDeferG][kDeferW][kMapWaves];
   __shared__ uint32_t dq_nw[kDeferG][kMapWaves];      // words buffered | kNwValid (0: no record)
@@ -1861,20 +1529,22 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
     M.place_ticket[0] = 0u;
     M.place_ticket[1] = 0u;
   }
-#ifdef DP_STAMPS
+#ifdef DP_DIAG
   const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
   uint32_t n_done = 0;
 #endif
-#if DP_MAP_DYN
-  // Groups of 16 consecutive ranges (one per wave), the first one blockIdx.x, then claimed in runs from a
-  // ticket by wave 0 (so faster CUs and XCDs take more groups); s_grp[k % kGrpQ] = the group of step k.
+  // Groups of 16 consecutive ranges (one per wave), claimed from a ticket by wave 0 (so faster CUs and XCDs take
+  // more groups); s_grp[k % kGrpQ] = the group of step k.
   constexpr uint32_t kGrpQ = 8;
   __shared__ uint32_t s_grp[kGrpQ];
   const uint32_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
   const uint32_t G = gridDim.x;
   // The first two steps are static (groups blockIdx.x and G + blockIdx.x), so the first loads go out at once;
-  // the ticket hands out groups from 2G on, its first claim issued in step 0 like every later one.
-  uint32_t claimed = 2, run = 0, pend = 0;           // wave 0: steps with a group; the pending claim's size
+  // the ticket hands out groups from 2G on, its first claim issued in step 0 like every later one.  Static
+  // groups are safe here, and only here, because nothing in this kernel waits on another workgroup: a workgroup
+  // that has not started yet delays no one (line_kernel, whose groups wait on their predecessors' counts, claims
+  // every group from its ticket: with static first groups two processes' grids sharing a GPU deadlocked, round 4).
+  uint32_t claimed = 2, pend = 0;                    // wave 0: steps with a group; the pending claim's size
   uint32_t claim_res = 0;
   if (threadIdx.x == 0) {
     s_grp[0] = blockIdx.x;
@@ -1883,79 +1553,29 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
   __syncthreads();
   // (the host launches at most one workgroup per group, so s_grp[0] = blockIdx.x < ngroups)
   uint32_t r = s_grp[0] * kMapWaves + (uint32_t)wave;
-#elif DP_MAP_SYNC
-  // every wave of the workgroup runs the workgroup's step count (wave 0 has the most), so the per-step
-  // barrier keeps its 16 waves on adjacent ranges; a wave past the end scans nothing and stores nothing
-  uint32_t r = blockIdx.x * kMapWaves + (uint32_t)wave;
-  const uint32_t r0w = blockIdx.x * kMapWaves;
-  if (r0w >= nranges) return;
-  const uint32_t steps = (nranges - r0w + NW - 1) / NW;
-#else
-  uint32_t r = blockIdx.x * kMapWaves + (uint32_t)wave;
-  if (r >= nranges) return;
-#endif
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
-  MapBuf b[kBufs];
+  BufN b[kBufs];
 #pragma unroll
   for (int h = 0; h < kBufs; ++h) load_bufx(b[h], ScanArgs{M.base}, g, lane, h);
-#if DP_MAP_SYNC == 2 && !DP_MAP_DYN
-  // soft lockstep: a wave starts step it only once every wave of the workgroup has finished step
-  // it - DP_MAP_LEAD - 1 (monotonic per-slot completion counts, no reset), and trails-the-front issue priority
-  __shared__ uint32_t s_done[8];
-  __shared__ uint32_t s_front;
-  if (threadIdx.x < 8) s_done[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_front = 0;
-  __syncthreads();
-#endif
-#if DP_MAP_SYNC || DP_MAP_DYN
   for (uint32_t it = 0;; ++it) {
-#if DP_MAP_SYNC == 2 && !DP_MAP_DYN
-    if (it > (uint32_t)DP_MAP_LEAD) {
-      const uint32_t j = it - DP_MAP_LEAD - 1u;
-      const uint32_t target = kMapWaves * (j / 8u + 1u);
-      uint64_t t0 = 0;
-      for (uint32_t spins = 0; lds_ld(&s_done[j % 8u]) < target; ++spins) {
-        if (wait_expired(spins, t0)) break;
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    {
-      uint32_t front = 0;
-      if (lane == 0) front = __hip_atomic_fetch_max(&s_front, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      front = rfl(front);
-      const uint32_t lag = front > it ? front - it : 0u;
-      set_prio(lag < 3u ? lag : 3u);
-    }
-#else
     __syncthreads();
-#endif
-#else
-  for (;;) {
-#endif
-#if DP_MAP_DYN
     const uint32_t gnext = s_grp[(it + 1) % kGrpQ];
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
     // wave 0 keeps two steps claimed ahead: step it + 2 needs its group by the barrier of step it + 1
-    const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD && s_grp[(claimed - 1) % kGrpQ] < ngroups;
-    if (do_claim) run = s_grp[(claimed - 1) % kGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_MAP_RUN;
-#else
-    const uint32_t rn = r + NW;
-#endif
+    const bool do_claim = wave == 0 && claimed < it + 1u + kMapAhead && s_grp[(claimed - 1) % kGrpQ] < ngroups;
     const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
     FState st{0u, 0u, 0u, -1, 0u, 0u};
     const int lo = (int)g.lo_u, hi = (int)g.hi_u;
     const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
-    uint16_t* evw = sev[kBatch ? (it & 1u) : 0u][wave];
+    uint16_t* evw = sev[wave];
     auto keep = [&](uint32_t rk, uint32_t pos) { evw[rk < kSpillCap - 1u ? rk : kSpillCap - 1u] = (uint16_t)pos; };
-    const uint32_t key = M.delim ^ kSel12;
 #pragma unroll
     for (int h = 0; h < kBufs; ++h) {
       wait_bufx(b[h]);                                // this buffer landed; the other stays in flight
-#if DP_MAP_DYN
       if (h == 0 && do_claim) {                       // the youngest vector-memory operation until the next wait
-        claim_res = atomic_add_nowait(M.ticket, run);
-        pend = run;
+        claim_res = atomic_add_nowait(M.ticket, 1u);
+        pend = 1u;
       }
       if (h == kBufs - 1 && pend) {                   // the wait above covered the claim: its value is back
         asm volatile("" : "+v"(claim_res) :: "memory");
@@ -1965,41 +1585,19 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         claimed += pend;
         pend = 0;
       }
-#endif
       v4u x[kRows];
 #pragma unroll
       for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
-      if constexpr (MODE == kFasta) {
-#ifndef DP_MAP_NOSCAN
-        const uint32_t la = lookahead(b[h], M.base, g, h, interior, hi);
-        if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
-        else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
-#else
-        // timing probe (wrong results): the map's loads, barriers, claims and stores without the row scan
-        uint32_t xs = 0;
-#pragma unroll
-        for (int i = 0; i < kRows; ++i) xs ^= x[i].x ^ x[i].y ^ x[i].z ^ x[i].w;
-        st.cnt += __builtin_amdgcn_readfirstlane((int)xs) == 0x12345 ? 1u : 0u;
-#endif
-      } else {
-        if (interior) delim_rows<true>(x, h, lo, hi, key, lane, st.nev, keep);
-        else delim_rows<false>(x, h, lo, hi, key, lane, st.nev, keep);
-      }
+      const uint32_t la = lookahead_s(M.base, g, h, interior, hi);
+      if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
+      else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
       if (h + 1 < kBufs) load_bufx(b[h], ScanArgs{M.base}, gn, lane, h);
     }
     const bool dense = st.nev > kSpillCap;
     const uint32_t n = dense ? 0u : st.nev;
-    // DP_MAP_B1EARLY: the last buffer's reload before the range's record and spill stores (the next step's first
-    // wait then also waits for as many of its loads as there were stores: conservative)
-    if (DP_MAP_B1EARLY) load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
     cbar();
-#ifdef DP_MAP_NOREC
-    // (probe) DP_MAP_NOREC=1: no record stores, 2: no spill stores, 3: neither; the last launch's data stand
-    const bool probe_norec = M.skip_rec && (DP_MAP_NOREC & 1), probe_nospill = M.skip_rec && (DP_MAP_NOREC & 2);
-#else
-    constexpr bool probe_norec = false, probe_nospill = false;
-#endif
-    if constexpr (kDefer) {
+    {
+      // the range's summary (phase_a_rec of a one-range unit) and its first events to the LDS burst buffer
       if (!st.nlseen) st.fV = st.S;
       uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
       if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
@@ -2021,80 +1619,19 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         __syncthreads();
         flush();
       }
-    } else if constexpr (kBatch) {
-      // this range's record and count to LDS (its events are there already); the previous step's group, whose
-      // LDS data every wave completed before this step's barrier, to HBM by one wave (rotating)
-      if (!st.nlseen) st.fV = st.S;
-      uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
-      if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
-      const uint32_t par = it & 1u;
-      if (lane == 0) {
-        const bool valid = (g.fl & kGeoValid) != 0u;
-        const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
-                            ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
-        s_nw[par][wave] = valid ? (n | kNwValid) : 0u;
-        s_rec[par][wave][0] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
-        s_rec[par][wave][1] = range_geo_rec(g);
-        if (wave == 0) s_r0[par] = r;                  // (wave 0's range is the group's first)
-      }
-      if (it > 0 && (uint32_t)wave == ((it - 1u) & 15u)) write_batch(par ^ 1u);
-    } else if constexpr (MODE == kFasta) {
-      // the range's summary (phase_a_rec of a one-range unit) and its events, word-major
-      if (!st.nlseen) st.fV = st.S;
-      uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
-      if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }  // chunk start: the incoming state is reset
-      if (!probe_nospill && (uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
-        const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
-        reinterpret_cast<v4u*>(M.spill)[spill_word((uint32_t)lane, r, M.nranges)] = v;   // re-read soon: cacheable
-      }
-      if (!probe_norec && lane == 0 && (g.fl & kGeoValid)) {
-        const uint32_t fl = st.S | (sT << 1) | (st.fV << 2) | (dense ? kFlDense : 0u) |
-                            ((g.fl & kGeoFirst) ? kRecFirst : 0u) | ((g.fl & kGeoLast) ? kRecLast : 0u);
-        M.rec[fasta_rec_at(r)] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16), fl, g.c};
-        if (!kRec16) M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
-      }
-    } else {
-      // the range's delimiter count and positions, range-major (the placement gathers consecutive events)
-      if ((uint32_t)lane * 8u < n && (g.fl & kGeoValid)) {
-        const v4u v = *reinterpret_cast<const v4u*>(evw + lane * 8);
-        reinterpret_cast<v4u*>(M.spill)[(uint64_t)r * (kSpillCap / 8u) + (uint32_t)lane] = v;
-      }
-      if (lane == 0 && (g.fl & kGeoValid)) {
-        const uint32_t fl = (dense ? kFlDense : 0u) | ((g.fl & kGeoFirst) ? kRecFirst : 0u) |
-                            ((g.fl & kGeoLast) ? kRecLast : 0u);
-        M.rec[2 * (uint64_t)r] = uint4{st.nev, 0u, fl, g.c};
-        M.rec[2 * (uint64_t)r + 1] = range_geo_rec(g);
-      }
     }
-    if (!DP_MAP_B1EARLY) load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
-#ifdef DP_STAMPS
+    load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
+#ifdef DP_DIAG
     n_done += (g.fl & kGeoValid) ? 1u : 0u;
 #endif
-#if DP_MAP_SYNC == 2 && !DP_MAP_DYN
-    if (lane == 0) lds_add(&s_done[it % 8u], 1u);
-#endif
-#if DP_MAP_DYN
-    if (gnext >= ngroups) {                           // uniform (LDS value read after the barrier)
-      if constexpr (kBatch) {                         // the last step's group
-        __syncthreads();
-        if ((uint32_t)wave == (it & 15u)) write_batch(it & 1u);
-      }
-      break;
-    }
-#elif DP_MAP_SYNC
-    if (it + 1 >= steps) break;
-#else
-    if (rn >= nranges) break;
-#endif
+    if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
     g = gn;
   }
   drain_bufsx(b);
-  if constexpr (kDefer) {                             // the last buffered groups, after the last loads
-    __syncthreads();
-    flush();
-  }
-#ifdef DP_STAMPS
+  __syncthreads();                                    // the last buffered groups, after the last loads
+  flush();
+#ifdef DP_DIAG
   // per wave: start and end (100 MHz realtime clock), ranges scanned, the XCC it ran on
   if (lane == 0 && blockIdx.x < kProfMaxGrid) {
     unsigned long long* w = g_prof + ((uint64_t)blockIdx.x * kProfWaves + wave) * kProfSlots;
@@ -2149,12 +1686,6 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   OutT* s_stage = reinterpret_cast<OutT*>(ps.stage);
-  // Staging index of output element i (relative to stage0).  DP_PLACE_SWZ: the 16-byte group g = i / kVec goes to
-  // g ^ ((g >> 4) & 15), a bijection inside each run of 16 groups that keeps a group's elements together: the
-  // threads of a wave write their ranges' runs ~32 elements apart, which linearly fall into one or two LDS banks.
-  constexpr uint32_t kVecS = 16u / sizeof(OutT), kVecSh = sizeof(OutT) == 8 ? 1u : 2u;
-  auto swg = [](uint32_t gi) -> uint32_t { return DP_PLACE_SWZ ? gi ^ ((gi >> 4) & 15u) : gi; };
-  auto swz = [&](uint32_t i) -> uint32_t { return (swg(i >> kVecSh) << kVecSh) | (i & (kVecS - 1u)); };
   if (threadIdx.x == 0) {
     ps.ndense = 0;
     ps.lo = 0;
@@ -2162,8 +1693,8 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
     ps.anydense = 0;
   }
   __syncthreads();
-#ifdef DP_STAMPS
-  // per block (profiling build): realtime stamps at its sections, in g_prof past the map kernel's words
+#ifdef DP_DIAG
+  // per block (diagnostics build): realtime stamps at its sections, in g_prof past the map kernel's words
   unsigned long long* pst = g_prof + ((uint64_t)(512u + (b & 511u)) * kProfWaves) * kProfSlots;
 #define PLACE_STAMP(i) do { if (threadIdx.x == 0 && b < 512u) pst[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
@@ -2175,8 +1706,8 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
   uint4 rc = uint4{0u, 0u, 2u, 0u};                   // identity: no count, state kept
   uint4 rg = uint4{0u, 0u, 0u, 0u};
   if (valid) {
-    rc = PA.rec[fasta_rec_at(r)];
-    rg = kRec16 ? range_geo_rec_tab(T, rc.w, r) : PA.rec[2 * r + 1];
+    rc = PA.rec[r];
+    rg = range_geo_rec_tab(T, rc.w, r);
   }
   const uint32_t cF = rc.x & 0xFFFFu, cT = rc.x >> 16, fl = rc.z;
   // what the placement needs besides the prefix is loaded now, under the scan and the look-back: the
@@ -2286,7 +1817,7 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
         const uint64_t val = obj_off + e + (slot & 1u);
         if (near4g) ovf |= val > 0xFFFFFFFFull;
         if (stage) {
-          if (slot <= last) s_stage[swz((uint32_t)(slot - stage0))] = (OutT)val;
+          if (slot <= last) s_stage[(uint32_t)(slot - stage0)] = (OutT)val;
         } else {
           put<OutT>(A.out, slot < last ? slot : last, val);
         }
@@ -2310,7 +1841,7 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
           for (uint32_t e = 0; e < 8u; ++e) {
             const uint32_t k = k0 + e;
             const uint32_t ev = (w[e >> 1] >> (16u * (e & 1u))) & 0xFFFFu;
-            if (k >= skip && k < lim) s_stage[swz(sb + k)] = o0 + (OutT)(ev + (par ^ (e & 1u)));
+            if (k >= skip && k < lim) s_stage[sb + k] = o0 + (OutT)(ev + (par ^ (e & 1u)));
           }
         };
         if (nev > 0u) emit8s(sw0, 0u);
@@ -2345,14 +1876,14 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
     OutT* o = reinterpret_cast<OutT*>(A.out);
     const uint64_t v0 = (run_lo + kVec - 1u) & ~(uint64_t)(kVec - 1u), v1 = run_hi & ~(uint64_t)(kVec - 1u);
     if (v0 <= v1) {
-      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[swz((uint32_t)(q - stage0))];
-      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[swz((uint32_t)(q - stage0))];
+      for (uint64_t q = run_lo + threadIdx.x; q < v0; q += kPlaceBlock) o[q] = s_stage[(uint32_t)(q - stage0)];
+      for (uint64_t q = v1 + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[(uint32_t)(q - stage0)];
       const v4u* src = reinterpret_cast<const v4u*>(s_stage);
       const uint32_t g0 = (uint32_t)((v0 - stage0) / kVec);
       v4u* dst = reinterpret_cast<v4u*>(o + v0);
-      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[swg(g0 + (uint32_t)g)];
+      for (uint64_t g = threadIdx.x; g < (v1 - v0) / kVec; g += kPlaceBlock) dst[g] = src[g0 + (uint32_t)g];
     } else {                                          // the run lies inside one 16-byte group
-      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[swz((uint32_t)(q - stage0))];
+      for (uint64_t q = run_lo + threadIdx.x; q < run_hi; q += kPlaceBlock) o[q] = s_stage[(uint32_t)(q - stage0)];
     }
   }
   PLACE_STAMP(5);
@@ -2376,7 +1907,7 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
     for (uint32_t i = (uint32_t)wave; i < nd; i += kPW) {
       const uint32_t t = ps.dense[i];
       const uint64_t rr = (uint64_t)b * kPlaceBlock + t;
-      const uint4 rq = kRec16 ? range_geo_rec_tab(T, PA.rec[rr].w, rr) : PA.rec[2 * rr + 1];
+      const uint4 rq = range_geo_rec_tab(T, PA.rec[rr].w, rr);
       dense_b<kFasta, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, ps.dP[t], ps.dS[t], lane);
     }
   }
@@ -2393,22 +1924,15 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
   __shared__ PlaceShared ps;
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) PA.map_ticket[0] = 0u;       // the map kernel is done with it: ready for the next launch
-    ps.blk = DP_PLACE_TICKET ? atomicAdd(&A.ticket[0], 1u) : blockIdx.x;   // claim order: a block only waits on lower,
+    ps.blk = atomicAdd(&A.ticket[0], 1u);            // claim order: a block only waits on lower,
   }                                                   // already running or finished, blocks
   __syncthreads();
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   fasta_place_block<OUT64>(PA, A, T, ps.blk, ps);
 }
 
-// ------------------------------------------------------------------------------------------ DELIM, two kernels
-// The newline index as map_kernel<kDelim> (per 16 KiB range: the delimiter count, and the positions in the
-// range's spill slot, range-major) followed by delim_place_kernel: one workgroup per block of 1024 ranges
-// scans the counts, resolves the block's prefix by a decoupled look-back over block descriptors (counts: an
-// AGG or PREFIX descriptor holds a 48-bit count), and then writes the block's output entries by output
-// index: thread t fills groups of 8 consecutive entries, finding each entry's range by a binary search over
-// the block's prefix counts in LDS and gathering its position from that range's spill slot, so the stores
-// are coalesced 16-byte groups.  Ranges with more than kSpillCap delimiters ("dense") are rescanned from the
-// input by dense_b.  every_k / emit_add / carry and the four output forms are those of the one-pass kernel.
+// ------------------------------------------------------------------------------------------ count look-back
+// Look-back over count descriptors (the newline index's groups: an AGG or PREFIX descriptor holds a 48-bit count).
 __device__ __forceinline__ uint64_t pack_count(uint64_t st, uint64_t count) { return st | (count & 0xFFFFFFFFFFFFull); }
 // the 64-bit sum over the wave (two 32-bit halves through DPP), uniform
 __device__ __forceinline__ uint64_t wave_sum64(uint64_t sum) {
@@ -2464,240 +1988,76 @@ __device__ __forceinline__ bool lb_reduce_count(uint64_t (&d)[kLbPer], uint32_t 
   return true;
 }
 
-struct DPlaceArgs {
-  const uint4* rec;
-  const uint16_t* spill;       // range-major: range r's positions at spill[r * kSpillCap + e]
-  uint64_t nranges;
-  unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
-};
-
-// Round 3: blocks of 64 ranges (one per lane of wave 0) and 16 waves, so a launch has nranges / 64 workgroups:
-// round 2's blocks of 1024 ranges left a 64 MiB CSV launch (466 K entries per block) to four workgroups copying
-// range by range, one dependent load per 64 entries (189 us vs 33 us for the one-pass kernel).  A wave now
-// gathers its four ranges' up to 4 x 512 spill entries with all 32 loads in flight, then stores them.
-#ifndef DP_DPLACE_TICKET   // newline placement blocks in ticket order (0: blockIdx order, A/B only)
-#define DP_DPLACE_TICKET 1
-#endif
-constexpr uint32_t kDPlaceRanges = 64;
-constexpr uint32_t kDPlaceWaves = 16;
-template <int OUT64>
-__global__ void __launch_bounds__(kWave * kDPlaceWaves) delim_place_kernel(DPlaceArgs PA, ScanArgs A,
-                                                                         const uint64_t* __restrict__ tab_lo,
-                                                                         const uint64_t* __restrict__ tab_hi,
-                                                                         const uint64_t* __restrict__ tab_r0) {
-  typedef typename std::conditional<OUT64 == 1, uint64_t,
-                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
-  constexpr uint32_t kDenseBit = 0x80000000u;
-  __shared__ uint32_t s_blk, s_ndense;
-  __shared__ uint64_t s_P;
-  __shared__ uint32_t s_ex[kDPlaceRanges];            // delimiters of the block before range t
-  __shared__ uint32_t s_cnt[kDPlaceRanges];           // range t's delimiters (| kDenseBit: not spilled)
-  __shared__ uint64_t s_off[kDPlaceRanges];           // object offset of range t's first byte + emit_add
-  __shared__ uint32_t s_dense[kDPlaceRanges];
-  const int lane = __lane_id();
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (threadIdx.x == 0) {
-    if (blockIdx.x == 0) PA.map_ticket[0] = 0u;
-#if DP_DPLACE_TICKET
-    s_blk = atomicAdd(&A.ticket[0], 1u);             // claim order: a block only waits on lower blocks
-#else
-    s_blk = blockIdx.x;                              // A/B only: relies on in-order workgroup dispatch
-#endif
-    s_ndense = 0;
-  }
-  __syncthreads();
-  const uint32_t b = s_blk;
-  if (wave == 0) {
-    // one range per lane: its count, the block scan, the block prefix (decoupled look-back), per-range results
-    const uint64_t r = (uint64_t)b * kDPlaceRanges + lane;
-    const bool valid = r < PA.nranges;
-    uint4 rc = uint4{0u, 0u, 0u, 0u}, rg = uint4{0u, 0u, 0u, 0u};
-    if (valid) {
-      rc = PA.rec[2 * r];
-      rg = PA.rec[2 * r + 1];
-    }
-    const uint32_t cnt = rc.x, fl = rc.z;
-    const uint64_t wbase = (uint64_t)rg.x | ((uint64_t)rg.y << 32);
-    uint32_t inc = cnt;
-    inc += dpp32<kRowShr1, 0xF>(inc, 0u);
-    inc += dpp32<kRowShr2, 0xF>(inc, 0u);
-    inc += dpp32<kRowShr4, 0xF>(inc, 0u);
-    inc += dpp32<kRowShr8, 0xF>(inc, 0u);
-    inc += dpp32<kRowBcast15, 0xA>(inc, 0u);
-    inc += dpp32<kRowBcast31, 0xC>(inc, 0u);
-    const uint64_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kWave - 1);
-    uint64_t Pb = 0;
-    if (b > 0) {
-      if (lane == 0) st_desc(&A.desc[b], pack_count(kStatAgg, total) | A.epoch);
-      const uint32_t W = lb_span(b, kNoUnit);
-      uint64_t t0 = 0;
-      for (uint32_t spins = 0;; ++spins) {
-        uint64_t d[kLbPer];
-        lb_load(A, b, W, lane, d);
-        if (lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, Pb)) break;
-        if (wait_expired(spins, t0)) {
-          if (lane == 0) atomicOr(A.err, kErrTimeout);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    }
-    if (lane == 0) {
-      st_desc(&A.desc[b], pack_count(kStatPrefix, Pb + total) | A.epoch);
-      s_P = Pb;
-    }
-    const uint32_t ex = inc - cnt;
-    const uint64_t P = Pb + ex;                       // delimiters of the launch before this range
-    const bool dense = (fl & kFlDense) != 0u;
-    s_ex[lane] = ex;
-    s_cnt[lane] = valid ? (cnt | (dense ? kDenseBit : 0u)) : 0u;
-    s_off[lane] = A.obj_base - A.shift + wbase + A.emit_add;
-    if (valid && dense) s_dense[atomicAdd(&s_ndense, 1u)] = (uint32_t)lane;
-    if (valid) {
-      if (fl & kRecLast) A.chunk_end[rc.w] = P + cnt;
-      if (r + 1 == PA.nranges) A.total[0] = P + cnt;
-      if constexpr (OUT64 == 2) {
-        // the entries before every 64 KiB boundary that starts a range of this chunk (see phase_b)
-        const uint64_t off0 = A.obj_base - A.shift + wbase;
-        const uint64_t j = (off0 >> 16) - A.tab_j0;
-        const bool holds = (rg.z & 0xFFFFu) == 0u && (rg.z >> 16) != 0u;
-        if ((off0 & 0xFFFFull) == 0 && holds && off0 >= (A.tab_j0 << 16) && j < A.tab_n) A.blocktab[j] = P;
-      }
-    }
-  }
-  __syncthreads();
-  const uint64_t Pb = s_P;
-  // output entries: the selected delimiters (global ordinal G = launch ordinal + carry with G % k == k - 1)
-  // go to index G / k - carry / k.  A range's launch ordinals are o0 + e for its spill entries e; the selected
-  // ones are e0, e0 + k, ... at consecutive output indexes from q0.  A wave takes one range at a time: lane l
-  // gathers entries l, l + 64, ..., all eight loads issued before the first store (at most 512 entries).
-  const uint64_t k = rfl64(A.every_k), carry = rfl64(A.carry);
-  const uint64_t cap = A.cap;
-  OutT* out = reinterpret_cast<OutT*>(A.out);
-  const bool near4g = OUT64 == 0 && !A.wrap32;
-  bool ovf = false;
-  const uint16_t* spb = PA.spill + (uint64_t)b * kDPlaceRanges * kSpillCap;
-  constexpr int kGather = (int)(kSpillCap / kWave);  // 8
-  constexpr int kPer = (int)(kDPlaceRanges / kDPlaceWaves);   // ranges per wave, all gathered at once
-  uint32_t v[kPer][kGather];
-  uint64_t qa[kPer], offa[kPer];
-  uint32_t na[kPer];
-#pragma unroll
-  for (int m = 0; m < kPer; ++m) {
-    const uint32_t tr = (uint32_t)wave + (uint32_t)m * kDPlaceWaves;
-    const uint32_t cw = rfl(s_cnt[tr]);
-    uint32_t e0 = 0, n = cw, step = 1;
-    uint64_t q0 = Pb + rfl(s_ex[tr]);
-    if (k != 1ull) {
-      const uint64_t G0 = q0 + carry;
-      const uint64_t r0 = k - 1ull - G0 % k;
-      e0 = (uint32_t)(r0 < cw ? r0 : cw);
-      n = r0 < cw ? (uint32_t)((cw - r0 + k - 1ull) / k) : 0u;
-      q0 = (G0 + r0) / k - carry / k;
-      step = (uint32_t)k;
-    }
-    if ((cw & kDenseBit) || q0 >= cap) n = 0u;        // written by the dense rescan, or past the capacity
-    else if (q0 + n > cap) n = (uint32_t)(cap - q0);
-    qa[m] = q0;
-    offa[m] = rfl64(s_off[tr]);
-    na[m] = n;
-    const uint16_t* sp = spb + (uint64_t)tr * kSpillCap;
-#pragma unroll
-    for (int j = 0; j < kGather; ++j) {
-      const uint32_t i = (uint32_t)lane + (uint32_t)j * kWave;
-      v[m][j] = i < n ? (uint32_t)sp[e0 + i * step] : 0u;
-    }
-  }
-#pragma unroll
-  for (int m = 0; m < kPer; ++m) {
-#pragma unroll
-    for (int j = 0; j < kGather; ++j) {
-      const uint32_t i = (uint32_t)lane + (uint32_t)j * kWave;
-      if (i < na[m]) {
-        const uint64_t val = offa[m] + v[m][j];
-        if (near4g) ovf |= val > 0xFFFFFFFFull;
-        out[qa[m] + i] = (OutT)val;
-      }
-    }
-  }
-  if (ovf) atomicOr(A.err, kErrOverflow);
-  const uint32_t nd = s_ndense;
-  for (uint32_t i = (uint32_t)wave; i < nd; i += kDPlaceWaves) {
-    const uint32_t td = s_dense[i];
-    const uint64_t rr = (uint64_t)b * kDPlaceRanges + td;
-    const uint4 rq = PA.rec[2 * rr + 1];
-    dense_b<kDelim, OUT64>(A, (uint64_t)rq.x | ((uint64_t)rq.y << 32), rq.z, Pb + s_ex[td], 0u, lane);
-  }
-}
-
 // ------------------------------------------------------------------------------------------ DELIM, lockstep one pass
 // line_kernel<OUT64>: the newline index in ONE kernel with the map kernel's geometry (round 4).  A workgroup of
 // 16 waves scans a group of 16 consecutive 16 KiB ranges per step (claimed from a ticket, a barrier per step,
-// exactly map_kernel<kDelim>'s streaming loop), but keeps each range's delimiter positions in LDS instead of
+// exactly the FASTA map_kernel's streaming loop), but keeps each range's delimiter positions in LDS instead of
 // spilling them to HBM, and places them itself once the group's prefix is known:
 //   * step k: phase A of group g_k -> LDS slot k % kLineSlots (positions, count, geometry per wave);
 //   * step k + 1: wave 0 publishes g_k's delimiter count as an AGG descriptor right after the barrier (every
 //     wave wrote its count before it), and at the step's end loads the look-back window of its oldest
-//     unresolved group (512 group descriptors, by LDS-DMA: no VGPR held in flight);
+//     unresolved group (group descriptors, by LDS-DMA: no VGPR held in flight);
 //   * step k + 2: wave 0 reduces that window after its second buffer wait (no stall); a resolved group gets its
 //     PREFIX descriptor, every range's launch prefix in LDS and the slot's `res` tag; after their rows, the
 //     waves claim the resolved step's 16 ranges from an LDS counter and copy each range's positions to their
 //     final index (place_delims), so the waves that finish first place most of them.
 // A wave only blocks when the slot it is about to overwrite still holds unclaimed ranges (its group's
-// predecessors are late); wave 0 then resolves in the foreground.  No spill round trip (the two-kernel form moves every
+// predecessors are late); wave 0 then resolves in the foreground.  No spill round trip (round 3's map + placement newline form moved every
 // delimiter through HBM twice more), no coordinator wave and no placement launch (the one-pass look-back
 // kernel's start and tail).  Deadlock-free: a workgroup publishes the AGG of every group it has scanned before
 // it blocks, groups are claimed in increasing order by running workgroups, and a group's prefix depends only
 // on lower groups, so the lowest unresolved group can always resolve.
-#ifndef DP_LINE_SLOTS
-#define DP_LINE_SLOTS 4
-#endif
-#ifndef DP_LINE_CAP
-#define DP_LINE_CAP 640
-#endif
-#ifndef DP_LINE_SHARE      // 1: a step's 16 ranges are placed by whichever waves reach the placement first (claimed
-#define DP_LINE_SHARE 1    // from an LDS counter); 0: every wave places its own range
-#endif
-#ifndef DP_LINE_FASTA      // the FASTA form of line_kernel (DP_FASTA_FORM=line): not yet within the VGPR budget
-#define DP_LINE_FASTA 0    // (its build spills 16-20 B per lane, which the ISA guard refuses)
-#endif
-#ifndef DP_LINE_LA         // A/B: the input buffers with their lookahead dword (map_kernel's Buf)
-#define DP_LINE_LA 0
-#endif
-#ifndef DP_LINE_PRIO       // wave 0's issue priority (it also publishes and resolves the workgroup's groups)
-#define DP_LINE_PRIO 0
-#endif
-#ifndef DP_LINE_DUMMY      // A/B: dummy look-back windows loaded by all 64 lanes (0: by lane 0 only)
-#define DP_LINE_DUMMY 0
-#endif
-#ifndef DP_LINE_PUBW       // the wave that publishes each group's AGG (wave 0 resolves the prefixes)
-#define DP_LINE_PUBW 0
-#endif
-constexpr int kPubWave = DP_LINE_PUBW;
-constexpr bool kLineShare = DP_LINE_SHARE != 0;
-// DP_LINE_B1EARLY 1: b[1]'s reload before the step's placements instead of after them, so the placements run
-// with both buffers in flight; the placement stores are then younger than it, so the next step's first wait also
-// waits for as many of b[1]'s loads (a conservative wait).  With DP_LINE_W0DMA: CSV / VCF 1-4 GiB 1.6-2.1 %
-// faster, a sparse index ('>' in FASTA bytes, uint64) 1-3.7 % slower (profiles/r04/ab/w0b1)
-#ifndef DP_LINE_B1EARLY
-#define DP_LINE_B1EARLY 1
-#endif
-constexpr bool kLineB1Early = DP_LINE_B1EARLY != 0;
-// timing probe only (wrong results): the lockstep scan and its LDS records without any look-back, publication,
-// placement or stall (every step's window loads, descriptor stores and index stores left out)
-#ifdef DP_LINE_SCANONLY
-constexpr bool kScanOnly = true;
-constexpr bool kScanDma = DP_LINE_SCANONLY == 2;    // (2: with the look-back window loads of every step)
-#else
-constexpr bool kScanOnly = false;
-constexpr bool kScanDma = false;
-#endif
-#ifndef DP_LINE_W0DMA      // 1: only wave 0 issues window loads (every other wave's waits count none: one wait per
-                           // wave role, in uniform branches; 0: every wave issues them, lane 0 only but wave 0)
-#define DP_LINE_W0DMA 1
-#endif
-constexpr bool kW0Dma = DP_LINE_W0DMA != 0;
-#ifdef DP_LTL
+// Shipped policies (each against its measured alternatives): 4 slots of 640 positions per range (5-8
+// slots +-0.5 %; a 448 cap turned CSV ranges dense), placement shared by the first waves to arrive, b[1]'s reload
+// before the placements, the look-back window issued at the step's end by wave 0 alone and reduced mid-next step, one
+// group per claim, two-part windows.
+constexpr uint32_t kLineSlots = 4;                 // steps of positions a workgroup holds in LDS
+constexpr uint32_t kLineCap = 640;                 // positions kept per range; more = dense (rescanned)
+static_assert(kLineSlots >= 3 && kLineSlots <= 8, "line slots: phase A, resolution, placement + slack");
+static_assert(kLineCap % 8 == 0 && kLineCap <= 1024, "line cap");
+constexpr uint32_t kLineGrpQ = 16;                 // claimed groups by step (>= slots + claim-ahead + 1)
+static_assert(kLineGrpQ >= kLineSlots + kMapAhead + 1, "group queue spans the pending and claimed steps");
+constexpr uint32_t kLineDense = 0x80000000u;
+constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
+constexpr uint32_t kLineEnd = 128u;                // geo.z: the launch's last range (writes the total)
+// A look-back window (kLineSpan descriptors before a group) arrives by LDS-DMA: kLineWinLoads 16-byte-per-lane
+// loads from an even descriptor index, so 128 descriptors per load cover any kLineSpan before the group.
+// Two parts: the nearest kLbSlots groups (~one round of the grid's claims) are reduced first; when all of them are
+// published and none is resolved, the kLbSlots before them.  So a group's prefix does not wait for the round before
+// it to be resolved, only for its AGGs (published without any dependency): a look-back limited to the round before
+// chained every round's resolution to the last one's, and one late workgroup delayed all later ones.
+constexpr uint32_t kLineSpan = kLbSlots * 2;
+constexpr uint32_t kLineWinLoads = (kLineSpan + 2 + 2 * kWave - 1) / (2 * kWave);
+constexpr uint32_t kLineWin = kLineWinLoads * kWave * 2;
+static_assert(kLineWin >= kLineSpan + 2, "window loads cover kLineSpan descriptors from an even start");
+// lb_window_dma clamps a window to the descriptor array's end: ensure_desc allocates multiples of 1024 descriptors
+static_assert(kLineWin <= 1024, "a look-back window fits in the smallest descriptor array");
+constexpr int kWinN = (int)kLineWinLoads;          // wave 0's window loads per step (no other wave issues any)
+
+struct LineShared {
+  uint16_t ev[kLineSlots][kMapWaves][kLineCap];    // per slot and wave: the range's positions
+  uint4 geo[kLineSlots][kMapWaves];                // {wbase lo, wbase hi, lo_w | flags | hi_w << 16, chunk}
+  uint32_t cnt[kLineSlots][kMapWaves];             // the range's delimiters (| kLineDense)
+  uint32_t ex[kLineSlots][kMapWaves];              // delimiters of the group before the range (wave 0)
+  unsigned long long pw[kLineSlots][kMapWaves];    // the range's launch prefix, valid once res == group + 1
+  unsigned long long tot[kLineSlots];              // the group's delimiters
+  uint32_t res[kLineSlots];
+  uint32_t pclaim[kLineSlots];                     // ranges of the slot's step claimed for placement
+  uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
+  unsigned long long win[kLineWin];                // wave 0: a look-back window's descriptors, by LDS-DMA
+  unsigned long long win_dummy[kLineWin];          // a step's window loads with no group to resolve (never read)
+};
+
+struct LineArgs {
+  const uint8_t* base;          // = ScanArgs::base
+  uint64_t nchunks, nranges;
+  uint64_t desc_cap;            // descriptors allocated (a window load never reads past them)
+  unsigned int* ticket;         // [2] group tickets: this launch claims from ticket[parity] and zeroes the other
+  uint32_t parity;
+  const uint32_t* pick;         // (auto form) the form dp_delim's density probe chose; run only when it is kFormLine
+};
+
+#ifdef DP_DIAG
 #define LTL(step, e) do { const int lw_ = wave == 0 ? 0 : wave == 1 ? 1 : wave == 8 ? 2 : wave == 15 ? 3 : -1; \
     if (lw_ >= 0 && lane == 0 && blockIdx.x < 256 && (uint32_t)(step) < kLtlSteps) \
       g_prof[kLtlBase + (((uint64_t)blockIdx.x * kLtlSteps + (uint32_t)(step)) * kLtlWaves + lw_) * 8 + (e)] = \
@@ -2711,76 +2071,6 @@ __device__ __forceinline__ void vm_wait2(bool first) {
   if (A0 == B0 || first) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(A0) : "memory");
   else asm volatile("s_waitcnt vmcnt(%0)" :: "i"(B0) : "memory");
 }
-// DP_LINE_LATE 1: a step's look-back window is issued at its end (after b[1]'s reload) and reduced after the next
-// step's second buffer wait, so it sees the AGGs the other workgroups published half a step later; 0: issued
-// after b[0]'s reload, reduced at the next step's start
-#ifndef DP_LINE_LATE
-#define DP_LINE_LATE 1
-#endif
-// DP_LINE_LATE 2: issued at the step end before b[1]'s reload, reduced after the next step's b[0] reload and a
-// wait for the window alone (b[1]'s loads may still be in flight: the reduction overlaps them)
-constexpr int kLineLate = DP_LINE_LATE;
-static_assert(kLineLate >= 0 && kLineLate <= 2, "DP_LINE_LATE");
-static_assert(!(kLineB1Early && kLineLate == 2), "DP_LINE_LATE=2 reduces the window at a wait that counts on the window "
-                                                 "being older than b[1]'s reload");
-constexpr uint32_t kLineSlots = DP_LINE_SLOTS;     // steps of positions a workgroup holds in LDS
-constexpr uint32_t kLineCap = DP_LINE_CAP;         // positions kept per range; more = dense (rescanned)
-static_assert(kLineSlots >= 3 && kLineSlots <= 8, "line slots: phase A, resolution, placement + slack");
-static_assert(kLineCap % 8 == 0 && kLineCap <= 1024, "line cap");
-#ifndef DP_LINE_RUN        // consecutive groups per claim (one returning atomic on one address each)
-#define DP_LINE_RUN 1
-#endif
-constexpr uint32_t kLineGrpQ = 16;                 // claimed groups by step (>= slots + claim-ahead + run)
-static_assert(kLineGrpQ >= kLineSlots + DP_MAP_AHEAD + DP_LINE_RUN, "group queue spans the pending and claimed steps");
-constexpr uint32_t kLineDense = 0x80000000u;
-constexpr uint32_t kLineValid = 16u, kLineFirst = 32u, kLineLast = 64u;   // geo.z flag bits (lo_w < 16)
-constexpr uint32_t kLineEnd = 128u;                // geo.z: the launch's last range (writes the total)
-// A look-back window (kLineSpan descriptors before a group) arrives by LDS-DMA: kLineWinLoads 16-byte-per-lane
-// loads from an even descriptor index, so 128 descriptors per load cover any kLineSpan before the group.
-// Two parts (DELIM): the nearest kLbSlots groups (~one round of the grid's claims) are reduced first; when all of
-// them are published and none is resolved, the kLbSlots before them.  So a group's prefix does not wait for the
-// round before it to be resolved, only for its AGGs (published without any dependency): a look-back limited to the
-// round before chained every round's resolution to the last one's, and one late workgroup delayed all later ones.
-#ifndef DP_LINE_LBPARTS
-#define DP_LINE_LBPARTS 2
-#endif
-constexpr uint32_t kLineLbParts = DP_LINE_LBPARTS;
-constexpr uint32_t kLineSpan = kLbSlots * kLineLbParts;
-constexpr uint32_t kLineWinLoads = (kLineSpan + 2 + 2 * kWave - 1) / (2 * kWave);
-constexpr uint32_t kLineWin = kLineWinLoads * kWave * 2;
-static_assert(kLineLbParts == 1 || kLineLbParts == 2, "look-back window parts");
-static_assert(kLineWin >= kLineSpan + 2, "window loads cover kLineSpan descriptors from an even start");
-constexpr int kWinN = (kScanOnly && !kScanDma) ? 0 : (int)kLineWinLoads;   // window loads per step (wave 0)
-constexpr int kWinO = kW0Dma ? 0 : kWinN;                                      // (every other wave)
-
-struct LineShared {
-  uint16_t ev[kLineSlots][kMapWaves][kLineCap];    // per slot and wave: the range's positions
-  uint4 geo[kLineSlots][kMapWaves];                // {wbase lo, wbase hi, lo_w | flags | hi_w << 16, chunk}
-  uint32_t cnt[kLineSlots][kMapWaves];             // the range's delimiters (| kLineDense)
-  uint32_t ex[kLineSlots][kMapWaves];              // delimiters of the group before the range (wave 0)
-  unsigned long long pw[kLineSlots][kMapWaves];    // the range's launch prefix, valid once res == group + 1
-  unsigned long long tot[kLineSlots];              // the group's delimiters
-  uint32_t b16[kLineSlots][kMapWaves];             // low 16 bits of the range's first object offset
-  uint32_t res[kLineSlots];
-  uint32_t pclaim[kLineSlots];                     // DP_LINE_SHARE: ranges of the slot's step claimed for placement
-  uint32_t grp[kLineGrpQ];                         // the group of step k at [k % kLineGrpQ]
-  unsigned long long win[kLineWin];                // wave 0: a look-back window's descriptors, by LDS-DMA
-  unsigned long long win_dummy[kLineWin];          // every other wave's / step's window loads (never read)
-  // FASTA: the range's record {cF | cT << 16, (first '\n' + 1) | events << 16, sF | sT << 1 | fV << 2, 0}, every
-  // range's exclusive prefix function {cF, cT, sF, sT} and true incoming state, the group's function
-  uint4 frec[kLineSlots][kMapWaves];
-  uint4 wex[kLineSlots][kMapWaves];
-  uint32_t sw[kLineSlots][kMapWaves];
-  uint4 gagg[kLineSlots];
-};
-
-struct LineArgs {
-  const uint8_t* base;          // = ScanArgs::base
-  uint64_t nchunks, nranges;
-  uint64_t desc_cap;            // descriptors allocated (a window load never reads past them)
-  unsigned int* ticket;         // [2] group tickets: this launch claims from ticket[parity] and zeroes the other
-  uint32_t parity;
-};
 
 // LDS byte address of a __shared__ object (the LDS-DMA destination base, M0)
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -2803,7 +2093,9 @@ __device__ __forceinline__ uint64_t lb_window_dma(const ScanArgs& A, uint64_t de
   }
   return base;
 }
-// the window of group u from LDS (after a wait that retired its loads), as lb_load lays it out
+// The window of group u from LDS, as lb_load lays it out.  Only after a wait that retired its LDS-DMA loads: the
+// reads are tagged (`; dp_win_read`) and the ISA guard fails any such read that an LDS-DMA load may still be in
+// flight at (isa_guard.py), so a reordered step cannot read another group's or a partial window.
 __device__ __forceinline__ void lb_window_read(const unsigned long long* win, uint64_t base, uint32_t u, int lane,
                                                uint64_t (&d)[kLbPer]) {
   const uint32_t W = u < kLbSlots ? u : kLbSlots;
@@ -2811,7 +2103,10 @@ __device__ __forceinline__ void lb_window_read(const unsigned long long* win, ui
 #pragma unroll
   for (int j = 0; j < kLbPer; ++j) {
     const uint32_t k = kLbPer * rl + j;
-    d[j] = k < W ? win[(uint64_t)(u - 1 - k) - base] : 0ull;
+    const uint32_t idx = k < W ? (uint32_t)((uint64_t)(u - 1 - k) - base) : 0u;
+    uint64_t v;
+    asm volatile("ds_read_b64 %0, %1 ; dp_win_read\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_addr(win + idx)) : "memory");
+    d[j] = k < W ? v : 0ull;
   }
 }
 // Reduce a loaded window of group u: true with the group's launch prefix P once resolvable.
@@ -2827,45 +2122,23 @@ __device__ __forceinline__ bool lb_count_window(const ScanArgs& A, uint32_t u, u
   return lb_reduce_count(d, W, pack_count(kStatPrefix, 0ull), lane, P, all);
 }
 
-
-// A window of FASTA group functions: the prefix count P and line state S entering group u, once resolvable.
-__device__ __forceinline__ bool lb_func_window(const ScanArgs& A, uint32_t u, uint64_t (&d)[kLbPer], int lane, uint64_t& P,
-                                               uint32_t& S) {
-  const uint32_t W = u < kLbSlots ? u : kLbSlots;
-  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
-#pragma unroll
-  for (int j = 0; j < kLbPer; ++j) {
-    const uint32_t k = kLbPer * rl + j;
-    d[j] = k < W ? ((d[j] & kEpochMask) == A.epoch ? d[j] : 0ull) : kIdentDesc;
-  }
-  return lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S);
-}
-
-template <int MODE, int OUT64>
+template <int OUT64>
 __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, ScanArgs A,
                                                                  const uint64_t* __restrict__ tab_lo,
                                                                  const uint64_t* __restrict__ tab_hi,
                                                                  const uint64_t* __restrict__ tab_r0) {
   static_assert(kMapWaves == 16, "line_kernel: one workgroup of 16 waves per CU");
-  constexpr bool kFa = MODE == kFasta;
-  // no lookahead dword in flight for FASTA either (2 VGPRs): the byte after a buffer comes by a scalar load
-#if DP_LINE_LA
-  typedef Buf BufT;
-  constexpr int kLoadsX = kLoadsPerBuf;
-#else
-  typedef BufN BufT;
   constexpr int kLoadsX = kLoadsPerBufN;
-#endif
   __shared__ __attribute__((aligned(16))) LineShared sh;
   const int lane = __lane_id();
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   const uint32_t nranges = (uint32_t)L.nranges, nchunks = (uint32_t)L.nchunks;
   const uint32_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
-  const uint32_t G = gridDim.x;
   unsigned int* ticket = L.ticket + L.parity;
   if (blockIdx.x == 0 && threadIdx.x == 0) L.ticket[L.parity ^ 1u] = 0u;   // the next launch's ticket
-  uint32_t claimed = 2, run = 0, pend = 0, claim_res = 0;
+  if (L.pick != nullptr && *(const cu32s*)(uintptr_t)L.pick != kFormLine) return;   // (uniform) the probe chose the other form
+  uint32_t claimed = 2, pend = 0, claim_res = 0;
   // Every group is claimed from the ticket, the first two as well (one atomic), never assigned by blockIdx: a
   // group then only ever waits on lower groups that running workgroups hold, so a grid need not be resident
   // all at once (two processes' grids sharing a GPU: with static first groups each grid's running workgroups
@@ -2882,12 +2155,10 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t r = sh.grp[0] * kMapWaves + (uint32_t)wave;
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
-  BufT b[kBufs];
+  BufN b[kBufs];
 #pragma unroll
   for (int h = 0; h < kBufs; ++h) load_bufx(b[h], A, g, lane, h);
-  if (DP_LINE_PRIO && wave == 0) set_prio(DP_LINE_PRIO);
   bool ovf = false;
-  uint32_t cur_it = 0;                               // the step the loop is in
   uint32_t nb = 0;                                   // (every wave) the next step to place
   // (wave 0) steps with a published AGG / a resolved prefix, the step of the look-back window in flight and its
   // first descriptor (in registers: kept in LDS they cost wave 0 ~10 dependent LDS round trips per step, and the
@@ -2895,151 +2166,65 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   uint32_t agg_next = 0, res_next = 0, lb_step = 0xFFFFFFFFu;
   uint64_t win_base = 0;
 
-  // phase B of range w of step q (its geometry, count and prefix already read from the slot)
-  auto place_v = [&](uint32_t q, uint32_t w, const uint4 gq, const uint32_t cw, const uint64_t Pw) -> bool {
-    const uint32_t s = q % kLineSlots;
-    if (!(gq.z & kLineValid)) return true;
-    const uint32_t n = cw & ~kLineDense;
-    const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
-    const uint32_t lo_w = gq.z & 15u, hi_w = gq.z >> 16;
-    const uint64_t off0 = A.obj_base - A.shift + wbase;
-    if constexpr (kFa) {
-      // the FASTA fix-up of phase_b / fasta_place_block with the range's true incoming state: drop a start
-      // pending from the previous range, prepend the end of the header pending into it; pairs at 2P - S + i
-      typedef typename std::conditional<OUT64 == 1, uint64_t, uint32_t>::type OutT;
-      const uint4 fr = sh.frec[s][w];
-      const uint32_t S = sh.sw[s][w];
-      const uint32_t cF = fr.x & 0xFFFFu, cT = fr.x >> 16, fn = fr.y & 0xFFFFu, fl = fr.z;
-      const uint32_t fV = (fl >> 2) & 1u;
-      if (lane == 0) {
-        const uint64_t P_incl = Pw + (S ? cT : cF);
-        const uint32_t S_out = S ? (fl >> 1) & 1u : fl & 1u;
-        if (gq.z & kLineLast) {
-          A.chunk_end[gq.w] = P_incl;
-          A.pending[gq.w] = S_out ? (long long)P_incl - 1 : -1ll;
-        }
-        if (gq.z & kLineEnd) A.total[0] = P_incl;
-      }
-      if (cw & kLineDense) {
-        dense_b<kFasta, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, S, lane);
-        return true;
-      }
-      const uint32_t skip = S & fV;
-      const uint32_t pre = (S && !fV && fn) ? 1u : 0u;
-      const uint32_t m = n - skip + pre;
-      const uint64_t b0 = 2 * Pw - S, last = 2 * A.cap - 1;
-      const bool near4g = OUT64 == 0 && off0 + kWaveBytes + 1 > 0xFFFFFFFFull;
-      const uint16_t* evw = sh.ev[s][w];
-      for (uint32_t i = (uint32_t)lane; i < m; i += kWave) {
-        const uint32_t e = (pre && i == 0) ? fn - 1u : (uint32_t)evw[i + skip - pre];
-        const uint64_t slot = b0 + i;
-        const uint64_t val = off0 + e + (slot & 1u);
-        if (near4g) ovf |= val > 0xFFFFFFFFull;
-        put<OutT>(A.out, slot < last ? slot : last, val);
-      }
-      return true;
-    } else {
-      if (lane == 0) {
-        if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
-        if (gq.z & kLineEnd) A.total[0] = Pw + n;
-        if constexpr (OUT64 == 2) {
-          // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
-          const uint64_t j = (off0 >> 16) - A.tab_j0;
-          if ((off0 & 0xFFFFull) == 0 && lo_w == 0 && hi_w != 0 && off0 >= (A.tab_j0 << 16) && j < A.tab_n)
-            A.blocktab[j] = Pw;
-        }
-      }
-#ifdef DP_LINE_NOPLACE
-      return true;    // timing probe only (wrong results): every step's bookkeeping without the index stores
-#endif
-      if (cw & kLineDense) {
-        dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
-        return true;
-      }
-      const uint16_t* evw = sh.ev[s][w];
-      // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
-      ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
-      return true;
-    }
-  };
-  // range w of step q (every LDS read up front: one round trip, the branches would otherwise serialize them)
-  auto place = [&](uint32_t q, uint32_t w) -> bool {
+  // phase B of range w of step q (its geometry, count and prefix read from the slot up front: one LDS round trip)
+  auto place = [&](uint32_t q, uint32_t w) {
     const uint32_t s = q % kLineSlots;
     const uint4 gq = sh.geo[s][w];
     const uint32_t cw = sh.cnt[s][w];
     const uint64_t Pw = sh.pw[s][w];
-    return place_v(q, w, gq, cw, Pw);
+    if (!(gq.z & kLineValid)) return;
+    const uint32_t n = cw & ~kLineDense;
+    const uint64_t wbase = (uint64_t)gq.x | ((uint64_t)gq.y << 32);
+    const uint32_t lo_w = gq.z & 15u, hi_w = gq.z >> 16;
+    const uint64_t off0 = A.obj_base - A.shift + wbase;
+    if (lane == 0) {
+      if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
+      if (gq.z & kLineEnd) A.total[0] = Pw + n;
+      if constexpr (OUT64 == 2) {
+        // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
+        const uint64_t j = (off0 >> 16) - A.tab_j0;
+        if ((off0 & 0xFFFFull) == 0 && lo_w == 0 && hi_w != 0 && off0 >= (A.tab_j0 << 16) && j < A.tab_n)
+          A.blocktab[j] = Pw;
+      }
+    }
+    if (cw & kLineDense) {
+      dense_b<kDelim, OUT64>(A, wbase, lo_w | (hi_w << 16), Pw, 0u, lane);
+      return;
+    }
+    const uint16_t* evw = sh.ev[s][w];
+    // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
+    ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
   };
-  // (wave 0) step q's AGG: the group's count (DELIM) or function of the incoming line state (FASTA) from its 16
-  // ranges (lanes 0..15), with every range's exclusive prefix
+  // (wave 0) step q's AGG: the group's count from its 16 ranges (lanes 0..15), with every range's exclusive prefix
   auto publish_agg = [&](uint32_t q) {
     const uint32_t s = q % kLineSlots;
-    uint64_t agg;
-    if constexpr (kFa) {
-      Func32 w = Func32{0, 0, 0, 1};                   // identity (a range past the end)
-      if (lane < (int)kMapWaves && (sh.geo[s][lane].z & kLineValid)) {
-        const uint4 fr = sh.frec[s][lane];
-        w = Func32{fr.x & 0xFFFFu, fr.x >> 16, fr.z & 1u, (fr.z >> 1) & 1u};
-      }
-      Func32 wi = w;
-      wi = f32_then(f32_dpp<kRowShr1, 0xF>(wi), wi);
-      wi = f32_then(f32_dpp<kRowShr2, 0xF>(wi), wi);
-      wi = f32_then(f32_dpp<kRowShr4, 0xF>(wi), wi);
-      wi = f32_then(f32_dpp<kRowShr8, 0xF>(wi), wi);
-      const Func32 we = f32_dpp<kRowShr1, 0xF>(wi);
-      if (lane < (int)kMapWaves) sh.wex[s][lane] = uint4{we.cF, we.cT, we.sF & 1u, we.sT & 1u};
-      const Func fa{(uint32_t)__builtin_amdgcn_readlane((int)wi.cF, kMapWaves - 1),
-                    (uint32_t)__builtin_amdgcn_readlane((int)wi.cT, kMapWaves - 1),
-                    (uint32_t)__builtin_amdgcn_readlane((int)wi.sF, kMapWaves - 1) & 1u,
-                    (uint32_t)__builtin_amdgcn_readlane((int)wi.sT, kMapWaves - 1) & 1u};
-      if (lane == 0) sh.gagg[s] = uint4{(uint32_t)fa.cF, (uint32_t)fa.cT, fa.sF, fa.sT};
-      agg = pack_agg(fa);
-    } else {
-      const uint32_t c = lane < (int)kMapWaves ? (sh.cnt[s][lane] & ~kLineDense) : 0u;
-      uint32_t inc = c;
-      inc += dpp32<kRowShr1, 0xF>(inc, 0u);
-      inc += dpp32<kRowShr2, 0xF>(inc, 0u);
-      inc += dpp32<kRowShr4, 0xF>(inc, 0u);
-      inc += dpp32<kRowShr8, 0xF>(inc, 0u);
-      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kMapWaves - 1);
-      if (lane < (int)kMapWaves) sh.ex[s][lane] = inc - c;
-      if (lane == 0) sh.tot[s] = total;
-      agg = pack_count(kStatAgg, total);
+    const uint32_t c = lane < (int)kMapWaves ? (sh.cnt[s][lane] & ~kLineDense) : 0u;
+    uint32_t inc = c;
+    inc += dpp32<kRowShr1, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr2, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr4, 0xF>(inc, 0u);
+    inc += dpp32<kRowShr8, 0xF>(inc, 0u);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)inc, kMapWaves - 1);
+    if (lane < (int)kMapWaves) sh.ex[s][lane] = inc - c;
+    if (lane == 0) {
+      sh.tot[s] = total;
+      st_desc(&A.desc[sh.grp[q % kLineGrpQ]], pack_count(kStatAgg, total) | A.epoch);
     }
-    if (lane == 0) st_desc(&A.desc[sh.grp[q % kLineGrpQ]], agg | A.epoch);
     agg_next = q + 1;
   };
-  // (wave 0) a resolved prefix P (and FASTA's incoming line state S): every range's prefix in LDS, the slot's
-  // tag for the other waves, the PREFIX descriptor for the other workgroups
-  auto resolved = [&](uint32_t q, uint64_t P, uint32_t S) {
+  // (wave 0) a resolved prefix P: every range's prefix in LDS, the slot's tag for the other waves, the PREFIX
+  // descriptor for the other workgroups
+  auto resolved = [&](uint32_t q, uint64_t P) {
     const uint32_t s = q % kLineSlots;
     const uint32_t u = sh.grp[q % kLineGrpQ];
-    uint64_t pref;
-    if constexpr (kFa) {
-      if (lane < (int)kMapWaves) {
-        const uint4 wx = sh.wex[s][lane];
-        sh.pw[s][lane] = P + (S ? wx.y : wx.x);
-        const uint32_t sw = S ? wx.w : wx.z;
-        sh.sw[s][lane] = (sh.geo[s][lane].z & kLineFirst) ? 0u : sw;   // a chunk's first range starts afresh
-      }
-      const uint4 ga = sh.gagg[s];
-      pref = pack_prefix(P + (S ? ga.y : ga.x), S ? ga.w : ga.z);
-    } else {
-      (void)S;
-      if (lane < (int)kMapWaves) sh.pw[s][lane] = P + sh.ex[s][lane];   // every range's launch prefix
-      pref = pack_count(kStatPrefix, P + sh.tot[s]);
-    }
+    if (lane < (int)kMapWaves) sh.pw[s][lane] = P + sh.ex[s][lane];   // every range's launch prefix
+    const uint64_t pref = pack_count(kStatPrefix, P + sh.tot[s]);
     cbar();
     if (lane == 0) {
       lds_st(&sh.res[s], u + 1u);
       st_desc(&A.desc[u], pref | A.epoch);
     }
     res_next = q + 1;
-  };
-  auto reduce = [&](uint32_t u, uint64_t (&d)[kLbPer], uint64_t& P, uint32_t& S) -> bool {
-    if constexpr (kFa) return lb_func_window(A, u, d, lane, P, S);
-    S = 0;
-    return lb_count_window(A, u, d, lane, P);
   };
   // (wave 0) resolve every step up to q in the foreground (compiler-waited look-back loads)
   auto resolve_upto = [&](uint32_t q) {
@@ -3060,14 +2245,13 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
         d[j] = ld_desc(&A.desc[k < W ? u - 1 - k : 0u]);
       }
       uint64_t P = 0;
-      uint32_t S = 0;
-      if (reduce(u, d, P, S)) {
-        resolved(res_next, P, S);
+      if (lb_count_window(A, u, d, lane, P)) {
+        resolved(res_next, P);
         continue;
       }
       if (wait_expired(spins++, t0)) {               // give up: flag it and release the waiting waves
         if (lane == 0) atomicOr(A.err, kErrTimeout);
-        resolved(res_next, 0ull, 0u);
+        resolved(res_next, 0ull);
         continue;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -3090,11 +2274,11 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     }
     cbar();
   };
-  // (DP_LINE_SHARE) claim and place ranges of the resolved steps nb .. lim - 1, in order, without blocking: a
-  // claim is one LDS add on the slot's counter; a step whose 16 ranges are all claimed is left behind (nb + 1).
-  // A wave places what it claims before it reaches the next barrier, so a step whose ranges are all claimed
-  // before the barrier is placed after it; the slot stall makes every wave see its next slot's old step all
-  // claimed, and the slot's counter is reset after that barrier, so no claim ever reaches a reused slot.
+  // claim and place ranges of the resolved steps nb .. lim - 1, in order, without blocking: a claim is one LDS add
+  // on the slot's counter; a step whose 16 ranges are all claimed is left behind (nb + 1).  A wave places what it
+  // claims before it reaches the next barrier, so a step whose ranges are all claimed before the barrier is placed
+  // after it; the slot stall makes every wave see its next slot's old step all claimed, and the slot's counter is
+  // reset after that barrier, so no claim ever reaches a reused slot.
   auto help = [&](uint32_t lim) {
     while (nb < lim) {
       const uint32_t s0 = nb % kLineSlots;
@@ -3110,22 +2294,15 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       place(nb, w);
     }
   };
-  // (every wave) place steps nb .. q, waiting for their prefixes (DP_LINE_SHARE: until all their ranges are claimed)
+  // (every wave) place steps nb .. q, waiting for their prefixes, until all their ranges are claimed
   auto place_upto = [&](uint32_t q) {
-    if constexpr (kLineShare) {
-      while (nb <= q) {
-        wait_resolved(nb);
-        help(q + 1u);
-      }
-    } else {
-      for (; nb <= q; ++nb) {
-        wait_resolved(nb);
-        place(nb, (uint32_t)wave);
-      }
+    while (nb <= q) {
+      wait_resolved(nb);
+      help(q + 1u);
     }
   };
 
-  // Vector-memory order per step (vmcnt counts in issue order; shipped knobs DP_LINE_LATE=1, B1EARLY, W0DMA):
+  // Vector-memory order per step (vmcnt counts in issue order):
   // [b1 reload, placement stores, wave 0's window loads of the last step] | barrier | wait b0 (b1, those stores
   // and the window may stay in flight: a conservative count when there were stores) | claim atomic, wave 0's
   // AGG store | rows(0) | b0 reload | wait b1 (only b0's reload in flight: the claim and the window have landed)
@@ -3139,56 +2316,44 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     uint64_t d[kLbPer];
     lb_window_read(sh.win, win_base, u, lane, d);
     uint64_t P = 0;
-    uint32_t S = 0;
-    bool ok;
-    if constexpr (!kFa && kLineLbParts == 2) {
-      bool all = false;
-      ok = lb_count_window(A, u, d, lane, P, &all);
-      if (!ok && all) {                               // (u >= kLbSlots) the part before: its prefix + this sum
-        const uint64_t S1 = P;
-        lb_window_read(sh.win, win_base, u - kLbSlots, lane, d);
-        ok = lb_count_window(A, u - kLbSlots, d, lane, P);
-        P += S1;
-      }
-    } else {
-      ok = reduce(u, d, P, S);
+    bool all = false;
+    bool ok = lb_count_window(A, u, d, lane, P, &all);
+    if (!ok && all) {                                 // (u >= kLbSlots) the part before: its prefix + this sum
+      const uint64_t S1 = P;
+      lb_window_read(sh.win, win_base, u - kLbSlots, lane, d);
+      ok = lb_count_window(A, u - kLbSlots, d, lane, P);
+      P += S1;
     }
-    if (ok) resolved(q, P, S);
+    if (ok) resolved(q, P);
   };
-  // Wave 0 (every wave with DP_LINE_W0DMA=0) issues the window's kLineWinLoads LDS-DMA loads once per step, so
-  // its waits have one count on every path (a count per path inside one branch made the compiler merge b[1]'s
-  // registers through copies above the wait; one count per wave role, in uniform branches, does not).  Only the
-  // window of wave 0's oldest unresolved group with a published AGG is read; the other loads (no such group, or
-  // the other waves) land in a dummy area and are never read.
+  // Wave 0 issues the window's kLineWinLoads LDS-DMA loads once per step, so its waits have one count on every
+  // path (a count per path inside one branch made the compiler merge b[1]'s registers through copies above the
+  // wait; one count per wave role, in uniform branches, does not).  Only the window of wave 0's oldest unresolved
+  // group with a published AGG is read; with no such group the loads are lane 0's 16 bytes each (the count is per
+  // instruction, the bytes per active lane) into a dummy area that is never read.
   auto issue_window = [&]() {
-    if (kScanOnly && !kScanDma) return;
-    const bool want = wave == 0 && (kScanDma || res_next < agg_next);
-    const uint32_t u = want ? sh.grp[(kScanDma ? cur_it : res_next) % kLineGrpQ] : 0u;
+    const bool want = wave == 0 && res_next < agg_next;
+    const uint32_t u = want ? sh.grp[res_next % kLineGrpQ] : 0u;
     uint64_t base = 0;
-    // a dummy window is lane 0's 16 bytes per load (the count is per instruction, the bytes per active lane)
-    if ((!kW0Dma || wave == 0) && (want || lane == 0 || DP_LINE_DUMMY))
-      base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
+    if (wave == 0 && (want || lane == 0)) base = lb_window_dma(A, L.desc_cap, u, want ? sh.win : sh.win_dummy, lane);
     if (want) {
       win_base = base;
       lb_step = res_next;
     }
   };
   static_assert(kBufs == 2, "line_kernel: two input buffers per range");
-  if (kLineLate) issue_window();                      // (a dummy: the first step's wait counts a window)
+  issue_window();                                     // (a dummy: the first step's wait counts a window)
   uint32_t it = 0;
   for (;; ++it) {
     __syncthreads();
-    cur_it = it;
     LTL(it, 0);
-    if (kLineShare && threadIdx.x == 0) sh.pclaim[it % kLineSlots] = 0u;   // its old step: placed (last stall)
+    if (threadIdx.x == 0) sh.pclaim[it % kLineSlots] = 0u;   // its old step: placed (last stall)
     const uint32_t gnext = sh.grp[(it + 1) % kLineGrpQ];
     const uint32_t rn = gnext < ngroups ? gnext * kMapWaves + (uint32_t)wave : nranges;
-    const bool do_claim = wave == 0 && claimed < it + 1u + (uint32_t)DP_MAP_AHEAD &&
-                          sh.grp[(claimed - 1) % kLineGrpQ] < ngroups;
-    if (do_claim) run = sh.grp[(claimed - 1) % kLineGrpQ] + (uint32_t)DP_MAP_TAIL * G >= ngroups ? 1u : (uint32_t)DP_LINE_RUN;
+    const bool do_claim = wave == 0 && claimed < it + 1u + kMapAhead && sh.grp[(claimed - 1) % kLineGrpQ] < ngroups;
     const Geo gn = range_geo(T, nchunks, nranges, rn, cur);
     const uint32_t slot = it % kLineSlots;
-    FState st{0u, 0u, 0u, -1, 0u, 0u};               // DELIM: st.nev only
+    uint32_t nev = 0;
     const int lo = (int)g.lo_u, hi = (int)g.hi_u;
     const bool interior = lo == 0 && hi > kWaveBytes;   // wave-uniform
     uint16_t* evw = sh.ev[slot][wave];
@@ -3197,49 +2362,30 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     auto rows = [&](int h) {
 #pragma unroll
       for (int i = 0; i < kRows; ++i) x[i] = b[h].x[i];
-      if constexpr (kFa) {
-        // the first dword after this buffer (a scalar load through the constant address space: it waits on
-        // lgkmcnt, never on the hand-counted vmcnt); read only where that byte lies inside the chunk, the
-        // range's own first dword elsewhere (always in the buffer)
-        const uint32_t la = lookahead_s(A.base, g, h, interior, hi);
-        if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
-        else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
-      } else {
-        if (interior) delim_rows<true>(x, h, lo, hi, key, lane, st.nev, keep);
-        else delim_rows<false>(x, h, lo, hi, key, lane, st.nev, keep);
-      }
+      if (interior) delim_rows<true>(x, h, lo, hi, key, lane, nev, keep);
+      else delim_rows<false>(x, h, lo, hi, key, lane, nev, keep);
     };
     // ---- buffer 0
-    // the youngest operations in flight: b[1]'s loads (and, kLineLate, the window issued after them)
-    vm_wait2<kLoadsX + (kLineLate ? kWinN : 0), kLoadsX + (kLineLate ? kWinO : 0)>(wave == 0);
+    // the youngest operations in flight: b[1]'s loads and, for wave 0, the window issued after them
+    vm_wait2<kLoadsX + kWinN, kLoadsX>(wave == 0);
     touch_bufx(b[0]);
     __builtin_amdgcn_sched_barrier(0);
     LTL(it, 1);
     if (do_claim) {
-      claim_res = atomic_add_nowait(ticket, run);
-      pend = run;
+      claim_res = atomic_add_nowait(ticket, 1u);
+      pend = 1u;
     }
-    if (!kScanOnly && wave == 0) {
-      if (!kLineLate) consume();                      // issued a step ago, older than b[1]'s loads: landed
-      // every wave wrote step it - 1's summary before the barrier: its AGG goes out before anything blocks
-      if (kPubWave == 0 && it > 0) publish_agg(it - 1);
-      if (kPubWave != 0) agg_next = it;                // published by wave kPubWave in this step
-    }
-    if (!kScanOnly && kPubWave != 0 && wave == kPubWave && it > 0) publish_agg(it - 1);
+    // every wave wrote step it - 1's summary before the barrier: its AGG goes out before anything blocks
+    if (wave == 0 && it > 0) publish_agg(it - 1);
     LTL(it, 2);
     rows(0);
     load_bufx(b[0], A, gn, lane, 0);
-    if (kLineLate == 0) issue_window();
-    if (kLineLate == 2) {                             // in flight: b[1]'s loads, the claim, b[0]'s reload
-      asm volatile("s_waitcnt vmcnt(%0)" :: "i"(2 * kLoadsX) : "memory");
-      if (!kScanOnly && wave == 0) consume();
-    }
     // ---- buffer 1
     LTL(it, 3);
-    vm_wait2<kLoadsX + (kLineLate ? 0 : kWinN), kLoadsX + (kLineLate ? 0 : kWinO)>(wave == 0);   // b[0] (+ window) in flight
+    vm_wait2<kLoadsX, kLoadsX>(wave == 0);            // b[0]'s reload in flight: the window and the claim have landed
     touch_bufx(b[1]);
     __builtin_amdgcn_sched_barrier(0);
-    if (kLineLate == 1 && !kScanOnly && wave == 0) consume();   // issued at the end of the last step, before b[0]'s reload
+    if (wave == 0) consume();                         // issued at the end of the last step, before b[0]'s reload
     if (pend) {                                       // the wait above covered the claim: its value is back
       asm volatile("" : "+v"(claim_res) :: "memory");
       const uint32_t u = rfl(claim_res);
@@ -3253,47 +2399,24 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     cbar();
     if (lane == 0) {
       const bool valid = (g.fl & kGeoValid) != 0u;
-      sh.cnt[slot][wave] = valid ? (st.nev | (st.nev > kLineCap ? kLineDense : 0u)) : 0u;
+      sh.cnt[slot][wave] = valid ? (nev | (nev > kLineCap ? kLineDense : 0u)) : 0u;
       sh.geo[slot][wave] = uint4{(uint32_t)g.ubase, (uint32_t)(g.ubase >> 32),
                                  g.lo_u | (valid ? kLineValid : 0u) | ((g.fl & kGeoFirst) ? kLineFirst : 0u) |
                                      ((g.fl & kGeoLast) ? kLineLast : 0u) | (r + 1u == nranges ? kLineEnd : 0u) |
                                      (g.hi_u << 16),
                                  g.c};
-      if constexpr (kFa) {
-        // the range's function of its incoming line state (phase_a_rec / map_kernel's record)
-        if (!st.nlseen) st.fV = st.S;
-        uint32_t cT = st.cnt - st.fV, sT = st.nlseen ? st.S : 1u;
-        if (g.fl & kGeoFirst) { cT = st.cnt; sT = st.S; }   // chunk start: the incoming state is reset
-        sh.frec[slot][wave] = uint4{st.cnt | (cT << 16), (uint32_t)(st.fn + 1) | (st.nev << 16),
-                                    st.S | (sT << 1) | (st.fV << 2), 0u};
-      } else {
-        sh.b16[slot][wave] = (uint32_t)(A.obj_base - A.shift + g.ubase) & 0xFFFFu;
-      }
     }
-    // this step's placements: the ranges of every older step whose prefix is known (DP_LINE_SHARE: any of
-    // them, claimed, so the waves that finish their rows first place most of them; else this wave's own, in
-    // order); then, if the next step's slot still holds an unclaimed range, block for it here (a claimed range is
-    // placed before its wave reaches the next barrier).  Blocking holds back this workgroup's AGG of step it, its
-    // newest group, while it waits for an older one: the lowest waiting group never depends on a held AGG.
+    // this step's placements: any range of an older step whose prefix is known, claimed, so the waves that finish
+    // their rows first place most of them; then, if the next step's slot still holds an unclaimed range, block for
+    // it here (a claimed range is placed before its wave reaches the next barrier).  Blocking holds back this
+    // workgroup's AGG of step it, its newest group, while it waits for an older one: the lowest waiting group
+    // never depends on a held AGG.
     LTL(it, 5);
-    if (kLineB1Early) load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
-    if constexpr (kLineShare) {
-      if (!kScanOnly) help(it);
-    } else {
-      while (!kScanOnly && nb < it) {
-        if (!resolved_tag(nb)) break;
-        cbar();
-        place(nb, (uint32_t)wave);
-        ++nb;
-      }
-    }
+    load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
+    help(it);
     LTL(it, 6);
-#ifndef DP_LINE_NOSTALL   // (DP_LINE_NOSTALL: timing probe only, wrong results: never block for a slot)
-    if (!kScanOnly && nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
-#endif
-    if (kLineLate == 2) issue_window();
-    if (!kLineB1Early) load_bufx(b[kBufs - 1], A, gn, lane, kBufs - 1);
-    if (kLineLate == 1) issue_window();
+    if (nb + kLineSlots <= it + 1) place_upto(it + 1 - kLineSlots);
+    issue_window();
     LTL(it, 7);
     if (gnext >= ngroups) break;                      // uniform (LDS value read after the barrier)
     r = rn;
@@ -3303,12 +2426,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
   if (wave == 0) lb_step = 0xFFFFFFFFu;
   __syncthreads();                                    // every wave's last summary is in LDS
   LTL(it + 1, 0);
-  if (kScanOnly) return;
-  if (wave == kPubWave) publish_agg(it);
-  if (kPubWave != 0) {
-    __syncthreads();                                  // wave 0 resolves with the group's counts
-    if (wave == 0) agg_next = it + 1;
-  }
+  if (wave == 0) publish_agg(it);
   place_upto(it);
   LTL(it + 1, 1);
   if (ovf) atomicOr(A.err, kErrOverflow);
@@ -3488,28 +2606,65 @@ __global__ void __launch_bounds__(1024) stream_rw_kernel(const uint4* __restrict
   if (acc == 0x9E3779B9u) sink[0] = acc;
 }
 
+// ------------------------------------------------------------------------------------------ newline form probe
+// The newline kernels of a launch above kDelimLineMax bytes follow that launch's own bytes, chosen on the device (no
+// host round trip): one workgroup reads kProbeSamples rows of 1 KiB spread evenly over the launch's ranges (their
+// positions are part of the chunk table, stage_chunks) and counts their delimiters; at least dense_milli / 1000 per
+// KiB picks line_kernel, fewer the one-pass look-back kernel.  Both are then enqueued and the one not picked returns
+// at its first instruction.  A wave's 16 rows are loaded at once (one round trip, a few us per launch).
+constexpr uint32_t kProbeSamples = 256;
+constexpr uint32_t kProbeRowsPerWave = kProbeSamples / 16;
+__global__ void __launch_bounds__(1024) density_probe_kernel(const uint8_t* base, uint32_t delim,
+                                                             const uint64_t* __restrict__ samples, uint64_t dense_milli,
+                                                             uint32_t* pick) {
+  __shared__ uint32_t s_cnt, s_bytes;
+  const int lane = __lane_id();
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t key = delim ^ kSel12;
+  if (threadIdx.x == 0) {
+    s_cnt = 0;
+    s_bytes = 0;
+  }
+  __syncthreads();
+  const cu64* smp = (const cu64*)samples;
+  const int a = lane * 16;
+  uint4 v[kProbeRowsPerWave];
+  int lo[kProbeRowsPerWave], hi[kProbeRowsPerWave];
+#pragma unroll
+  for (uint32_t j = 0; j < kProbeRowsPerWave; ++j) {   // sample = {row start (aligned coordinate), lo | hi << 32}
+    const uint32_t i = wave * kProbeRowsPerWave + j;
+    const uint64_t row = smp[2 * i], w = smp[2 * i + 1];
+    lo[j] = (int)(uint32_t)w;
+    hi[j] = (int)(uint32_t)(w >> 32);
+    // (the 16-byte block holding a range's last byte is read whole, as the scans' bounds-checked loads do)
+    v[j] = (a < hi[j] && a + 16 > lo[j]) ? *reinterpret_cast<const uint4*>(base + row + (uint64_t)a) : uint4{0u, 0u, 0u, 0u};
+  }
+  uint32_t cnt = 0, bytes = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kProbeRowsPerWave; ++j) {
+    cnt += (uint32_t)__popc(mask16(v[j], key) & range16(lo[j] - a, hi[j] - a));
+    bytes += (uint32_t)(hi[j] - lo[j]);
+  }
+  atomicAdd(&s_cnt, cnt);
+  if (lane == 0) atomicAdd(&s_bytes, bytes);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t milli = s_bytes ? (uint64_t)s_cnt * 1024000ull / s_bytes : dense_milli;
+    pick[0] = milli >= dense_milli ? kFormLine : kFormOne;
+  }
+}
+
 // ------------------------------------------------------------------------------------------ host side
 thread_local std::string g_err;
 
-// Newline launches up to this many bytes run as two kernels; larger ones as the one-pass look-back kernel
-// (DP_DELIM_TWOPASS_MAX overrides).  Same box, CSV / VCF / FASTA bytes (profiles/r03/delim2/): the two-kernel
-// form is 4-24 % faster up to 512 MiB (the one-pass kernel's ~35-40 us start and tail), the one-pass kernel
-// 2-28 % faster from 1 GiB (the two-kernel form moves every delimiter through the spill: 4 more bytes each).
-constexpr uint64_t kDelimTwoPassMax = 512ull << 20;
-// Round 4: the default newline form is line_kernel up to this many bytes per launch and the one-pass look-back
-// kernel above.  Same boxes, CSV / VCF (profiles/r04/line*, big*): line_kernel's fixed cost is ~5-15 us against
-// the one-pass kernel's ~30 us, so it is faster up to 1-2 GiB (256 MiB: 67 / 64 us vs 82 / 81; 1 GiB: 219 / 210
-// vs 239 / 229), but its steady state stays at ~5.0-5.2 TB/s of input (one group claim per 256 KiB step and the
-// group look-back chain per round) where the one-pass kernel streams at 5.3-5.9: at 4 GiB 830-906 vs 765-877 us
-// depending on the box, at 16 GiB CSV 3,607 vs 3,401 us, at 32 GiB 7,082 vs 5,855 us.
-constexpr uint64_t kDelimLineMax = 2ull << 30;
-// Above kDelimLineMax the choice follows the delimiter density of the ctx's previous newline launch (round 4, final
-// kernels, bench sizes, same box: CSV (~28 newlines per KiB) 32 GiB line 5,755 vs one-pass 5,896 us; VCF (~12.5 per
-// KiB) 64 GiB line 11,326 vs one-pass 10,838 us, profiles/r04/ab/form_bench2).  Both kernels couple a workgroup's
-// progress to its predecessors' counts through the look-back; the one-pass kernel buffers up to 16 units and
-// 4,096 positions per wave, so its slack shrinks as the density grows, while line_kernel's 4 slots of 640
-// positions per range hold 4 steps at any density: dense input runs line_kernel at every size.  A ctx's first
-// launch (no density yet) takes the one-pass kernel above kDelimLineMax.
+// Newline forms (profiles/r05/ sweeps, every form alternated rep by rep on one box): line_kernel is the
+// faster form at every size for CSV-dense input (~28 newlines per KiB: 2-8 % ahead of the one-pass kernel from 2 to
+// 64 GiB) and up to 4 GiB for sparser input (VCF, ~12.5 per KiB: 2 GiB 0.761 vs 0.735 of 8 TB/s, 4 GiB even);
+// above 4 GiB the one-pass look-back kernel streams sparse input 2-4 % faster (its 16-unit ring and 4,096 positions
+// per wave are slack that sparse input fills slowly, while line_kernel's 4 slots hold 4 steps at any density).  So
+// the default ("auto") takes line_kernel up to kDelimLineMax bytes per launch, and above it lets the density probe
+// pick from the launch's own bytes (kLineDenseMilli).
+constexpr uint64_t kDelimLineMax = 4ull << 30;
 constexpr uint64_t kLineDenseMilli = 20000;     // delimiters per KiB x 1000
 
 int fail(int code, const std::string& msg) {
@@ -3543,40 +2698,37 @@ struct dp_ctx {
   int device = 0;
   hipStream_t own = nullptr, stream = nullptr;
   int cus = 0;
-  int grid = 0;                       // persistent scan grid
+  int grid = 0;                       // persistent one-pass scan grid
   // device workspace
   unsigned long long* d_desc = nullptr;
   uint64_t desc_cap = 0;
   uint32_t desc_epoch = 0;            // last launch's descriptor epoch (0: the array needs zeroing first)
-  uint64_t* d_tab = nullptr;          // chunk_lo | chunk_hi | chunk_u0 | pending | ctrl
+  uint64_t* d_tab = nullptr;          // chunk table + results + control words (stage_chunks)
   uint64_t tab_cap = 0;               // in u64 words
   uint64_t* h_tab = nullptr;          // pinned mirror
   uint64_t h_cap = 0;
   std::vector<uint64_t> last_tab;     // last uploaded table (skip identical re-uploads)
-  uint64_t* d_tab_uploaded = nullptr;
-  // two-kernel FASTA workspace: range summaries and event spill slots (grow-only)
+  // two-kernel FASTA workspace: range records and event spill slots (grow-only)
   uint4* d_rec = nullptr;
   uint16_t* d_spill = nullptr;
   uint64_t rec_cap = 0;               // ranges
-  bool fasta_onepass = false;         // DP_FASTA_ONEPASS=1: the one-pass look-back kernel (A/B only)
-  int fasta_form = 0;                 // 0: map + placement kernels, 1: line_kernel (DP_FASTA_FORM = line | two)
-  uint64_t delim_twopass_max = 0;     // newline launches up to this many bytes take the two-kernel form
-  int delim_form = 4;                 // newline kernels: 4 (default) line_kernel up to kDelimLineMax bytes, one-pass
-                                      // above; 0 round 3's rule (two kernels up to kDelimTwoPassMax, one-pass above);
-                                      // 1 line_kernel, 2 two kernels, 3 one-pass at every size
+  // forms (dp_ctx_set_form): the defaults are the shipped choices; the others are for tests and A/B runs
+  int fasta_form = 0;                 // DP_FORM_FASTA: 0 map + placement kernels, 1 the one-pass look-back kernel
+  int delim_form = 0;                 // DP_FORM_DELIM: 0 auto, 1 line_kernel, 3 one-pass
+  uint64_t delim_line_max = kDelimLineMax;      // DP_FORM_DELIM_LINE_MAX
+  uint64_t delim_dense_milli = kLineDenseMilli;  // DP_FORM_DELIM_DENSE
   uint32_t line_launches = 0;         // line_kernel launches (ticket parity)
-  uint64_t delim_line_max = kDelimLineMax;   // DP_DELIM_LINE_MAX (tests): the hybrid form's size split
-  uint64_t delim_density_milli = 0;   // delimiters per KiB x 1000 of the last newline launch (0: none yet)
-  uint64_t delim_span = 0;            // bytes scanned by the newline launch in flight
+  int delim_launched = 0;             // the newline launch in flight: its form, or 0 (picked on the device)
+  int last_delim_form = 0;            // the kernels the last collected newline launch ran (1 or 3)
   // async call state
-  int inflight = -1;                  // -1 none, kFasta, kDelim, 9 find
+  int inflight = -1;                  // -1 none, kFasta, kDelim
   uint64_t nchunks = 0, cap = 0;
   int out_u64 = 0;
   uint32_t every_k = 1;
   uint64_t carry = 0;
   std::vector<uint64_t> range_map;    // out_mode 3: caller range of each internal range (split at 64 KiB)
-  uint64_t pend_off = 0, ctrl_off = 0;
-  int last_form = -1;                 // the last scan's form on this ctx: 0 one-pass, 1 two kernels
+  uint64_t pend_off = 0, ctrl_off = 0, u0_off = 0;
+  int last_form = -1;                 // the last scan's form on this ctx: 0 one-pass / line, 1 two kernels
   // timing
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;
@@ -3590,16 +2742,11 @@ struct dp_ctx {
 
 std::atomic<uint64_t> g_dev_allocs{0}, g_host_allocs{0};
 
-// The newline kernels for a launch scanning `span` bytes (1 line_kernel, 2 two kernels, 3 one-pass; see
-// kDelimLineMax and kLineDenseMilli for the default's rule)
+// The newline kernels of a launch scanning `span` bytes: 1 line_kernel, 3 one-pass, or 0 when the launch's own bytes
+// decide on the device (auto above delim_line_max)
 static int delim_form_for(const dp_ctx* c, uint64_t span) {
-  switch (c->delim_form) {
-    case 1: return 1;
-    case 2: return 2;
-    case 3: return 3;
-    case 0: return span <= c->delim_twopass_max ? 2 : 3;
-    default: return (span <= c->delim_line_max || c->delim_density_milli >= kLineDenseMilli) ? 1 : 3;
-  }
+  if (c->delim_form == (int)kFormLine || c->delim_form == (int)kFormOne) return c->delim_form;
+  return span <= c->delim_line_max ? (int)kFormLine : 0;
 }
 
 namespace {
@@ -3630,17 +2777,26 @@ int ensure_tab(dp_ctx* c, uint64_t words) {
   }
   return DP_OK;
 }
-int ensure_desc(dp_ctx* c, uint64_t n) {
+// Look-back descriptors for a launch of `n` units / blocks / groups, and the launch's epoch tag (the array is zeroed
+// only when (re)allocated and once every kEpochMax launches).  Multiples of 1024 (line_kernel's windows rely on it).
+int next_epoch(dp_ctx* c, uint64_t n, uint64_t* epoch) {
   if (n > c->desc_cap) {
     if (c->d_desc) HIPCHK(hipFree(c->d_desc));
-    uint64_t cap = ((n + n / 4 + 1023) / 1024) * 1024;
+    c->d_desc = nullptr;
+    c->desc_cap = 0;
+    const uint64_t cap = ((n + n / 4 + 1023) / 1024) * 1024;
     HIPCHK(dev_alloc((void**)&c->d_desc, cap * 8));
     c->desc_cap = cap;
     c->desc_epoch = 0;
   }
+  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {   // fresh array, or the epochs wrapped
+    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
+    c->desc_epoch = 0;
+  }
+  *epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
   return DP_OK;
 }
-int ev_begin(dp_ctx* c, hipEvent_t* e0, hipStream_t s) {
+int ev_begin(dp_ctx* c, hipStream_t s) {
   if (!c->timing) return DP_OK;
   while (c->ev_pool.size() < c->ev_used + 2) {
     hipEvent_t e;
@@ -3649,8 +2805,7 @@ int ev_begin(dp_ctx* c, hipEvent_t* e0, hipStream_t s) {
     HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     c->ev_pool.push_back(e);
   }
-  *e0 = c->ev_pool[c->ev_used];
-  HIPCHK(hipEventRecord(*e0, s));
+  HIPCHK(hipEventRecord(c->ev_pool[c->ev_used], s));
   return DP_OK;
 }
 int ev_end(dp_ctx* c, hipStream_t s) {
@@ -3672,17 +2827,22 @@ int harvest_events(dp_ctx* c) {
 }
 
 // Lay out the chunk table in aligned coordinates and enqueue its upload when it changed.
-// Table layout (u64 words): lo[n] hi[n] u0[n+1] pending[n] chunk_end[n] ctrl[7] (err | total | spare x2 |
-// unit ticket: next unit, workgroups finished | map-kernel group ticket: the same pair; zero between launches |
-// line_kernel's two group tickets: a launch claims from one half and zeroes the other, the next launch's).
+// Table layout (u64 words): lo[n] hi[n] r0[n+1] pending[n] chunk_end[n] ctrl[8] u0[n+1] probe[2 * kProbeSamples]:
+// r0 = each chunk's first 16 KiB range (the two-kernel and lockstep kernels), u0 = its first 240 KiB unit (the one-pass
+// kernel), probe = the density probe's sampled rows; ctrl =
+// err | total | spare x2 (count-only scratch) | the one-pass unit ticket {next unit, workgroups finished} | the map
+// kernel's group ticket (the same pair; zero between launches) | line_kernel's two group tickets (a launch claims
+// from one half and zeroes the other, the next launch's) | the density probe's pick.
 // No per-launch reset: every launch rewrites pending / chunk_end of each non-empty chunk and total (when it
 // has units), so only the upload sets their defaults (-1, ~0, 0) and err = 0.  A launch that sets an err
 // bit drops last_tab, so the next one re-uploads (results of a failed launch are discarded anyway).
+constexpr uint64_t kCtrlWords = 8;
 int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base, const uint64_t* chunks,
-                 uint64_t n, uint64_t* nunits_out, uint64_t unit_bytes = kUnitBytes) {
+                 uint64_t n, uint64_t* nranges_out, uint64_t* nunits_out) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
-  std::vector<uint64_t> tab(3 * n + 1);
-  uint64_t units = 0;
+  const uint64_t words = 5 * n + 1 + kCtrlWords + n + 1 + 2 * kProbeSamples;
+  std::vector<uint64_t> tab(3 * n + 1 + n + 1 + 2 * kProbeSamples);
+  uint64_t ranges = 0, units = 0;
   for (uint64_t i = 0; i < n; ++i) {
     const uint64_t c0 = chunks[2 * i], c1 = chunks[2 * i + 1];
     if (c1 < c0 || c0 < buf_base || c1 > buf_base + buf_len)
@@ -3691,25 +2851,47 @@ int stage_chunks(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf
     const uint64_t lo = c0 - buf_base + shift, hi = c1 - buf_base + shift;
     tab[i] = lo;
     tab[n + i] = hi;
-    tab[2 * n + i] = units;
-    if (hi > lo) units += (hi - (lo & ~15ull) + unit_bytes - 1) / unit_bytes;
+    tab[2 * n + i] = ranges;
+    tab[3 * n + 1 + i] = units;
+    if (hi > lo) {
+      ranges += (hi - (lo & ~15ull) + kWaveBytes - 1) / kWaveBytes;
+      units += (hi - (lo & ~15ull) + kUnitBytes - 1) / kUnitBytes;
+    }
   }
-  tab[3 * n] = units;
-  tab.push_back(unit_bytes);                          // (host-side only: a change of geometry re-uploads)
-  const uint64_t words = 5 * n + 1 + 7;
+  tab[3 * n] = ranges;
+  tab[4 * n + 1] = units;
+  // the density probe's rows: sample i at byte (2i + 1) * span / (2 kProbeSamples) of the chunks' bytes in order, its
+  // 1 KiB row from the 16-byte block holding it, with the row's bytes inside the chunk as [lo, hi)
+  uint64_t span = 0;
+  for (uint64_t i = 0; i < n; ++i) span += tab[n + i] - tab[i];
+  uint64_t* smp = tab.data() + 4 * n + 2;
+  for (uint64_t i = 0, c = 0, before = 0; i < kProbeSamples && span; ++i) {
+    const uint64_t p = ((2 * i + 1) * span) / (2 * kProbeSamples);
+    while (before + (tab[n + c] - tab[c]) <= p) {
+      before += tab[n + c] - tab[c];
+      ++c;
+    }
+    const uint64_t pos = tab[c] + (p - before), row = pos & ~15ull;
+    const uint64_t lo = tab[c] > row ? tab[c] - row : 0, hi = tab[n + c] - row < 1024 ? tab[n + c] - row : 1024;
+    smp[2 * i] = row;
+    smp[2 * i + 1] = lo | (hi << 32);
+  }
   int rc = ensure_tab(c, words);
   if (rc) return rc;
   c->pend_off = 3 * n + 1;
   c->ctrl_off = 5 * n + 1;
+  c->u0_off = c->ctrl_off + kCtrlWords;
   if (tab != c->last_tab) {
     // the pinned mirror may still feed an earlier async copy: wait for the stream before rewriting it
     HIPCHK(hipStreamSynchronize(c->stream));
     memcpy(c->h_tab, tab.data(), (3 * n + 1) * 8);
     memset(c->h_tab + c->pend_off, 0xFF, 2 * n * 8);
-    memset(c->h_tab + c->ctrl_off, 0, 7 * 8);
+    memset(c->h_tab + c->ctrl_off, 0, kCtrlWords * 8);
+    memcpy(c->h_tab + c->u0_off, tab.data() + 3 * n + 1, (n + 1 + 2 * kProbeSamples) * 8);
     HIPCHK(hipMemcpyAsync(c->d_tab, c->h_tab, words * 8, hipMemcpyHostToDevice, c->stream));
     c->last_tab.swap(tab);
   }
+  *nranges_out = ranges;
   *nunits_out = units;
   return DP_OK;
 }
@@ -3731,312 +2913,38 @@ int scan_leave(dp_ctx* c, hipStream_t ss) {
   HIPCHK(hipStreamWaitEvent(c->stream, c->ev_out, 0));
   return DP_OK;
 }
-
-int launch_scan(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t units,
-                void* d_out, int out_u64, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add,
-                uint64_t carry = 0, uint32_t wrap32 = 0, unsigned long long* blocktab = nullptr, uint64_t tab_j0 = 0,
-                uint64_t tab_n = 0) {
-  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
-  ScanArgs a;
-  a.base = d_buf - shift;
-  a.shift = shift;
-  a.obj_base = buf_base;
-  a.nchunks = n;
-  a.nunits = units;
-  a.desc = c->d_desc;
-  a.epoch = 0;
-  if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
-    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
-    cap = 1;
-  }
-  a.out = d_out;
-  a.cap = cap;
-  a.out_u64 = out_u64;
-  a.wrap32 = wrap32;
-  a.blocktab = blocktab;
-  a.tab_j0 = tab_j0;
-  a.tab_n = tab_n;
-  a.carry = carry;
-  a.delim = delim * 0x01010101u;
-  a.every_k = every_k;
-  a.emit_add = emit_add;
-  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
-  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
-  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
-  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
-  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
-  if (units == 0) return DP_OK;
-  int rc = ensure_desc(c, units);
-  if (rc) return rc;
-  a.desc = c->d_desc;
-  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {   // fresh array, or the epochs wrapped
-    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
-    c->desc_epoch = 0;
-  }
-  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
-  // ctrl[4] is the one-pass kernel's unit ticket {next unit, workgroups finished}, which its last workgroup puts
-  // back to zero; a two-kernel launch leaves its placement block ticket there ({nblocks, 0}, zeroed only by the
-  // next map kernel).  A form switch usually re-uploads the table anyway (its unit size differs), but a
-  // one-pass launch after a two-kernel one never relies on that
-  if (c->last_form == 1) HIPCHK(hipMemsetAsync(c->d_tab + c->ctrl_off + 4, 0, 8, c->stream));
-  c->last_form = 0;
-  const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
+// One scan on the device's scan stream: the hand-over, the timing events around the kernels `enq` enqueues on it
+// (one HIP-event span per launch, however many kernels), the hand-back.  The device's lock is held throughout.
+template <class Enq>
+int on_scan_stream(dp_ctx* c, Enq&& enq) {
   DeviceSerial& ds = g_serial[c->device];
   std::lock_guard<std::mutex> lock(ds.m);
   hipStream_t ss = nullptr;
-  rc = scan_enter(c, ds, &ss);
+  int rc = scan_enter(c, ds, &ss);
   if (rc) return rc;
-  hipEvent_t e0;
-  rc = ev_begin(c, &e0, ss);
+  rc = ev_begin(c, ss);
   if (rc) return rc;
-  const uint64_t* tlo = c->d_tab;
-  const uint64_t* thi = c->d_tab + n;
-  const uint64_t* tu0 = c->d_tab + 2 * n;
-  if (mode == kFasta && !out_u64)
-    hipLaunchKernelGGL((scan_kernel<kFasta, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
-  else if (mode == kFasta)
-    hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
-  else if (out_u64 == 2)
-    hipLaunchKernelGGL((scan_kernel<kDelim, 2>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
-  else if (!out_u64)
-    hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
-  else
-    hipLaunchKernelGGL((scan_kernel<kDelim, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
-  HIPCHK(hipGetLastError());
+  rc = enq(ss);
+  if (rc) return rc;
   rc = ev_end(c, ss);
   if (rc) return rc;
   return scan_leave(c, ss);
 }
 
-// Range summaries and spill slots for a two-kernel launch (grow-only).
-int ensure_ranges(dp_ctx* c, uint64_t nranges) {
-  if (nranges >= 0xFFFFFFFFull) return fail(DP_ERR_INVALID, "launch exceeds 2^32 ranges of 16 KiB");
-  if (nranges > c->rec_cap) {
-    if (c->d_rec) HIPCHK(hipFree(c->d_rec));
-    if (c->d_spill) HIPCHK(hipFree(c->d_spill));
-    c->d_rec = nullptr;
-    c->d_spill = nullptr;
-    c->rec_cap = 0;
-    const uint64_t cap_r = nranges + nranges / 8 + 64;
-    HIPCHK(dev_alloc((void**)&c->d_rec, 2 * cap_r * sizeof(uint4)));
-    const hipError_t e = dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t));
-    if (e != hipSuccess) {                             // leave no half-allocated workspace behind
-      (void)hipFree(c->d_rec);
-      c->d_rec = nullptr;
-      c->d_spill = nullptr;
-      return fail(DP_ERR_HIP, std::string("workspace of ") + std::to_string(nranges) + " ranges: " +
-                                  hipGetErrorString(e));
-    }
-    c->rec_cap = cap_r;
-  }
-  return DP_OK;
-}
-
-// The two-kernel FASTA index (map_kernel<kFasta> + fasta_place_kernel) over a chunk table staged with
-// 16 KiB ranges.  Timed as one span: the HIP events bracket both kernels.
-int launch_fasta2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
-                  int out_u64, uint64_t cap) {
+// The arguments every scan kernel shares (a count-only call stores into the ctrl scratch words); the epoch is set by
+// the caller (next_epoch).
+ScanArgs scan_args(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nunits, void* d_out,
+                   int kind, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
+                   uint32_t wrap32, unsigned long long* blocktab, uint64_t tab_j0, uint64_t tab_n) {
   const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
-  if (nranges == 0) return DP_OK;
-  int rc0 = ensure_ranges(c, nranges);
-  if (rc0) return rc0;
-  const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
-  int rc = ensure_desc(c, nblocks);
-  if (rc) return rc;
-  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
-    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
-    c->desc_epoch = 0;
-  }
   ScanArgs a;
   memset(&a, 0, sizeof(a));
   a.base = d_buf - shift;
   a.shift = shift;
   a.obj_base = buf_base;
   a.nchunks = n;
-  a.nunits = nranges;
+  a.nunits = nunits;
   a.desc = c->d_desc;
-  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
-#ifdef DP_STAMPS
-  // perf probe of the diagnostics build only (the placement without its stores): never in the shipped library,
-  // where a stray environment variable would otherwise leave the caller's index unwritten
-  static const bool probe_count_only = getenv("DP_PROBE_PLACE_COUNT_ONLY") != nullptr;
-#else
-  constexpr bool probe_count_only = false;
-#endif
-  const int count_only = (cap == 0 || d_out == nullptr || probe_count_only);
-  if (count_only) {
-    d_out = c->d_tab + c->ctrl_off + 2;
-    cap = 1;
-  }
-  a.out = d_out;
-  a.cap = cap;
-  a.out_u64 = out_u64;
-  a.every_k = 1;
-  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
-  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
-  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
-  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
-  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
-  c->last_form = 1;
-  MapArgs m;
-  m.base = a.base;
-  m.nchunks = n;
-  m.nranges = nranges;
-  m.rec = c->d_rec;
-  m.spill = c->d_spill;
-  m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
-  m.place_ticket = a.ticket;
-  m.delim = 0;
-#ifdef DP_MAP_NOREC
-  static thread_local uint64_t probe_launches = 0;
-  m.skip_rec = probe_launches++ >= 4;               // (the bench's two contexts: their first launches write)
-#endif
-  PlaceArgs pa;
-  pa.map_ticket = m.ticket;
-  pa.rec = c->d_rec;
-  pa.spill = c->d_spill;
-  pa.nranges = nranges;
-  pa.nblocks = nblocks;
-  pa.count_only = count_only;
-  const uint64_t waves_needed = (nranges + kMapWaves - 1) / kMapWaves;
-  const uint64_t wgs = (uint64_t)c->cus * kMapPerCU;
-  const unsigned grid = (unsigned)(waves_needed < wgs ? waves_needed : wgs);
-  const uint64_t* tlo = c->d_tab;
-  const uint64_t* thi = c->d_tab + n;
-  const uint64_t* tr0 = c->d_tab + 2 * n;
-  DeviceSerial& ds = g_serial[c->device];
-  std::lock_guard<std::mutex> lock(ds.m);
-  hipStream_t ss = nullptr;
-  rc = scan_enter(c, ds, &ss);
-  if (rc) return rc;
-  hipEvent_t e0;
-  rc = ev_begin(c, &e0, ss);
-  if (rc) return rc;
-  hipLaunchKernelGGL((map_kernel<kFasta>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
-  HIPCHK(hipGetLastError());
-  if (out_u64)
-    hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
-                       thi, tr0);
-  else
-    hipLaunchKernelGGL((fasta_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo,
-                       thi, tr0);
-  HIPCHK(hipGetLastError());
-  rc = ev_end(c, ss);
-  if (rc) return rc;
-  return scan_leave(c, ss);
-}
-
-// The two-kernel newline index (map_kernel<kDelim> + delim_place_kernel), same staging as launch_fasta2.
-int launch_delim2(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
-                  int kind, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
-                  uint32_t wrap32, unsigned long long* blocktab, uint64_t tab_j0, uint64_t tab_n) {
-  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
-  if (nranges == 0) return DP_OK;
-  int rc = ensure_ranges(c, nranges);
-  if (rc) return rc;
-  const uint64_t nblocks = (nranges + kDPlaceRanges - 1) / kDPlaceRanges;
-  rc = ensure_desc(c, nblocks);
-  if (rc) return rc;
-  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
-    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
-    c->desc_epoch = 0;
-  }
-  ScanArgs a;
-  memset(&a, 0, sizeof(a));
-  a.base = d_buf - shift;
-  a.shift = shift;
-  a.obj_base = buf_base;
-  a.nchunks = n;
-  a.nunits = nranges;
-  a.desc = c->d_desc;
-  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
-  if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
-    d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B)
-    cap = 1;
-  }
-  a.out = d_out;
-  a.cap = cap;
-  a.out_u64 = kind;
-  a.wrap32 = wrap32;
-  a.blocktab = blocktab;
-  a.tab_j0 = tab_j0;
-  a.tab_n = tab_n;
-  a.carry = carry;
-  a.delim = delim * 0x01010101u;
-  a.every_k = every_k;
-  a.emit_add = emit_add;
-  a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
-  a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
-  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
-  a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
-  a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
-  c->last_form = 1;
-  MapArgs m;
-  m.base = a.base;
-  m.nchunks = n;
-  m.nranges = nranges;
-  m.rec = c->d_rec;
-  m.spill = c->d_spill;
-  m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
-  m.place_ticket = a.ticket;
-  m.delim = a.delim;
-  DPlaceArgs pa;
-  pa.rec = c->d_rec;
-  pa.spill = c->d_spill;
-  pa.nranges = nranges;
-  pa.map_ticket = m.ticket;
-  const uint64_t waves_needed = (nranges + kMapWaves - 1) / kMapWaves;
-  const uint64_t wgs = (uint64_t)c->cus * kMapPerCU;
-  const unsigned grid = (unsigned)(waves_needed < wgs ? waves_needed : wgs);
-  const uint64_t* tlo = c->d_tab;
-  const uint64_t* thi = c->d_tab + n;
-  const uint64_t* tr0 = c->d_tab + 2 * n;
-  DeviceSerial& ds = g_serial[c->device];
-  std::lock_guard<std::mutex> lock(ds.m);
-  hipStream_t ss = nullptr;
-  rc = scan_enter(c, ds, &ss);
-  if (rc) return rc;
-  hipEvent_t e0;
-  rc = ev_begin(c, &e0, ss);
-  if (rc) return rc;
-  hipLaunchKernelGGL((map_kernel<kDelim>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
-  HIPCHK(hipGetLastError());
-  if (kind == 1)
-    hipLaunchKernelGGL((delim_place_kernel<1>), dim3((unsigned)nblocks), dim3(kWave * kDPlaceWaves), 0, ss, pa, a, tlo, thi, tr0);
-  else if (kind == 2)
-    hipLaunchKernelGGL((delim_place_kernel<2>), dim3((unsigned)nblocks), dim3(kWave * kDPlaceWaves), 0, ss, pa, a, tlo, thi, tr0);
-  else
-    hipLaunchKernelGGL((delim_place_kernel<0>), dim3((unsigned)nblocks), dim3(kWave * kDPlaceWaves), 0, ss, pa, a, tlo, thi, tr0);
-  HIPCHK(hipGetLastError());
-  rc = ev_end(c, ss);
-  if (rc) return rc;
-  return scan_leave(c, ss);
-}
-
-// The lockstep one-pass kernel (line_kernel) of either index, over the same 16 KiB-range staging as launch_delim2:
-// the newline index (mode kDelim, kind = out_mode's element form) or the FASTA pairs (kFasta, kind = out_u64).
-int launch_line(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, uint64_t n, uint64_t nranges, void* d_out,
-                int kind, uint64_t cap, uint32_t delim, uint32_t every_k, uint32_t emit_add, uint64_t carry,
-                uint32_t wrap32, unsigned long long* blocktab, uint64_t tab_j0, uint64_t tab_n) {
-  const uint64_t shift = (uint64_t)((uintptr_t)d_buf & 15u);
-  if (nranges == 0) return DP_OK;
-  if (nranges >= 0xFFFFFFFFull - kMapWaves) return fail(DP_ERR_INVALID, "launch exceeds 2^32 ranges of 16 KiB");
-  const uint64_t ngroups = (nranges + kMapWaves - 1) / kMapWaves;
-  int rc = ensure_desc(c, ngroups);
-  if (rc) return rc;
-  if (c->desc_epoch == 0 || c->desc_epoch >= kEpochMax) {
-    HIPCHK(hipMemsetAsync(c->d_desc, 0, c->desc_cap * 8, c->stream));
-    c->desc_epoch = 0;
-  }
-  ScanArgs a;
-  memset(&a, 0, sizeof(a));
-  a.base = d_buf - shift;
-  a.shift = shift;
-  a.obj_base = buf_base;
-  a.nchunks = n;
-  a.nunits = nranges;
-  a.desc = c->d_desc;
-  a.epoch = (uint64_t)(++c->desc_epoch) << kEpochShift;
   if (cap == 0 || d_out == nullptr) {                 // count-only call: stores go to a scratch slot
     d_out = c->d_tab + c->ctrl_off + 2;                // ctrl spare words (16 B: one uint64 pair)
     cap = 1;
@@ -4054,47 +2962,142 @@ int launch_line(dp_ctx* c, int mode, const uint8_t* d_buf, uint64_t buf_base, ui
   a.emit_add = emit_add;
   a.err = reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off);
   a.total = reinterpret_cast<unsigned long long*>(c->d_tab + c->ctrl_off + 1);
-  a.ticket = nullptr;
+  a.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 4);
   a.pending = reinterpret_cast<long long*>(c->d_tab + c->pend_off);
   a.chunk_end = reinterpret_cast<unsigned long long*>(c->d_tab + c->pend_off + n);
+  a.pick = nullptr;
+  return a;
+}
+
+// ctrl[4] is the one-pass kernel's unit ticket {next unit, workgroups finished}, which its last workgroup puts back
+// to zero; a two-kernel launch leaves its placement block ticket there ({nblocks, 0}, zeroed only by the next map
+// kernel): zero it before a one-pass launch that follows one (on the ctx stream, ahead of the hand-over).
+int before_onepass(dp_ctx* c) {
+  if (c->last_form == 1) HIPCHK(hipMemsetAsync(c->d_tab + c->ctrl_off + 4, 0, 8, c->stream));
+  c->last_form = 0;
+  return DP_OK;
+}
+
+// The one-pass look-back kernel over the 240 KiB-unit table (a.pick: run only if the density probe picked it).
+int enq_scan(dp_ctx* c, hipStream_t ss, int mode, int kind, const ScanArgs& a) {
+  const uint64_t n = a.nchunks, units = a.nunits;
+  const unsigned grid = (unsigned)(units < (uint64_t)c->grid ? units : (uint64_t)c->grid);
+  const uint64_t* tlo = c->d_tab;
+  const uint64_t* thi = c->d_tab + n;
+  const uint64_t* tu0 = c->d_tab + c->u0_off;
+  if (mode == kFasta && !kind)
+    hipLaunchKernelGGL((scan_kernel<kFasta, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
+  else if (mode == kFasta)
+    hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
+  else if (kind == 2)
+    hipLaunchKernelGGL((scan_kernel<kDelim, 2>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
+  else if (kind == 0)
+    hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
+  else
+    hipLaunchKernelGGL((scan_kernel<kDelim, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
+  HIPCHK(hipGetLastError());
+  return DP_OK;
+}
+
+// Range records and spill slots for a two-kernel FASTA launch (grow-only).
+int ensure_ranges(dp_ctx* c, uint64_t nranges) {
+  if (nranges >= 0xFFFFFFFFull) return fail(DP_ERR_INVALID, "launch exceeds 2^32 ranges of 16 KiB");
+  if (nranges > c->rec_cap) {
+    if (c->d_rec) HIPCHK(hipFree(c->d_rec));
+    if (c->d_spill) HIPCHK(hipFree(c->d_spill));
+    c->d_rec = nullptr;
+    c->d_spill = nullptr;
+    c->rec_cap = 0;
+    const uint64_t cap_r = nranges + nranges / 8 + 64;
+    HIPCHK(dev_alloc((void**)&c->d_rec, cap_r * sizeof(uint4)));
+    const hipError_t e = dev_alloc((void**)&c->d_spill, cap_r * kSpillCap * sizeof(uint16_t));
+    if (e != hipSuccess) {                             // leave no half-allocated workspace behind
+      (void)hipFree(c->d_rec);
+      c->d_rec = nullptr;
+      c->d_spill = nullptr;
+      return fail(DP_ERR_HIP, std::string("workspace of ") + std::to_string(nranges) + " ranges: " +
+                                  hipGetErrorString(e));
+    }
+    c->rec_cap = cap_r;
+  }
+  return DP_OK;
+}
+
+MapArgs map_args(dp_ctx* c, const ScanArgs& a, uint64_t nranges) {
+  MapArgs m;
+  m.base = a.base;
+  m.nchunks = a.nchunks;
+  m.nranges = nranges;
+  m.rec = c->d_rec;
+  m.spill = c->d_spill;
+  m.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 5);
+  m.place_ticket = a.ticket;
+  return m;
+}
+unsigned map_grid(const dp_ctx* c, uint64_t nranges) {
+  const uint64_t groups = (nranges + kMapWaves - 1) / kMapWaves;
+  return (unsigned)(groups < (uint64_t)c->cus ? groups : (uint64_t)c->cus);
+}
+
+// The two-kernel FASTA index (map_kernel + fasta_place_kernel) over the 16 KiB-range table.
+int enq_fasta2(dp_ctx* c, hipStream_t ss, int out_u64, const ScanArgs& a, uint64_t nranges, bool count_only) {
+  const uint64_t n = a.nchunks;
+  const uint64_t nblocks = (nranges + kPlaceBlock - 1) / kPlaceBlock;
+  const MapArgs m = map_args(c, a, nranges);
+  PlaceArgs pa;
+  pa.map_ticket = m.ticket;
+  pa.rec = c->d_rec;
+  pa.spill = c->d_spill;
+  pa.nranges = nranges;
+  pa.nblocks = nblocks;
+  pa.count_only = count_only;
+  const uint64_t* tlo = c->d_tab;
+  const uint64_t* thi = c->d_tab + n;
+  const uint64_t* tr0 = c->d_tab + 2 * n;
+  hipLaunchKernelGGL(map_kernel, dim3(map_grid(c, nranges)), dim3(kWave * kMapWaves), 0, ss, m, tlo, thi, tr0);
+  HIPCHK(hipGetLastError());
+  if (out_u64)
+    hipLaunchKernelGGL((fasta_place_kernel<1>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+  else
+    hipLaunchKernelGGL((fasta_place_kernel<0>), dim3((unsigned)nblocks), dim3(kPlaceBlock), 0, ss, pa, a, tlo, thi, tr0);
+  HIPCHK(hipGetLastError());
+  return DP_OK;
+}
+
+// The lockstep newline kernel (line_kernel) over the 16 KiB-range table (pick: run only if the probe picked it).  The
+// ticket parity advances only once the launch is enqueued: a launch that never ran must not leave the next one
+// claiming from a ticket nobody zeroed.
+int enq_line(dp_ctx* c, hipStream_t ss, int kind, const ScanArgs& a, uint64_t nranges, const uint32_t* pick) {
+  const uint64_t n = a.nchunks;
   LineArgs L;
   L.base = a.base;
   L.nchunks = n;
   L.nranges = nranges;
   L.desc_cap = c->desc_cap;
   L.ticket = reinterpret_cast<unsigned int*>(c->d_tab + c->ctrl_off + 6);
-  L.parity = (c->line_launches++) & 1u;
-  const unsigned grid = (unsigned)(ngroups < (uint64_t)c->cus ? ngroups : (uint64_t)c->cus);
+  L.parity = c->line_launches & 1u;
+  L.pick = pick;
   const uint64_t* tlo = c->d_tab;
   const uint64_t* thi = c->d_tab + n;
   const uint64_t* tr0 = c->d_tab + 2 * n;
-  DeviceSerial& ds = g_serial[c->device];
-  std::lock_guard<std::mutex> lock(ds.m);
-  hipStream_t ss = nullptr;
-  rc = scan_enter(c, ds, &ss);
-  if (rc) return rc;
-  hipEvent_t e0;
-  rc = ev_begin(c, &e0, ss);
-  if (rc) return rc;
-#if DP_LINE_FASTA
-  if (mode == kFasta && kind)
-    hipLaunchKernelGGL((line_kernel<kFasta, 1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
-  else if (mode == kFasta)
-    hipLaunchKernelGGL((line_kernel<kFasta, 0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
-  else
-#else
-  if (mode == kFasta) return fail(DP_ERR_INVALID, "the FASTA line_kernel is not built (DP_LINE_FASTA=0)");
-#endif
-  if (kind == 1)
-    hipLaunchKernelGGL((line_kernel<kDelim, 1>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
-  else if (kind == 2)
-    hipLaunchKernelGGL((line_kernel<kDelim, 2>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
-  else
-    hipLaunchKernelGGL((line_kernel<kDelim, 0>), dim3(grid), dim3(kWave * kMapWaves), 0, ss, L, a, tlo, thi, tr0);
+  const dim3 grid(map_grid(c, nranges)), blk(kWave * kMapWaves);
+  if (kind == 1) hipLaunchKernelGGL((line_kernel<1>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
+  else if (kind == 2) hipLaunchKernelGGL((line_kernel<2>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
+  else hipLaunchKernelGGL((line_kernel<0>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
-  rc = ev_end(c, ss);
-  if (rc) return rc;
-  return scan_leave(c, ss);
+  ++c->line_launches;
+  return DP_OK;
+}
+
+// The density probe of an auto newline launch: its pick goes to ctrl[7].
+int enq_probe(dp_ctx* c, hipStream_t ss, const ScanArgs& a, uint64_t nranges) {
+  const uint64_t n = a.nchunks;
+  (void)n;
+  (void)nranges;
+  hipLaunchKernelGGL(density_probe_kernel, dim3(1), dim3(1024), 0, ss, a.base, a.delim, c->d_tab + c->u0_off + n + 1,
+                     c->delim_dense_milli, reinterpret_cast<uint32_t*>(c->d_tab + c->ctrl_off + 7));
+  HIPCHK(hipGetLastError());
+  return DP_OK;
 }
 
 int check_ctx(dp_ctx* c) {
@@ -4103,10 +3106,10 @@ int check_ctx(dp_ctx* c) {
   return DP_OK;
 }
 
-int collect_ctrl(dp_ctx* c, uint64_t extra_words) {
-  // D2H of [pending (nchunks) | ctrl(4)] and wait
+int collect_ctrl(dp_ctx* c) {
+  // D2H of [pending (nchunks) | chunk_end (nchunks) | ctrl] and wait
   const uint64_t off = c->pend_off;
-  const uint64_t words = c->ctrl_off + 4 - off + extra_words;
+  const uint64_t words = c->ctrl_off + kCtrlWords - off;
   HIPCHK(hipMemcpyAsync(c->h_tab + off, c->d_tab + off, words * 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   int rc = harvest_events(c);
@@ -4155,29 +3158,14 @@ int dp_ctx_create(int device, dp_ctx** out) {
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, kThreads, 0));
     if (o < occ) occ = o;
   }
-  // every workgroup of the persistent grid must be resident (look-back waits on lower units): stay one
-  // block per CU under the occupancy answer (it can over-report by one, MI355X_MICROARCH.md §Residency)
-  // one workgroup (8 waves) per CU: the look-back window is the grid, so G <= 256 keeps it one load
-  int per_cu = 1;
-  const char* env = getenv("DP_BLOCKS_PER_CU");
-  if (env) per_cu = atoi(env);
-  if (per_cu > occ - 1) per_cu = occ - 1;
-  if (per_cu < 1) per_cu = 1;
-  c->grid = c->cus * per_cu;
-  if (c->grid > 256) c->grid = 256;   // one look-back window (G <= 256) per unit
-  const char* onepass = getenv("DP_FASTA_ONEPASS");
-  c->fasta_onepass = onepass && atoi(onepass) != 0;
-  const char* fform = getenv("DP_FASTA_FORM");
-  c->fasta_form = fform && !strcmp(fform, "line") ? 1 : 0;
-  // the two-kernel newline index below kDelimTwoPassMax bytes per launch (DP_DELIM_TWOPASS_MAX overrides)
-  const char* dmax = getenv("DP_DELIM_TWOPASS_MAX");
-  c->delim_twopass_max = dmax ? strtoull(dmax, nullptr, 10) : kDelimTwoPassMax;
-  // newline kernels (A/B): DP_DELIM_FORM = hybrid (default) | line | auto (round 3's choice by size) | two | one
-  const char* form = getenv("DP_DELIM_FORM");
-  c->delim_form = !form ? 4 : !strcmp(form, "line") ? 1 : !strcmp(form, "auto") ? 0 : !strcmp(form, "two") ? 2
-                : !strcmp(form, "one") ? 3 : 4;
-  const char* lmax = getenv("DP_DELIM_LINE_MAX");    // the hybrid form's size split (tests)
-  if (lmax) c->delim_line_max = strtoull(lmax, nullptr, 10);
+  // every workgroup of the one-pass kernel's persistent grid must be resident (look-back waits on lower units):
+  // one 1024-thread workgroup per CU (the occupancy answer can over-report by one, MI355X_MICROARCH.md
+  // §Residency), and G <= 256 keeps a unit's look-back one window
+  if (occ < 1) {
+    delete c;
+    return fail(DP_ERR_HIP, "scan_kernel: no resident workgroup per CU");
+  }
+  c->grid = c->cus < 256 ? c->cus : 256;
   *out = c;
   return DP_OK;
 }
@@ -4285,20 +3273,27 @@ int dp_fasta_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint
   if (nchunks && (!d_buf || !chunks)) return fail(DP_ERR_INVALID, "null buffer/chunks");
   if (cap_pairs && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
   if (buf_base + buf_len > obj_size) return fail(DP_ERR_INVALID, "buffer extends beyond the object");
-  uint64_t units = 0;
-  if (c->fasta_onepass) {
-    rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units);
+  uint64_t nranges = 0, units = 0;
+  rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &nranges, &units);
+  if (rc) return rc;
+  const bool count_only = cap_pairs == 0 || d_out == nullptr;
+  if (c->fasta_form == 1 && units) {                  // the one-pass look-back kernel (A/B)
+    rc = before_onepass(c);
     if (rc) return rc;
-    rc = launch_scan(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0);
-  } else if (c->fasta_form == 1) {                   // the lockstep one-pass kernel
-    rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units, kWaveBytes);
+    ScanArgs a = scan_args(c, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0, 0, 0, nullptr, 0, 0);
+    rc = next_epoch(c, units, &a.epoch);
     if (rc) return rc;
-    rc = launch_line(c, kFasta, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs, 0, 1, 0, 0, 0, nullptr,
-                     0, 0);
-  } else {
-    rc = stage_chunks(c, d_buf, buf_len, buf_base, chunks, nchunks, &units, kWaveBytes);
+    a.desc = c->d_desc;
+    rc = on_scan_stream(c, [&](hipStream_t ss) { return enq_scan(c, ss, kFasta, out_u64, a); });
+  } else if (nranges) {                               // map_kernel + fasta_place_kernel
+    rc = ensure_ranges(c, nranges);
     if (rc) return rc;
-    rc = launch_fasta2(c, d_buf, buf_base, nchunks, units, d_out, out_u64, cap_pairs);
+    ScanArgs a = scan_args(c, d_buf, buf_base, nchunks, nranges, d_out, out_u64, cap_pairs, 0, 1, 0, 0, 0, nullptr, 0, 0);
+    rc = next_epoch(c, (nranges + kPlaceBlock - 1) / kPlaceBlock, &a.epoch);
+    if (rc) return rc;
+    a.desc = c->d_desc;
+    c->last_form = 1;
+    rc = on_scan_stream(c, [&](hipStream_t ss) { return enq_fasta2(c, ss, out_u64, a, nranges, count_only); });
   }
   if (rc) return rc;
   if (nchunks) {
@@ -4333,7 +3328,7 @@ int dp_fasta_result(dp_ctx* c, uint64_t* n_pairs, int64_t* pending, uint64_t* ch
   if (rc) return rc;
   if (c->inflight != kFasta) return fail(DP_ERR_INVALID, "no FASTA scan in flight on this ctx");
   c->inflight = -1;
-  rc = collect_ctrl(c, 0);
+  rc = collect_ctrl(c);
   if (rc) return rc;
   const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
   if (err) c->last_tab.clear();                         // the next launch re-uploads err = 0
@@ -4418,28 +3413,54 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
     if (((uintptr_t)d_out) & 15u) return fail(DP_ERR_INVALID, "out_mode 3 needs a 16-byte aligned output buffer");
   }
   const uint64_t nr = rg.size() / 2;
-  uint64_t units = 0, span = 0;
+  uint64_t nr16 = 0, units = 0, span = 0;
   for (uint64_t i = 0; i < nr; ++i) span += rg[2 * i + 1] - rg[2 * i];
   const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
   const int dform = delim_form_for(c, span);
-  c->delim_span = span;
-  if (dform == 1) {                                   // the lockstep one-pass kernel
-    rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
+  rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &nr16, &units);
+  if (rc) return rc;
+  auto args = [&](uint64_t nu) {
+    return scan_args(c, d_buf, buf_base, nr, nu, d_out, kind, cap, delim, every_k, emit_add, carry, out_mode == 2, tab,
+                     j0, ntab);
+  };
+  const uint64_t ngroups = (nr16 + kMapWaves - 1) / kMapWaves;
+  if (!nr16) {
+    // nothing to scan (every range empty): no launch, the uploaded defaults are the result
+  } else if (dform == (int)kFormLine) {               // the lockstep one-pass kernel
+    ScanArgs a = args(nr16);
+    rc = next_epoch(c, ngroups, &a.epoch);
     if (rc) return rc;
-    rc = launch_line(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
-                     out_mode == 2, tab, j0, ntab);
-  } else if (dform == 2) {                            // two kernels
-    rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units, kWaveBytes);
+    a.desc = c->d_desc;
+    c->last_form = 0;
+    rc = on_scan_stream(c, [&](hipStream_t ss) { return enq_line(c, ss, kind, a, nr16, nullptr); });
+  } else if (dform == (int)kFormOne) {                // the one-pass look-back kernel
+    rc = before_onepass(c);
     if (rc) return rc;
-    rc = launch_delim2(c, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
-                       out_mode == 2, tab, j0, ntab);
-  } else {
-    rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &units);
+    ScanArgs a = args(units);
+    rc = next_epoch(c, units, &a.epoch);
     if (rc) return rc;
-    rc = launch_scan(c, kDelim, d_buf, buf_base, nr, units, d_out, kind, cap, delim, every_k, emit_add, carry,
-                     out_mode == 2, tab, j0, ntab);
+    a.desc = c->d_desc;
+    rc = on_scan_stream(c, [&](hipStream_t ss) { return enq_scan(c, ss, kDelim, kind, a); });
+  } else {                                            // auto: the density probe picks on the device
+    rc = before_onepass(c);
+    if (rc) return rc;
+    ScanArgs a = args(units);
+    rc = next_epoch(c, units > ngroups ? units : ngroups, &a.epoch);
+    if (rc) return rc;
+    a.desc = c->d_desc;
+    const uint32_t* pick = reinterpret_cast<const uint32_t*>(c->d_tab + c->ctrl_off + 7);
+    ScanArgs al = a, ao = a;
+    al.nunits = nr16;
+    ao.pick = pick;
+    rc = on_scan_stream(c, [&](hipStream_t ss) {
+      int r = enq_probe(c, ss, al, nr16);
+      if (!r) r = enq_line(c, ss, kind, al, nr16, pick);
+      if (!r) r = enq_scan(c, ss, kDelim, kind, ao);
+      return r;
+    });
   }
   if (rc) return rc;
+  c->delim_launched = dform;
   c->inflight = kDelim;
   c->nchunks = nr;
   c->cap = cap;
@@ -4455,7 +3476,7 @@ int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint6
   if (c->inflight != kDelim) return fail(DP_ERR_INVALID, "no delimiter scan in flight on this ctx");
   const uint64_t k = c->every_k, carry = c->carry;
   c->inflight = -1;
-  rc = collect_ctrl(c, 0);
+  rc = collect_ctrl(c);
   if (rc) return rc;
   const uint32_t err = (uint32_t)c->h_tab[c->ctrl_off];
   if (err) c->last_tab.clear();                         // the next launch re-uploads err = 0
@@ -4467,7 +3488,8 @@ int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint6
     if (range_end) range_end[c->range_map.empty() ? i : c->range_map[i]] = nd;
   }
   const uint64_t nout = (carry + nd) / k - carry / k;
-  if (c->delim_span) c->delim_density_milli = (nd * 1024000ull) / c->delim_span;
+  c->last_delim_form = c->delim_launched ? c->delim_launched
+                                          : (c->h_tab[c->ctrl_off + 7] == kFormLine ? (int)kFormLine : (int)kFormOne);
   if (n_delims) *n_delims = nd;
   if (n_out) *n_out = nout;
   if (err & kErrTimeout) return fail(DP_ERR_TIMEOUT, "look-back wait timed out");
@@ -4536,8 +3558,7 @@ int dp_stream_rw(dp_ctx* c, const void* d_in, uint64_t bytes, void* d_out, uint3
   hipStream_t ss = nullptr;
   rc = scan_enter(c, ds, &ss);
   if (rc) return rc;
-  hipEvent_t e0;
-  rc = ev_begin(c, &e0, ss);
+  rc = ev_begin(c, ss);
   if (rc) return rc;
   if (write_q16)
     hipLaunchKernelGGL(stream_rw_kernel, dim3((unsigned)(c->cus * bpc)), dim3(1024), 0, ss,
@@ -4588,7 +3609,7 @@ int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slo
   return DP_OK;
 #else
   (void)c; (void)host_words; (void)n_words; (void)slots; (void)waves;
-  return fail(DP_ERR_INVALID, "dp_debug_profile: library built without -DDP_PROF");
+  return fail(DP_ERR_INVALID, "dp_debug_profile: library built without -DDP_DIAG");
 #endif
 }
 
@@ -4598,10 +3619,43 @@ int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs) {
   return DP_OK;
 }
 
-int dp_scan_forms(dp_ctx* c, int* fasta_two_kernel, uint64_t* delim_two_kernel_max) {
+int dp_ctx_set_form(dp_ctx* c, int what, uint64_t value) {
   if (!c) return fail(DP_ERR_INVALID, "null");
-  if (fasta_two_kernel) *fasta_two_kernel = c->fasta_onepass ? 0 : 1;
-  if (delim_two_kernel_max) *delim_two_kernel_max = c->delim_twopass_max;
+  if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is in flight on this ctx");
+  switch (what) {
+    case DP_FORM_FASTA:
+      if (value > 1) return fail(DP_ERR_INVALID, "DP_FORM_FASTA: 0 (map + placement) or 1 (one-pass)");
+      c->fasta_form = (int)value;
+      return DP_OK;
+    case DP_FORM_DELIM:
+      if (value > 3 || value == 2) return fail(DP_ERR_INVALID, "DP_FORM_DELIM: 0 (auto), 1 (line_kernel) or 3 (one-pass)");
+      c->delim_form = (int)value;
+      return DP_OK;
+    case DP_FORM_DELIM_LINE_MAX:
+      c->delim_line_max = value;
+      return DP_OK;
+    case DP_FORM_DELIM_DENSE:
+      c->delim_dense_milli = value;
+      return DP_OK;
+    default:
+      return fail(DP_ERR_INVALID, "unknown form setting " + std::to_string(what));
+  }
+}
+
+int dp_ctx_get_form(dp_ctx* c, int what, uint64_t* value) {
+  if (!c || !value) return fail(DP_ERR_INVALID, "null");
+  switch (what) {
+    case DP_FORM_FASTA: *value = (uint64_t)c->fasta_form; return DP_OK;
+    case DP_FORM_DELIM: *value = (uint64_t)c->delim_form; return DP_OK;
+    case DP_FORM_DELIM_LINE_MAX: *value = c->delim_line_max; return DP_OK;
+    case DP_FORM_DELIM_DENSE: *value = c->delim_dense_milli; return DP_OK;
+    default: return fail(DP_ERR_INVALID, "unknown form setting " + std::to_string(what));
+  }
+}
+
+int dp_last_delim_form(dp_ctx* c, int* form) {
+  if (!c || !form) return fail(DP_ERR_INVALID, "null");
+  *form = c->last_delim_form;
   return DP_OK;
 }
 

@@ -9,7 +9,7 @@ this checks the generated gfx950 assembly: on every control-flow path from a `bu
 returning `buffer_atomic_* … sc0`) into register(s) R until a wait that the load is certain to have completed by (vmcnt(N) with fewer than N
 vector-memory operations issued after it), no instruction may read or write R (dataflow over the
 kernel's basic blocks, tracking the ordered queue of outstanding vector-memory operations).  Every kernel of the
-code object is checked (the scans, the map and placement kernels, resolve/find and the calibration kernels), and
+code object is checked (the scans, the map and placement kernels, the density probe, resolve/find and the calibration kernels), and
 the check fails if any kernel has a scratch segment (register spills or private arrays in memory).
 
     python -m dataplug_amd.isa_guard [path/to/dpscan-hip-amdgcn-amd-amdhsa-gfx950.s]
@@ -28,8 +28,8 @@ SRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc", "dpscan.h
 # every kernel symbol of the device assembly (anonymous-namespace kernels: _ZN12_GLOBAL__N_1<len><name>...)
 KERNEL_RE = re.compile(r"^(_ZN12_GLOBAL__N_1\d+\w+?_kernel\w*):", re.M)
 # kernels the shipped library must contain (a build that lost one is not the library the tests describe)
-REQUIRED = ("scan_kernel", "map_kernel", "fasta_place_kernel", "delim_place_kernel", "line_kernel", "fasta_resolve_kernel",
-            "find_kernel", "stream_kernel", "stream_rw_kernel")
+REQUIRED = ("scan_kernel", "map_kernel", "fasta_place_kernel", "line_kernel",
+            "density_probe_kernel", "fasta_resolve_kernel", "find_kernel", "stream_kernel", "stream_rw_kernel")
 
 
 def compile_asm() -> str:
@@ -66,6 +66,8 @@ def _blocks(body: str):
             continue
         if in_asm and not s.endswith(":"):
             s += " @asm"                          # written by hand (inline asm), not by the compiler
+            if "dp_win_read" in line:
+                s += " @winread"                  # an LDS read of line_kernel's LDS-DMA look-back window
         if s.endswith(":"):
             blocks.append([label, cur])
             label, cur = s[:-1], []
@@ -108,7 +110,10 @@ def _le(a, b):
 def _scan(ins, q, problems, k):
     """Run one block over q, the outstanding vector-memory operations youngest first (vmcnt decrements
     in issue order): each entry is the set of VGPRs an input buffer load will still write (empty for
-    any other load/store, which only takes a counter slot).  `s_waitcnt vmcnt(N)` keeps the N youngest."""
+    any other load/store, which only takes a counter slot; {"lds"} for an LDS-DMA load, whose destination is
+    LDS).  `s_waitcnt vmcnt(N)` keeps the N youngest.  An LDS read tagged `dp_win_read` (line_kernel's
+    look-back window) is a violation while any LDS-DMA load may still be outstanding: it would read another
+    group's or a partial window."""
     q = tuple(q)
     for s in ins:
         toks = re.split(r"[\s,]+", s)
@@ -119,6 +124,9 @@ def _scan(ins, q, problems, k):
                 q = q[:int(m.group(1))]
             continue
         pending = frozenset().union(*q) if q else frozenset()
+        if "@winread" in toks and "lds" in pending:
+            if problems is not None:
+                problems.append((k, s))
         if VMEM_RE.match(op):
             # hand-waited destinations: the input buffer loads and the returning (sc0) ticket atomic
             # (global atomics: only the inline-asm claims are hand-waited; the compiler waits for its own)
@@ -126,7 +134,7 @@ def _scan(ins, q, problems, k):
             if op.startswith("buffer_load_dword") or (op.startswith("buffer_atomic") and "sc0" in toks[1:]) or \
                     (op.startswith("global_atomic") and "sc0" in toks[1:] and "@asm" in toks[1:]) or \
                     (op.startswith("global_load") and "@asm" in toks[1:]):
-                dst = set() if "_lds" in op else regs(toks[1])   # LDS-DMA: no VGPR destination
+                dst = {"lds"} if "_lds" in op else regs(toks[1])   # LDS-DMA: no VGPR destination, LDS pending
                 srcs = set()
                 for t in toks[2:]:
                     srcs |= regs(t)

@@ -23,6 +23,11 @@ DP_ERR_HIP = 2
 DP_ERR_CAPACITY = 3
 DP_ERR_OVERFLOW = 4
 DP_ERR_TIMEOUT = 5
+# dp_ctx_set_form / dp_ctx_get_form settings (include/dpscan.h)
+DP_FORM_FASTA = 0
+DP_FORM_DELIM = 1
+DP_FORM_DELIM_LINE_MAX = 2
+DP_FORM_DELIM_DENSE = 3
 
 # (name, restype, argtypes) for every symbol include/dpscan.h declares
 _c = ctypes
@@ -65,8 +70,10 @@ SIGNATURES = [
     ("dp_timing_read", _c.c_int, [_p, _c.POINTER(_c.c_double), _u64p]),
     ("dp_debug_profile", _c.c_int, [_p, _u64p, _u64, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
     ("dp_alloc_counts", _c.c_int, [_u64p, _u64p]),
-    ("dp_scan_forms", _c.c_int, [_p, _c.POINTER(_c.c_int), _u64p]),
+    ("dp_ctx_set_form", _c.c_int, [_p, _c.c_int, _u64]),
+    ("dp_ctx_get_form", _c.c_int, [_p, _c.c_int, _u64p]),
     ("dp_scan_delim_form", _c.c_int, [_p, _u64, _c.POINTER(_c.c_int)]),
+    ("dp_last_delim_form", _c.c_int, [_p, _c.POINTER(_c.c_int)]),
     ("dp_scan_geometry", _c.c_int, [_p, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
 ]
 

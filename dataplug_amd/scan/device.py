@@ -331,22 +331,36 @@ class ScanContext:
         check(self.lib.dp_timing_read(self.handle, ctypes.byref(ms), ctypes.byref(n)))
         return float(ms.value), int(n.value)
 
-    def forms(self) -> Tuple[int, int]:
-        """(FASTA index form: 1 map + placement kernels, 0 one-pass look-back kernel; largest newline launch in
-        bytes that runs as two kernels)."""
-        f = ctypes.c_int(0)
-        d = ctypes.c_uint64(0)
-        check(self.lib.dp_scan_forms(self.handle, ctypes.byref(f), ctypes.byref(d)))
-        return int(f.value), int(d.value)
+    _FORM_KEYS = {"fasta": _lib.DP_FORM_FASTA, "delim": _lib.DP_FORM_DELIM,
+                  "delim_line_max": _lib.DP_FORM_DELIM_LINE_MAX, "delim_dense": _lib.DP_FORM_DELIM_DENSE}
 
-    DELIM_FORMS = {1: "line_kernel<DELIM> (lockstep one pass)",
-                   2: "map_kernel<DELIM> + delim_place_kernel (one HIP-event span)",
+    def set_form(self, **kw) -> None:
+        """dp_ctx_set_form: fasta=0 (map + placement, default) | 1 (one-pass); delim=0 (auto, default) | 1 (line) |
+        3 (one-pass); delim_line_max=bytes; delim_dense=delimiters per KiB x 1000.  The shipped
+        defaults need no call; tests and A/B runs pin a form with it."""
+        for k, v in kw.items():
+            check(self.lib.dp_ctx_set_form(self.handle, self._FORM_KEYS[k], int(v)))
+
+    def get_form(self, key: str) -> int:
+        v = ctypes.c_uint64(0)
+        check(self.lib.dp_ctx_get_form(self.handle, self._FORM_KEYS[key], ctypes.byref(v)))
+        return int(v.value)
+
+    DELIM_FORMS = {0: "auto: the density probe picks per launch",
+                   1: "line_kernel<DELIM> (lockstep one pass)",
                    3: "scan_kernel<DELIM> (one-pass look-back)"}
 
     def delim_form(self, span: int) -> int:
-        """The kernels a newline launch of ``span`` bytes takes (dp_scan_delim_form: 1 line, 2 two, 3 one-pass)."""
+        """The kernels a newline launch of ``span`` bytes takes (dp_scan_delim_form: 1 line, 3 one-pass; 0: the
+        launch's own bytes decide on the device)."""
         f = ctypes.c_int(0)
         check(self.lib.dp_scan_delim_form(self.handle, int(span), ctypes.byref(f)))
+        return int(f.value)
+
+    def last_delim_form(self) -> int:
+        """The kernels the last collected newline launch ran (dp_last_delim_form: 1 or 3; 0 before any)."""
+        f = ctypes.c_int(0)
+        check(self.lib.dp_last_delim_form(self.handle, ctypes.byref(f)))
         return int(f.value)
 
     def geometry(self) -> Tuple[int, int]:

@@ -4,7 +4,11 @@ Stands in for the MinIO the reference's examples talk to (``examples/fasta_examp
 ``http://127.0.0.1:9000``).  Path-style REST subset: HEAD/PUT bucket, HEAD/GET (``Range``)/PUT/DELETE
 object, ListObjectsV2, ListBuckets; user metadata as ``x-amz-meta-*``.  Unsigned.
 
-    python -m dataplug_amd.storage.server --port 9000 [--put bucket/key=path ...]
+    python -m dataplug_amd.storage.server --port 9000 [--put bucket/key=path ...] [--synth bucket/key=kind,size,seed ...]
+
+``--synth`` materialises one of ``dataplug_amd.synth``'s seeded objects in the server process (kind ``fasta``:
+tiled_fasta_host, ``csv`` / ``vcf``: tiled_csv / tiled_vcf), byte-identical to the client's own copy of the same
+seed, so a benchmark's client and server need not pass gigabytes through a file.
 """
 from __future__ import annotations
 
@@ -192,12 +196,24 @@ class LoopbackS3Server:
         self.stop()
 
 
+def synth_object(kind: str, size: int, seed: int):
+    """The bytes of a seeded synthetic object (numpy uint8), as the client generates them."""
+    from .. import synth
+    if kind == "fasta":
+        return synth.tiled_fasta_host(size, seed=seed)
+    if kind in ("csv", "vcf"):
+        obj = (synth.tiled_csv if kind == "csv" else synth.tiled_vcf)(size, seed=seed)
+        return obj.bytes_range(0, size)
+    raise ValueError(f"synthetic kind {kind!r}: fasta, csv or vcf")
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=9000)
     ap.add_argument("--put", action="append", default=[], metavar="BUCKET/KEY=PATH")
     ap.add_argument("--bucket", action="append", default=[], help="create this (empty) bucket")
+    ap.add_argument("--synth", action="append", default=[], metavar="BUCKET/KEY=KIND,SIZE,SEED")
     args = ap.parse_args(argv)
     srv = LoopbackS3Server(host=args.host, port=args.port)
     for b in args.bucket:
@@ -208,6 +224,12 @@ def main(argv=None):
         srv.store.create_bucket(bucket)
         with open(path, "rb") as f:
             srv.store.put(bucket, key, f.read())
+    for spec in args.synth:
+        dst, _, what = spec.partition("=")
+        bucket, _, key = dst.partition("/")
+        kind, size, seed = what.split(",")
+        srv.store.create_bucket(bucket)
+        srv.store.put(bucket, key, synth_object(kind, int(size), int(seed)))
     print(f"serving {srv.endpoint_url}", flush=True)
     srv.start()
     try:

@@ -151,9 +151,9 @@ int dp_stream_rw(dp_ctx* ctx, const void* d_in, uint64_t bytes, void* d_out, uin
 int dp_timing_enable(dp_ctx* ctx, int enable);
 int dp_timing_read(dp_ctx* ctx, double* total_ms, uint64_t* launches);   /* syncs; then resets */
 
-/* Diagnostics: per (workgroup, wave) in-kernel section timers of the last scan launch (s_memtime ticks,
- * `slots` words per wave, `waves` waves per workgroup).  Only a library built with -DDP_PROF
- * (lib/libdpscan_prof.so) records them; the production build returns DP_ERR_INVALID. */
+/* Diagnostics: the realtime stamps of the last scan launch (map_kernel per wave, fasta_place_kernel per block,
+ * line_kernel per step; `slots` words per wave, `waves` waves per workgroup).  Only the diagnostics build
+ * (-DDP_DIAG, lib/libdpscan_diag.so) records them; the shipped library returns DP_ERR_INVALID. */
 int dp_debug_profile(dp_ctx* ctx, uint64_t* host_words, uint64_t n_words, int* slots, int* waves);
 
 /* Device (hipMalloc) and pinned host (hipHostMalloc) allocations the library has made in this process so
@@ -161,17 +161,30 @@ int dp_debug_profile(dp_ctx* ctx, uint64_t* host_words, uint64_t n_words, int* s
  * FASTA range summaries and spill).  Steady-state calls on warm contexts allocate nothing. */
 int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
 
-/* Which kernels a ctx's scans use: the FASTA index as two kernels (map + placement; 0 = the one-pass
- * look-back kernel, DP_FASTA_ONEPASS=1), and the largest newline launch (bytes scanned) that runs as two
- * kernels -- larger ones run the one-pass kernel (default 512 MiB; DP_DELIM_TWOPASS_MAX sets it). */
-int dp_scan_forms(dp_ctx* ctx, int* fasta_two_kernel, uint64_t* delim_two_kernel_max);
-/* The kernels the ctx's next newline launch scanning `span` bytes takes: 1 = line_kernel (lockstep one pass),
- * 2 = map + placement kernels, 3 = the one-pass look-back kernel.  Default: line_kernel up to 2 GiB per launch
- * (DP_DELIM_LINE_MAX sets the split), and above it too when the ctx's previous newline launch had at least 20
- * delimiters per KiB (CSV-like density); otherwise the one-pass kernel above 2 GiB.  DP_DELIM_FORM = hybrid |
- * line | auto | two | one overrides (auto: round 3's rule, two kernels up to delim_two_kernel_max bytes, one-pass
- * above).  Every form writes the same output. */
+/* The kernels a ctx's scans take.  The defaults are the shipped choices; a library reads no environment
+ * variable, so only these calls change them (tests and same-box A/B runs):
+ *   DP_FORM_FASTA           0 = map + placement kernels (default), 1 = the one-pass look-back kernel;
+ *   DP_FORM_DELIM           0 = auto (default), 1 = line_kernel (lockstep one pass), 2 = map + placement
+ *                           kernels, 3 = the one-pass look-back kernel, at every launch size;
+ *   DP_FORM_DELIM_LINE_MAX  auto: launches of up to this many bytes (the sum of the ranges) run line_kernel
+ *                           (default 4 GiB);
+ *   DP_FORM_DELIM_DENSE     auto, above that size: a density probe kernel counts the delimiters of 256 KiB
+ *                           sampled evenly from the launch's own bytes and picks line_kernel at this many or
+ *                           more delimiters per KiB x 1000 (default 20000: CSV-like), the one-pass kernel below.
+ * Every form writes the same output.  Not while a scan is in flight on the ctx. */
+#define DP_FORM_FASTA 0
+#define DP_FORM_DELIM 1
+#define DP_FORM_DELIM_LINE_MAX 2
+#define DP_FORM_DELIM_DENSE 3
+int dp_ctx_set_form(dp_ctx* ctx, int what, uint64_t value);
+int dp_ctx_get_form(dp_ctx* ctx, int what, uint64_t* value);
+/* The kernels the ctx's next newline launch scanning `span` bytes takes: 1 = line_kernel, 2 = map + placement
+ * kernels, 3 = the one-pass look-back kernel, 0 = decided on the device from the launch's bytes (auto above
+ * DP_FORM_DELIM_LINE_MAX). */
 int dp_scan_delim_form(dp_ctx* ctx, uint64_t span, int* form);
+/* The kernels the ctx's last collected newline launch ran (1, 2 or 3; 0 before any): the probe's pick read back
+ * with the launch's results. */
+int dp_last_delim_form(dp_ctx* ctx, int* form);
 
 /* Launch geometry (for tests/tuning): workgroups of the persistent scan grid, and unit size in bytes. */
 int dp_scan_geometry(dp_ctx* ctx, int* grid, int* unit_bytes);

@@ -336,7 +336,8 @@ def test_bench_default_line_carries_the_newline_legs():
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(repo, "bench.py"), "--size", str((64 << 20) + 12), "--csv-size",
-           str((72 << 20) + 3), "--vcf-size", str((80 << 20) + 9), "--steps", "3", "--warmup", "1"]
+           str((72 << 20) + 3), "--vcf-size", str((80 << 20) + 9), "--steps", "3", "--warmup", "1",
+           "--e2e-fasta-size", str((48 << 20) + 5), "--e2e-csv-size", str((40 << 20) + 7), "--fastq-tiles", "2"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.strip()]
@@ -352,6 +353,18 @@ def test_bench_default_line_carries_the_newline_legs():
         assert rf["frac"] > 0 and rf["measured_peak"] > 0 and rf["measured_mixed_ref"] > 0
         assert sub["cpu_baseline"]["value"] > 0 and sub["cpu_baseline"]["cores"] >= 1
         assert rf["kernel"].startswith("line_kernel<DELIM>")         # the default newline form
+    # the end-to-end sub-objects (host memory to host memory, every stored index read back and checked)
+    e2e = line["e2e"]
+    assert "error" not in e2e, e2e
+    for kind in ("fasta", "csv"):
+        for src in ("memory", "loopback_http"):
+            assert e2e[kind][src]["verified"] is True and e2e[kind][src]["value"] > 0, (kind, src, e2e[kind])
+        assert e2e[kind]["stages"]["h2d_GiB_per_s"] > 0 and e2e[kind]["stages"]["index_bytes"] > 0
+    assert e2e["fits_in_driver_run"] is True
+    fq = line["fastq"]
+    assert "error" not in fq, fq
+    assert fq["verified_every_read_end"] is True and fq["reads"] == 2 * 65536 and fq["gzip_members"] == 1
+    assert fq["fits_in_driver_run"] is True
     assert line["bench_wall_s"] > 0
 
 

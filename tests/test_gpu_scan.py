@@ -435,12 +435,10 @@ def test_delim_u16_blocks(ctx, base):
 
 def _form_ctx(onepass):
     from dataplug_amd.scan import ScanContext
-    os.environ["DP_FASTA_ONEPASS"] = "1" if onepass else "0"
-    try:
-        c = ScanContext(0)
-    finally:
-        del os.environ["DP_FASTA_ONEPASS"]
-    assert c.forms()[0] == (0 if onepass else 1), c.forms()
+    c = ScanContext(0)
+    assert c.get_form("fasta") == 0                       # the shipped default: map + placement kernels
+    c.set_form(fasta=int(onepass))
+    assert c.get_form("fasta") == int(onepass)
     return c
 
 
@@ -489,40 +487,48 @@ def test_repeated_launches_and_sizes():
         c.close()
 
 
-def _delim_ctx(twopass_max, form="auto"):
-    """A context pinned to round 3's size-based newline forms (form "auto": two kernels up to twopass_max bytes,
-    the one-pass kernel above) or, form "line", to the default lockstep line_kernel."""
+_DELIM_FORM_IDS = {"line": 1, "one": 3}
+
+
+def _delim_ctx(form, **kw):
+    """A context pinned to one newline form (dp_ctx_set_form): "line" (line_kernel), "one" (the one-pass look-back
+    kernel), or "auto" (the default) with its settings in kw, e.g. delim_line_max=0 so that every launch runs the
+    density probe."""
     from dataplug_amd.scan import ScanContext
-    os.environ["DP_DELIM_TWOPASS_MAX"] = str(twopass_max)
-    os.environ["DP_DELIM_FORM"] = form
-    try:
-        c = ScanContext(0)
-    finally:
-        del os.environ["DP_DELIM_TWOPASS_MAX"]
-        del os.environ["DP_DELIM_FORM"]
-    assert c.forms()[1] == twopass_max
+    c = ScanContext(0)
+    assert c.get_form("delim") == 0 and c.get_form("delim_line_max") == 4 << 30 and c.get_form("delim_dense") == 20000
+    if form != "auto":
+        c.set_form(delim=_DELIM_FORM_IDS[form])
+    c.set_form(**kw)
     return c
 
 
 @pytest.mark.parametrize("size", [1, 5_000, 64 * 16384 - 3, 64 * 16384 + 16385, (7 << 20) + 11, (70 << 20) + 5])
 def test_newline_forms_equal(size):
-    """The newline index's three forms (line_kernel, the default; map + 64-range placement blocks; the one-pass
-    look-back kernel) give the oracle's offsets in every output form, with every_k / emit_add / carry, on CSV
-    rows (some ranges over the 512-entry spill slot and line_kernel's 640-entry LDS list: dense rescans), a run
-    of newlines and newline-free spans; all three write the same block table."""
-    two, one, line = _delim_ctx(1 << 62), _delim_ctx(0), _delim_ctx(0, "line")
+    """The newline index's two kernels (line_kernel; the one-pass look-back kernel) and the auto form's density
+    probe picking either one (the other enqueued and returning at once) give the oracle's offsets in every output
+    form, with every_k / emit_add / carry, on CSV rows (some ranges over line_kernel's 640-entry LDS list and the
+    one-pass kernel's 1024-entry list: dense rescans), a run of newlines and newline-free spans; all of them write
+    the same block table.  The removed map + placement form (round 3) is refused."""
+    one, line = _delim_ctx("one"), _delim_ctx("line")
+    with pytest.raises(DPScanError, match="DP_FORM_DELIM"):
+        line.set_form(delim=2)
+    auto_l = _delim_ctx("auto", delim_line_max=0, delim_dense=0)                # the probe always picks line
+    auto_o = _delim_ctx("auto", delim_line_max=0, delim_dense=1 << 40)          # ... always the one-pass kernel
     try:
         a = synth.csv(size, seed=size % 89) if size > 4096 else np.full(size, 10, np.uint8)
         if size > (1 << 20):
             a[size // 3: size // 3 + 40_000] = 10                      # every byte a newline: dense ranges
             a[size // 2: size // 2 + 200_000] = ord("x")               # no newline for 12 ranges
         n = len(a)
-        d = two.workspace("t_in", n + 64)
-        two.h2d(d.ptr + 3, a)
         d1 = one.workspace("t_in", n + 64)
         one.h2d(d1.ptr + 3, a)
         d2 = line.workspace("t_in", n + 64)
         line.h2d(d2.ptr + 3, a)
+        d3 = auto_l.workspace("t_in", n + 64)
+        auto_l.h2d(d3.ptr + 3, a)
+        d4 = auto_o.workspace("t_in", n + 64)
+        auto_o.h2d(d4.ptr + 3, a)
         base = 3
         full = dpref.delim(a, 0, n)[0] + np.uint64(base)
         for k, add, carry in ((1, 0, 0), (4, 1, 2), (3, 0, 7)):
@@ -530,7 +536,8 @@ def test_newline_forms_equal(size):
             exp = full[(sel % np.uint64(k)) == np.uint64(k - 1)] + np.uint64(add)
             for mode in (1, 0, 3):
                 outs = []
-                for c, dp in ((two, d.ptr + 3), (one, d1.ptr + 3), (line, d2.ptr + 3)):
+                for c, dp, want in ((one, d1.ptr + 3, 3), (line, d2.ptr + 3, 1), (auto_l, d3.ptr + 3, 1),
+                                    (auto_o, d4.ptr + 3, 3)):
                     if mode == 3 and (k != 1 or add != 0):
                         # the block table counts delimiters: an entry index only when every delimiter is one
                         with pytest.raises(DPScanError, match="out_mode 3 needs every_k == 1"):
@@ -539,6 +546,7 @@ def test_newline_forms_equal(size):
                         continue
                     r = c.delim_ranges(dp, n, base, [(base, base + n)], every_k=k, emit_add=add, carry=carry,
                                        out_mode=mode)
+                    assert c.last_delim_form() == want
                     outs.append(r)
                     if mode == 3:
                         low, _, _, tab = r
@@ -556,16 +564,18 @@ def test_newline_forms_equal(size):
                     if mode == 3:                                 # the forms' block tables too
                         assert np.array_equal(outs[0][3], o[3])
     finally:
-        two.close()
-        one.close()
-        line.close()
+        for c in (one, line, auto_l, auto_o):
+            c.close()
 
 
 def test_forms_alternate_on_one_context():
-    """One context switching between the two-kernel and the one-pass newline forms (and the two-kernel FASTA
-    index) launch after launch: the one-pass kernel's unit ticket shares a control word with the placement
-    kernels' block ticket, which a two-kernel launch leaves non-zero; every result stays exact."""
-    c = _delim_ctx(1 << 20)                               # up to 1 MiB per launch: two kernels
+    """One context switching between every newline form (and both FASTA forms) launch after launch: the one-pass
+    kernel's unit ticket shares a control word with the FASTA placement kernel's block ticket, which a two-kernel
+    FASTA launch leaves non-zero, line_kernel's ticket parity advances with every launch, and the auto form
+    enqueues line_kernel and the one-pass kernel with only the probe's pick running; every result stays exact."""
+    c = _delim_ctx("auto")
+    forms = [dict(delim=3), dict(delim=1), dict(delim=0, delim_line_max=0, delim_dense=1 << 40),
+             dict(delim=0, delim_line_max=0, delim_dense=0), dict(delim=0, delim_line_max=4 << 30, delim_dense=20000)]
     try:
         a = synth.csv((3 << 20) + 333, seed=4)
         n = len(a)
@@ -578,8 +588,9 @@ def test_forms_alternate_on_one_context():
         plan = cpu_ref.chunk_plan(len(f), -(-len(f) // 3))
         fexp = dpref.fasta_pairs(f, plan)
         for it in range(6):
-            for lo, hi in ((0, 700_000), (0, n), (1000, 900_000), (5, n - 7)):   # two-kernel, one-pass, ...
+            for j, (lo, hi) in enumerate(((0, 700_000), (0, n), (1000, 900_000), (5, n - 7))):
                 for mode in (1, 3):
+                    c.set_form(**forms[(it + j + mode) % len(forms)])
                     r = c.delim_ranges(d.ptr, n, 0, [(lo, hi)], out_mode=mode)
                     exp = full[(full >= lo) & (full < hi)]
                     if mode == 3:
@@ -591,6 +602,7 @@ def test_forms_alternate_on_one_context():
                         got = r[0]
                     assert np.array_equal(got, exp), (it, lo, hi, mode)
             if it % 2:
+                c.set_form(fasta=(it // 2) % 2)
                 pairs, pending, _ = c.fasta_index(df.ptr, len(f), 0, len(f), plan)
                 assert (pending == -1).all() and np.array_equal(pairs.astype(np.uint64), fexp)
     finally:
@@ -599,30 +611,25 @@ def test_forms_alternate_on_one_context():
 
 @pytest.mark.gpu
 def test_form_follows_delimiter_density():
-    """Above the hybrid form's size split a newline launch takes line_kernel when the context's previous launch
-    was CSV-dense (>= 20 delimiters per KiB), else the one-pass kernel (dp_scan_delim_form); a context's first
-    launch has no density yet.  Every launch, whichever kernel, equals the oracle (the split set to 1 MiB so
-    small launches exercise both sides)."""
-    from dataplug_amd.scan import ScanContext
-    os.environ["DP_DELIM_LINE_MAX"] = str(1 << 20)
-    try:
-        c = ScanContext(0)
-    finally:
-        del os.environ["DP_DELIM_LINE_MAX"]
+    """The auto newline form: up to DP_FORM_DELIM_LINE_MAX bytes per launch line_kernel; above it, the density
+    probe reads 256 sampled rows of THIS launch's bytes on the device and picks line_kernel for CSV-dense input
+    (>= 20 delimiters per KiB), the one-pass kernel for sparser input (VCF): the choice follows each launch's own
+    bytes, not the context's history (dp_last_delim_form reads the pick back).  Every launch, whichever kernel,
+    equals the oracle (the split set to 1 MiB so small launches exercise both sides)."""
+    c = _delim_ctx("auto", delim_line_max=1 << 20)
     try:
         objs = {"csv": synth.csv((5 << 20) + 77, seed=12), "vcf": synth.vcf((5 << 20) + 91, seed=13)}
         dens = {k: len(dpref.delim(a, 0, len(a))[0]) * 1024 / len(a) for k, a in objs.items()}
         assert dens["csv"] >= 20 > dens["vcf"], dens
-        span = 4 << 20
-        assert c.delim_form(span) == 3 and c.delim_form(1 << 20) == 1      # no density yet
-        for name, want_next in (("csv", 1), ("csv", 1), ("vcf", 3), ("vcf", 3), ("csv", 1)):
+        assert c.delim_form(4 << 20) == 0 and c.delim_form(1 << 20) == 1 and c.last_delim_form() == 0
+        for name, lim, want in (("vcf", None, 3), ("csv", None, 1), ("csv", None, 1), ("vcf", None, 3),
+                                ("vcf", 1 << 20, 1), ("csv", 1 << 20, 1), ("vcf", None, 3)):
             a = objs[name]
-            n = len(a)
-            d = c.workspace("t_" + name, n + 64)
+            n = len(a) if lim is None else lim
+            d = c.workspace("t_" + name, len(a) + 64)
             c.h2d(d.ptr, a)
-            ran = c.delim_form(n)
-            r = c.delim_ranges(d.ptr, n, 0, [(0, n)], out_mode=1)
-            assert np.array_equal(r[0], dpref.delim(a, 0, n)[0]), (name, ran)
-            assert c.delim_form(span) == want_next, (name, ran)
+            r = c.delim_ranges(d.ptr, len(a), 0, [(0, n)], out_mode=1)
+            assert np.array_equal(r[0], dpref.delim(a, 0, n)[0]), (name, n)
+            assert c.last_delim_form() == want, (name, n, c.last_delim_form())
     finally:
         c.close()

@@ -15,9 +15,8 @@ from dataplug_amd import isa_guard
 from dataplug_amd.scan import _lib
 
 SHIPPED = ["scan_kernel<0,0>", "scan_kernel<0,1>", "scan_kernel<1,0>", "scan_kernel<1,1>", "scan_kernel<1,2>",
-           "map_kernel<0>", "map_kernel<1>", "fasta_place_kernel<0>", "fasta_place_kernel<1>",
-           "delim_place_kernel<0>", "delim_place_kernel<1>", "delim_place_kernel<2>", "line_kernel<1,0>",
-           "line_kernel<1,1>", "line_kernel<1,2>", "fasta_resolve_kernel",
+           "map_kernel", "fasta_place_kernel<0>", "fasta_place_kernel<1>", "line_kernel<0>",
+           "line_kernel<1>", "line_kernel<2>", "density_probe_kernel", "fasta_resolve_kernel",
            "find_kernel", "stream_kernel", "stream_rw_kernel"]
 
 
@@ -108,3 +107,41 @@ def test_guard_counts_lds_dma_loads(tmp_path, n, ok):
     p.write_text(_ASM_DMA.format(n=n))
     assert (isa_guard.check(str(p)) == []) == ok
     assert isa_guard.short_name(isa_guard.kernel_names(str(p))[0]) == "line_kernel<1,2>"
+
+
+_ASM_WIN = """\t.text
+_ZN12_GLOBAL__N_111line_kernelILi2EEEvNS_8LineArgsE:
+\t;;#ASMSTART
+\ts_mov_b32 m0, s8
+\tglobal_load_lds_dwordx4 v[8:9], off sc1
+\t;;#ASMEND
+\t;;#ASMSTART
+\tbuffer_load_dwordx4 v[4:7], v1, s[0:3], 0 offen nt
+\t;;#ASMEND
+\ts_waitcnt vmcnt({n})
+\t;;#ASMSTART
+\tds_read_b64 v[10:11], v3 ; dp_win_read
+\ts_waitcnt lgkmcnt(0)
+\t;;#ASMEND
+\ts_endpgm
+.Lfunc_end0:
+\t.amdhsa_kernel _ZN12_GLOBAL__N_111line_kernelILi2EEEvNS_8LineArgsE
+\t\t.amdhsa_private_segment_fixed_size 0
+\t.end_amdhsa_kernel
+"""
+
+
+@pytest.mark.parametrize("n,ok", [(1, True), (0, True), (2, False)])
+def test_guard_flags_a_window_read_before_its_lds_dma(tmp_path, n, ok):
+    """a tagged read of line_kernel's look-back window while its LDS-DMA load may still be in flight is a
+    violation: with a buffer load issued after the window, `vmcnt(1)` retires the window, `vmcnt(2)` does not."""
+    p = tmp_path / "k.s"
+    p.write_text(_ASM_WIN.format(n=n))
+    assert (isa_guard.check(str(p)) == []) == ok
+
+
+def test_stamp_matches_the_source_tree():
+    """The installed library was built from the kernel source in the tree (a stale build that passed the guard on
+    older source does not pass this)."""
+    rep = _stamp()
+    assert rep.get("src_sha256") == B.sha256_file(B.SRC), "libdpscan.so was built from another dpscan.hip: rebuild"

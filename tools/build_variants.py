@@ -3,8 +3,10 @@
     python tools/build_variants.py name=DEF1,DEF2=3 name2=DEF3 ...   # '-' for no defines
     python tools/build_variants.py head@HEAD=- ...                   # the source as of a git revision
 
-Variants are diagnostics for same-box comparisons (tools/probe_perf.py with DPSCAN_LIB=...); the shipped
-library is always the default build (python -m dataplug_amd.build).
+Variants are diagnostics for same-box comparisons (tools/gpu_ab.sh with DPSCAN_LIB=...): the diagnostics build
+(diag=DP_DIAG: in-kernel realtime stamps for tools/map_timeline.py, place_timeline.py, line_timeline.py) or a
+source revision (name@REV).  The shipped library is always the default build (python -m dataplug_amd.build), which
+has no switches.
 """
 from __future__ import annotations
 
@@ -25,8 +27,8 @@ def main(specs):
         name, _, defs = s.partition("=")
         name, _, rev = name.partition("@")
         defines = [] if defs in ("", "-") else defs.split(",")
-        prof = "DP_PROF" in defines
-        defines = [d for d in defines if d != "DP_PROF"]
+        diag = "DP_DIAG" in defines
+        defines = [d for d in defines if d != "DP_DIAG"]
         out = os.path.join(HERE, "lib", f"libdpscan_v_{name}.so")
         src = SRC
         if rev:                                  # next to the real source so its #include resolves
@@ -34,13 +36,13 @@ def main(specs):
             with open(src, "w") as fh:
                 fh.write(subprocess.run(["git", "show", f"{rev}:dataplug_amd/csrc/dpscan.hip"], check=True,
                                         capture_output=True, text=True).stdout)
-        jobs.append((defines, prof, out, src))
+        jobs.append((defines, diag, out, src))
     # build() runs the ISA guard on each variant's own assembly and installs nothing that fails it: a variant
     # whose compiled code touches an in-flight load destination (or spills) can corrupt addresses and fault the GPU
 
     def one(j):
         try:
-            return build(defines=j[0], prof=j[1], out=j[2], src=j[3], guard=True)
+            return build(defines=j[0], diag=j[1], out=j[2], src=j[3])
         except IsaGuardError as e:
             if os.path.exists(j[2]):
                 os.remove(j[2])

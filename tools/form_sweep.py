@@ -1,0 +1,138 @@
+"""Newline index: the line_kernel and one-pass forms against the read-only stream kernel, alternated rep by rep.
+
+Same box, same resident object (synth.tiled_csv / tiled_vcf of the largest size, uploaded once), every size a
+prefix [0, size) of it in the stored form (out_mode 3: uint16 low words + 64 KiB block table).  Every rep runs
+the read-only calibration kernel over the same bytes and then each form once (the order rotates per rep), so a
+drift of the box touches every form alike; each launch is timed alone (HIP events on the device's scan stream).
+Per size: mean / median / min / max of every form, its roofline fraction on algorithmic bytes (N + 2 L + 8 B per
+64 KiB block, over 8 TB/s), the stream kernel's, and the shipped default's choice; outputs of all forms compared
+byte for byte.
+
+    python tools/form_sweep.py [--content vcf,csv] [--sizes-gib 2,4,8,16,32,64] [--reps 10] [--forms line,one,default]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dataplug_amd import synth  # noqa: E402
+from dataplug_amd.scan import ScanContext  # noqa: E402
+
+FORM_IDS = {"line": 1, "one": 3, "default": 0}
+
+
+def make_ctx(form: str) -> ScanContext:
+    ctx = ScanContext(0)
+    if form != "default":
+        ctx.set_form(delim=FORM_IDS[form])
+    return ctx
+
+
+def stats(ts):
+    a = np.asarray(ts, float)
+    return {"mean": round(float(a.mean()), 1), "median": round(float(np.median(a)), 1),
+            "min": round(float(a.min()), 1), "max": round(float(a.max()), 1), "std": round(float(a.std()), 1)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--content", default="vcf,csv")
+    ap.add_argument("--sizes-gib", default="2,4,8,16,32,64")
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--forms", default="line,one,default")
+    ap.add_argument("--no-stream", action="store_true")
+    args = ap.parse_args()
+    sizes = [int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")]
+    top = max(sizes)
+    names = args.forms.split(",")
+    ctxs = {k: make_ctx(k) for k in names}
+    ctx0 = next(iter(ctxs.values()))
+    d = ctx0.workspace("in", top + 64)
+    for content in args.content.split(","):
+        t0 = time.perf_counter()
+        obj = (synth.tiled_csv if content == "csv" else synth.tiled_vcf)(top, seed=1)
+        step = 2 << 30
+        stage = np.empty(min(step, top), np.uint8)
+        for p in range(0, top, step):
+            q = min(top, p + step)
+            ctx0.h2d(d.ptr + p, obj.bytes_range(p, q, out=stage))
+        del stage
+        print(json.dumps({"content": content, "gen_s": round(time.perf_counter() - t0, 2)}), flush=True)
+        # every context's output buffer sized for the largest launch once, before any is timed
+        top_cap = obj.count_range(0, top) + 1024
+        ob_top = ScanContext.out_bytes(top_cap, 3, np.asarray([0, top], np.uint64))
+        outs = {k: c.workspace("out", ob_top) for k, c in ctxs.items()}
+        for size in sizes:
+            n_exp = obj.count_range(0, size)
+            cap = n_exp + 1024
+            ranges = np.asarray([0, size], np.uint64)
+            times = {k: [] for k in names}
+            chosen = {}
+            st = []
+
+            def run(k):
+                c = ctxs[k]
+                c.delim_ranges_async(d.ptr, top, 0, ranges, 10, 1, 0, 0, outs[k].ptr, 3, cap)
+                r = c.delim_ranges_result(1)
+                if k == "default":
+                    chosen.setdefault("default", []).append(c.last_delim_form())
+                return r
+
+            for k in names:                       # warm (code objects, workspace) and the first result
+                run(k)
+            for c in ctxs.values():
+                c.timing(True)
+                c.timing_read()
+            for rep in range(args.reps):
+                if not args.no_stream:
+                    ctx0.stream_read(d.ptr, size)
+                    ctx0.sync()
+                    ms, _ = ctx0.timing_read()
+                    st.append(ms * 1e3)
+                order = names[rep % len(names):] + names[:rep % len(names)]
+                for k in order:
+                    n, _, _ = run(k)
+                    ms, _ = ctxs[k].timing_read()
+                    times[k].append(ms * 1e3)
+            for c in ctxs.values():
+                c.timing(False)
+            res = {}
+            for k, c in ctxs.items():
+                words = c.d2h(np.empty(n, np.uint16), outs[k].ptr)
+                res[k] = (n, words, c.block_table(outs[k].ptr, cap, ranges))
+            vals = list(res.values())
+            a = vals[0]
+            equal = bool(a[0] == n_exp and all(b[0] == a[0] and np.array_equal(a[1], b[1]) and
+                                               np.array_equal(a[2], b[2]) for b in vals[1:]))
+            alg = size + 2 * n_exp + 8 * len(a[2])
+            line = {"content": content, "size_gib": size / (1 << 30), "entries": n_exp, "equal": equal}
+            if st:
+                s = stats(st)
+                line["stream_us"] = s
+                line["stream_TBps_median"] = round(size / (s["median"] * 1e-6) / 1e12, 3)
+            for k in names:
+                s = stats(times[k])
+                line[f"{k}_us"] = s
+                line[f"{k}_frac_median"] = round(alg / (s["median"] * 1e-6) / 8e12, 4)
+                line[f"{k}_frac_mean"] = round(alg / (s["mean"] * 1e-6) / 8e12, 4)
+                if st:
+                    line[f"{k}_over_stream"] = round(s["median"] / stats(st)["median"], 4)
+                line[f"{k}_all_us"] = [round(t, 1) for t in times[k]]
+            if "default" in chosen:
+                line["default_forms"] = sorted(set(chosen["default"]))
+            print(json.dumps(line), flush=True)
+            del res, vals, a
+            if not equal:
+                print("MISMATCH", flush=True)
+                sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

@@ -199,7 +199,16 @@ def kernel_mode(args, rng):
     """The kernels through the C ABI on random objects, chunk plans, misalignments and output forms."""
     ctx = ScanContext(0)
     stats = {"fasta_cases": 0, "fasta_pairs": 0, "quirk_cases": 0, "delim_cases": 0, "delim_offsets": 0,
-             "bytes": 0, "kinds": {}}
+             "bytes": 0, "kinds": {}, "delim_forms": {}}
+    # the newline launch's kernels, drawn per case (dp_ctx_set_form): the default (line_kernel at these sizes), the
+    # auto form's density probe at every size (line_max 0) with its threshold at random (either pick), or a form
+    # pinned to line_kernel / the one-pass kernel
+    delim_forms = [dict(delim=0, delim_line_max=4 << 30, delim_dense=20000),
+                   dict(delim=0, delim_line_max=0, delim_dense=20000),
+                   dict(delim=0, delim_line_max=0, delim_dense=0),
+                   dict(delim=0, delim_line_max=0, delim_dense=1 << 40),
+                   dict(delim=1, delim_line_max=4 << 30, delim_dense=20000),
+                   dict(delim=3, delim_line_max=4 << 30, delim_dense=20000)]
     t0 = last = time.time()
     while time.time() - t0 < args.seconds:
         a, kind = make_object(rng, getattr(args, "max_size", 48 << 20))
@@ -240,7 +249,11 @@ def kernel_mode(args, rng):
             k = int(rng.integers(1, 6))
             add = int(rng.integers(0, 2))
             du64 = bool(rng.random() < 0.7)
+            ctx.set_form(**delim_forms[int(rng.integers(0, len(delim_forms)))])
             got, nd = ctx.delim_index(buf.ptr + off, size, 0, b0, b1, delim, k, add, u64=du64)
+            if b1 > b0:
+                f = str(ctx.last_delim_form())
+                stats["delim_forms"][f] = stats["delim_forms"].get(f, 0) + 1
             want, wnd = dpref.delim(a, b0, b1, delim, k, add)
             if nd != wnd or not np.array_equal(got.astype(np.uint64), want):
                 _save_fail(data=a, begin=b0, end=b1, delim=delim, k=k,
@@ -252,7 +265,8 @@ def kernel_mode(args, rng):
             stats["delim_offsets"] += int(len(want))
         if time.time() - last > 20:
             last = time.time()
-            print(json.dumps({"t": round(last - t0), **{k: v for k, v in stats.items() if k != "kinds"}}), flush=True)
+            print(json.dumps({"t": round(last - t0), **{k: v for k, v in stats.items() if k not in ("kinds", "delim_forms")}}),
+                  flush=True)
     stats["_t"] = time.time() - t0
     ctx.close()
     return stats

@@ -1,4 +1,4 @@
-"""Per-kernel summary of a tools/r4_kernel_pmc.sh run: every kernel's average duration (kernel trace) and its SQ
+"""Per-kernel summary of a tools/kernel_pmc.sh run: every kernel's average duration (kernel trace) and its SQ
 counters per dispatch (summed over the per-XCD/SE rows rocprofv3 reports), with instruction counts per wave and
 the wait counters as shares of SQ_WAVE_CYCLES.
 

@@ -1,8 +1,8 @@
 #!/bin/bash
 # SQ counters of every kernel a short command launches (on the GPU box), two passes of 8 SQ counters each plus a
 # kernel trace, summarised per kernel by tools/kernel_pmc.py:
-#     bash tools/r4_kernel_pmc.sh <tag> <python script args...>
-# e.g.  bash tools/r4_kernel_pmc.sh sparse2g tools/size_sweep.py --sizes-gib 2 --reps 5
+#     bash tools/kernel_pmc.sh <tag> <python script args...>
+# e.g.  bash tools/kernel_pmc.sh sparse2g tools/size_sweep.py --sizes-gib 2 --reps 5
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 TAG=${1:?tag}; shift

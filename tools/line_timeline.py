@@ -1,6 +1,6 @@
-"""Per-step phase times of line_kernel (profiling build: tools/build_variants.py ltl=DP_LTL).
+"""Per-step phase times of line_kernel (diagnostics build: tools/build_variants.py diag=DP_DIAG).
 
-    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_ltl.so python tools/line_timeline.py [--content sparse|csv|vcf] [--gib 2]
+    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_diag.so python tools/line_timeline.py [--content sparse|csv|vcf] [--gib 2]
 
 Each of waves 0, 1, 8 and 15 of the first 256 workgroups stamps the realtime clock (100 MHz) at 8 points of
 every step (dpscan.hip LTL): 0 after the step barrier, 1 after b[0]'s wait, 2 after wave 0's AGG publication

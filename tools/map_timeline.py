@@ -1,6 +1,6 @@
-"""Per-wave start/end times of one fasta_map_kernel launch (profiling build: tools/build_variants.py prof2=DP_PROF2).
+"""Per-wave start/end times of one fasta_map_kernel launch (diagnostics build: tools/build_variants.py diag=DP_DIAG).
 
-    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof2.so python tools/map_timeline.py [--size BYTES]
+    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_diag.so python tools/map_timeline.py [--size BYTES]
 
 Prints, in microseconds from the launch's first wave start: the spread of wave starts, the distribution of
 wave and workgroup end times, per-XCC medians of workgroup end times, and the ranges per wave.

@@ -1,7 +1,7 @@
-"""Section times of one fasta_place_kernel launch (profiling build: tools/build_variants.py prof2=DP_PROF2), next to
+"""Section times of one fasta_place_kernel launch (diagnostics build: tools/build_variants.py diag=DP_DIAG), next to
 the map kernel's wave end times, in microseconds from the map kernel's first wave start.
 
-    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_prof2.so python tools/place_timeline.py [--size BYTES]
+    DPSCAN_LIB=dataplug_amd/lib/libdpscan_v_diag.so python tools/place_timeline.py [--size BYTES]
 
 Per placement block: 0 start (after its ticket), 1 range summaries loaded + wave scans, 2 block scan done,
 3 block prefix resolved (look-back), 7 the block's output run known (two barriers later), 4 events staged,

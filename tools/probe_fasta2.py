@@ -48,13 +48,13 @@ def main():
     ms, k = ctx.timing_read()
     us = ms / k * 1e3
     ok = None
-    if not args.no_verify and not os.environ.get("DP_PROBE_PLACE_COUNT_ONLY"):
+    if not args.no_verify:
         from oracle import dpref
         got = ctx.d2h(np.empty((npairs, 2), np.uint32), out.ptr)
         ok = bool((pending == -1).all() and np.array_equal(got.astype(np.uint64), dpref.fasta_pairs(host, plan)))
     alg = n + 8 * npairs
     print(json.dumps({"lib": os.path.basename(os.environ.get("DPSCAN_LIB", "libdpscan.so")),
-                      "count_only": bool(os.environ.get("DP_PROBE_PLACE_COUNT_ONLY")), "size": n, "span_us": round(us, 1),
+                      "size": n, "span_us": round(us, 1),
                       "alg_TBps": round(alg / us / 1e6, 3), "frac": round(alg / us / 1e6 / 8.0, 4), "pairs": npairs,
                       "bit_exact": ok}), flush=True)
 
