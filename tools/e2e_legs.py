@@ -110,7 +110,8 @@ def _stages(co, kind: str, size: int, chunk_size: int):
         ctx.sync()
     t_pipe = _timed(pipe, 2)
     if kind == "fasta":
-        plan = [(i * chunk_size, min(size, (i + 1) * chunk_size)) for i in range(-(-size // chunk_size))]
+        from dataplug_amd.preprocessing.handler import chunk_plan
+        plan = chunk_plan(size, chunk_size)          # the reference's plan (preprocess.py:38, handler.py:36-38)
         ch = np.ascontiguousarray(np.asarray(plan, np.uint64).reshape(-1))
         cap = size // 256 + 1024
         out = ctx.workspace("e2e_out", 8 * cap)
@@ -157,9 +158,8 @@ def _stages(co, kind: str, size: int, chunk_size: int):
 
 
 def _verify_fasta(co, host: np.ndarray, chunk_size: int) -> bool:
-    from oracle import dpref                     # the checker (test infrastructure), outside every timed region
-    size = len(host)
-    plan = [(i * chunk_size, min(size, (i + 1) * chunk_size)) for i in range(-(-size // chunk_size))]
+    from oracle import cpu_ref, dpref            # the checker (test infrastructure), outside every timed region
+    plan = cpu_ref.chunk_plan(len(host), chunk_size)   # the reference's plan (preprocess.py:30-61), quirks included
     exp = dpref.fasta_pairs(host, plan).astype(np.uint32).reshape(-1)
     got = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=co.meta_path.key)["Body"].read(),
                         np.uint32)
