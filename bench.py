@@ -88,9 +88,10 @@ def parse(argv=None):
     p.add_argument("--csv-size", type=int, default=32 << 30, help="csv leg: bytes per GPU")
     p.add_argument("--vcf-size", type=int, default=64 << 30, help="vcf leg: object bytes (cut over the GPUs)")
     p.add_argument("--chunks", type=int, default=4, help="FASTA map chunks per object (chunk_size = size / chunks)")
-    p.add_argument("--index-dtype", choices=["u16b", "u32p", "u64"], default="u16b",
-                   help="csv/vcf newline index form: u16b = uint16 low words + 64 KiB block table (what "
-                        "co.preprocess stores), u32p = uint32 low words + 4 GiB page counts, u64 = plain uint64")
+    p.add_argument("--index-dtype", choices=["u8s", "u16b", "u32p", "u64"], default="u8s",
+                   help="csv/vcf newline index form: u8s = uint8 low bytes + 256-byte counts + 64 KiB block table, "
+                        "u16b = uint16 low words + 64 KiB block table, u32p = uint32 low words + 4 GiB page counts, "
+                        "u64 = plain uint64")
     p.add_argument("--devices", default=None,
                    help="comma-separated device of each worker / local rank (default 0..N-1); e.g. 0,0,0,0 "
                         "rehearses the multi-GPU split on one GPU")
@@ -714,6 +715,40 @@ def _verify_blocked(obj, begin, end, got, tab, n_out):
     return bool(i == n_out and (tab[nxt - j0:] == np.uint64(n_out)).all())
 
 
+def _verify_bytes(obj, begin, end, got, sub, tab, n_out):
+    """Every offset of a uint8 + 256-byte + 64 KiB table index (out_mode 4) against the object's analytic newline
+    positions: the low bytes equal the expected offsets' low 8 bits, every 256-byte entry equals the low 16 bits of
+    the expected offsets below its boundary, and the block table as in _verify_blocked; together they pin every
+    offset."""
+    s0, j0 = begin >> 8, begin >> 16
+    ns, nb = len(sub), len(tab)
+    i, nxt_s, nxt_j = 0, s0 + (1 if begin & 0xFF else 0), j0 + (1 if begin & 0xFFFF else 0)
+    if (begin & 0xFF and sub[0] != 0) or (begin & 0xFFFF and tab[0] != 0):
+        return False
+    for piece in obj.delims_range(begin, end):
+        if len(piece) == 0:
+            continue
+        if i + len(piece) > n_out or not np.array_equal(got[i:i + len(piece)],
+                                                        (piece & np.uint64(0xFF)).astype(np.uint8)):
+            return False
+        hs = min(int(piece[-1]) >> 8, s0 + ns - 1)
+        if hs >= nxt_s:
+            bnd = np.arange(nxt_s, hs + 1, dtype=np.uint64) << np.uint64(8)
+            exp = (np.uint64(i) + np.searchsorted(piece, bnd).astype(np.uint64)) & np.uint64(0xFFFF)
+            if not np.array_equal(sub[nxt_s - s0:hs + 1 - s0].astype(np.uint64), exp):
+                return False
+            nxt_s = hs + 1
+        hj = min(int(piece[-1]) >> 16, j0 + nb - 1)
+        if hj >= nxt_j:
+            bnd = np.arange(nxt_j, hj + 1, dtype=np.uint64) << np.uint64(16)
+            if not np.array_equal(tab[nxt_j - j0:hj + 1 - j0], np.uint64(i) + np.searchsorted(piece, bnd).astype(np.uint64)):
+                return False
+            nxt_j = hj + 1
+        i += len(piece)
+    return bool(i == n_out and (sub[nxt_s - s0:].astype(np.uint64) == np.uint64(n_out & 0xFFFF)).all()
+                and (tab[nxt_j - j0:] == np.uint64(n_out)).all())
+
+
 def delim_worker(args, team, leg, k, world, dev):
     """configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3] (vcf: ONE
     64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong scaling): the
@@ -743,8 +778,8 @@ def delim_worker(args, team, leg, k, world, dev):
     del stage
     gen_s = time.perf_counter() - t0
     cap = n_exp + 1024
-    item = {"u16b": 2, "u32p": 4, "u64": 8}[fmt]
-    mode = {"u16b": 3, "u32p": 2, "u64": 1}[fmt]
+    item = {"u8s": 1, "u16b": 2, "u32p": 4, "u64": 8}[fmt]
+    mode = {"u8s": 4, "u16b": 3, "u32p": 2, "u64": 1}[fmt]
     rg = np.ascontiguousarray(np.asarray(page_ranges(begin, end) if fmt == "u32p" else [(begin, end)],
                                          np.uint64).reshape(-1))
     nr = len(rg) // 2
@@ -773,9 +808,13 @@ def delim_worker(args, team, leg, k, world, dev):
     verified, t_ver = None, time.perf_counter()
     if not args.no_verify:
         last = d_outs[(args.steps - 1) % 2].ptr
-        got = ctxs[0].d2h(np.empty(n_out, {"u16b": np.uint16, "u32p": np.uint32, "u64": np.uint64}[fmt]), last)
+        got = ctxs[0].d2h(np.empty(n_out, {"u8s": np.uint8, "u16b": np.uint16, "u32p": np.uint32, "u64": np.uint64}[fmt]),
+                          last)
         with _VERIFY_SLOTS:
-            if fmt == "u16b":
+            if fmt == "u8s":
+                verified = n_out == n_exp and _verify_bytes(obj, begin, end, got, ctxs[0].sub_table(last, cap, rg),
+                                                            ctxs[0].block_table(last, cap, rg, 4), n_out)
+            elif fmt == "u16b":
                 verified = n_out == n_exp and _verify_blocked(obj, begin, end, got, ctxs[0].block_table(last, cap, rg),
                                                               n_out)
             else:
@@ -797,7 +836,8 @@ def delim_worker(args, team, leg, k, world, dev):
     t_ver = time.perf_counter() - t_ver
     out = {"worker": k, "device": dev, "dt": dt, "dt_overlap": dt_ov, "kern_s": kms / 1e3 / max(1, kn),
            "scanned": nbytes, "offsets": n_out, "kernel": kernel,
-           "alg_bytes": nbytes + item * n_out + (8 * ScanContext.block_table_size(rg)[1] if fmt == "u16b" else 0),
+           "alg_bytes": nbytes + item * n_out + (8 * ScanContext.block_table_size(rg)[1] if fmt in ("u8s", "u16b") else 0)
+                        + (2 * ScanContext.sub_table_size(rg)[1] if fmt == "u8s" else 0),
            "verified": verified, "verify_s": t_ver, "gen_s": gen_s, "size": size, "wpr": wpr,
            "stream_peak": peak, "mixed_peak": mixed, "range": (begin, end)}
     for c in ctxs:
@@ -842,7 +882,8 @@ def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
     traffic, traffic_src = (load_traffic(args, leg, allres[0]["scanned"], pmc_kernel, args.index_dtype)
                             if world == 1 else (None, None))
     name = "CSV" if csv_mode else "VCF"
-    idx = {"u16b": "uint16 low words + 64 KiB block table", "u32p": "uint32 low words + 4 GiB pages",
+    idx = {"u8s": "uint8 low bytes + 256-byte counts + 64 KiB block table",
+           "u16b": "uint16 low words + 64 KiB block table", "u32p": "uint32 low words + 4 GiB pages",
            "u64": "uint64"}[args.index_dtype]
     cfg = (f"'\\n' index ({idx}), {size / GiB:g} GiB cities.csv-shaped object per GPU (BASELINE configs[2])"
            if csv_mode else
@@ -868,9 +909,10 @@ def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
                      "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                      "kernel": allres[0]["kernel"], "kernel_avg_us": round(kern * 1e6, 2),
                      "alg_bytes_per_launch": int(allres[0]["alg_bytes"]),
-                     "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)%s" % (
-                         {"u16b": 2, "u32p": 4, "u64": 8}[args.index_dtype],
-                         " + 8 B per 64 KiB block" if args.index_dtype == "u16b" else ""),
+                     "alg_bytes_def": "N + %d * L (N input bytes read once, L offsets written)%s%s" % (
+                         {"u8s": 1, "u16b": 2, "u32p": 4, "u64": 8}[args.index_dtype],
+                         " + 2 B per 256 B" if args.index_dtype == "u8s" else "",
+                         " + 8 B per 64 KiB block" if args.index_dtype in ("u8s", "u16b") else ""),
                      "measured_peak": None if peak_meas is None else round(peak_meas / 1e9, 1),
                      "frac_of_measured_peak": None if peak_meas is None else round(ach / peak_meas, 4),
                      "measured_mixed_ref": None if mixed is None else round(mixed / 1e9, 1),
@@ -934,6 +976,7 @@ def main(argv=None):
             budgets = {"e2e": 90.0, "fastq": 45.0}
             for name, fn in (("e2e", lambda: e2e_legs.e2e_leg(args.e2e_fasta_size, args.e2e_csv_size,
                                                                verify_blocked=_verify_blocked,
+                                                               verify_bytes=_verify_bytes,
                                                                verify=not args.no_verify, log=log)),
                              ("fastq", lambda: e2e_legs.fastq_leg(tiles=args.fastq_tiles, verify=not args.no_verify,
                                                                   log=log))):

@@ -137,8 +137,10 @@ struct ScanArgs {
   uint64_t cap;                // entries (FASTA: pairs)
   int out_u64;
   uint32_t wrap32;             // DELIM uint32 output as low words (paged index): no overflow check
-  unsigned long long* blocktab;  // DELIM uint16 output: entries before each 64 KiB boundary (index - tab_j0)
+  unsigned long long* blocktab;  // DELIM uint16 / uint8 output: entries before each 64 KiB boundary (index - tab_j0)
   uint64_t tab_j0, tab_n;
+  uint16_t* subtab;            // DELIM uint8 output: low 16 bits of the entries before each 256-byte boundary
+  uint64_t sub_s0, sub_n;      // (index - sub_s0)
   uint64_t carry;              // DELIM: delimiters before this launch's first byte (a streamed object's pieces)
   uint32_t delim;              // DELIM: byte replicated x4
   uint32_t every_k;
@@ -257,6 +259,11 @@ __device__ __forceinline__ void set_prio(uint32_t p) {
     default: __builtin_amdgcn_s_setprio(3); break;
   }
 }
+
+// the element type of an output form: 0 uint32, 1 uint64, 2 uint16 low words, 3 uint8 low bytes
+template <int OUT64>
+using OutOf = typename std::conditional<OUT64 == 1, uint64_t, typename std::conditional<OUT64 == 2, uint16_t,
+              typename std::conditional<OUT64 == 3, uint8_t, uint32_t>::type>::type>::type;
 
 template <typename T, bool NT = false>
 __device__ __forceinline__ void put(void* out, uint64_t i, uint64_t v) {
@@ -846,14 +853,40 @@ __device__ __forceinline__ void phase_a_rec(PhaseA& pa, const Geo& g, int wave, 
   rec.nev = dense ? 0u : st.nev;
 }
 
+// uint8 output (out_mode 4): the low 16 bits of `count`, the entries before the 256-byte boundary at range position
+// `key` (16-byte aligned, as every range starts 16-byte aligned and object offsets are congruent to device addresses
+// mod 16), when that boundary is one of the launch's and lies inside the range's chunk bytes [lo, hi): each boundary
+// of the contiguous ranges is then written by exactly one range.  Within a 64 KiB block the counts before its 256
+// boundaries differ from the block table's entry by at most 255 x 256 < 2^16, so 16 bits locate every entry.
+__device__ __forceinline__ void put_sub(const ScanArgs& A, uint64_t off0, int key, int lo, int hi, uint64_t count) {
+  const uint64_t b = off0 + (uint64_t)key;
+  if ((b & 255u) != 0u || key < lo || key >= hi || key >= kWaveBytes) return;
+  const uint64_t s = (b >> 8) - A.sub_s0;
+  if ((b >> 8) >= A.sub_s0 && s < A.sub_n) __builtin_nontemporal_store((uint16_t)count, A.subtab + s);
+}
+// ... for a range's sorted position list: lane l takes the range's l-th 256-byte boundary (a range of 16 KiB holds
+// exactly 64) and counts the positions before it by a binary search over the list.  (Counting the boundaries between
+// consecutive entries instead, through an LDS scratch run, measured 7 % slower on CSV and 3 % on VCF.)
+template <class Ev>
+__device__ __forceinline__ void place_subs(const ScanArgs& A, Ev&& ev, uint32_t nev, uint64_t P, uint64_t off0, int lo,
+                                           int hi, int lane) {
+  const int key = (int)(((off0 + 255u) & ~255ull) - off0) + 256 * lane;
+  uint32_t a = 0, b = nev;
+  while (a < b) {
+    const uint32_t m = (a + b) >> 1;
+    if ((int)ev(m) < key) a = m + 1u;
+    else b = m;
+  }
+  put_sub(A, off0, key, lo, hi, P + a);
+}
+
 // Dense phase B: rescan the range from the input with its true state and count, writing the output
 // directly.  Plain loads (the compiler waits for them; the older in-flight prefetch only makes those
 // waits conservative).  Runs only where the other buffer's registers are free (after phase A).
 template <int MODE, int OUT64>
 __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint32_t lohi, uint64_t P, uint32_t S,
                                         int lane) {
-  typedef typename std::conditional<OUT64 == 1, uint64_t,
-                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
+  typedef OutOf<OUT64> OutT;
   const int lo = (int)(lohi & 0xFFFFu), hi = (int)(lohi >> 16);
   const int hi16 = (hi + 15) & ~15;
   const uint8_t* src = A.base + wbase;
@@ -900,7 +933,18 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
     };
     const uint32_t key = A.delim ^ kSel12;
 #pragma unroll 1
-    for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) delim_row<false>(row_in(r), r, lo, hi, key, lane, n, out);
+    for (int r = 0; r < kRangeRows && r * kRowBytes < hi; ++r) {
+      const v4u x = row_in(r);
+      if constexpr (OUT64 == 3) {
+        // the 256-byte boundaries of this row: the lane whose 16 bytes start at one counts the delimiters before it
+        const int a = r * kRowBytes + lane * 16;
+        uint32_t tot;
+        const uint32_t m = pack16(match4(x[0], key), match4(x[1], key), match4(x[2], key), match4(x[3], key));
+        const uint32_t ex = wave_excl<5>((uint32_t)__popc(m & range16(lo - a, hi - a)), tot);
+        put_sub(A, obj_off, a, lo, hi, P + n + ex);
+      }
+      delim_row<false>(x, r, lo, hi, key, lane, n, out);
+    }
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
@@ -913,8 +957,7 @@ __device__ __forceinline__ void dense_b(const ScanArgs& A, uint64_t wbase, uint3
 template <int OUT64, bool PAIR = true, class Ev>
 __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_t nev, uint64_t P, uint64_t obj_off,
                                              int lane) {
-  typedef typename std::conditional<OUT64 == 1, uint64_t,
-                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
+  typedef OutOf<OUT64> OutT;
   const bool near4g = OUT64 == 0 && !A.wrap32 && obj_off + kWaveBytes + 1 > 0xFFFFFFFFull;
   bool ovf = false;
   const uint64_t last = A.cap - 1, add = obj_off + A.emit_add;
@@ -976,6 +1019,32 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
       return false;
     }
   }
+  if constexpr (OUT64 == 3) {
+    // uint8 low bytes (out_mode 4): sixteen entries per lane, one 16-byte store; the first (16 - q0 % 16) % 16
+    // entries go alone so that the groups are 16-byte aligned
+    if (k == 1u && q0 + nq <= A.cap && ((uintptr_t)A.out & 15u) == 0) {
+      uint8_t* o = reinterpret_cast<uint8_t*>(A.out) + q0;
+      const uint32_t hh = (uint32_t)((16u - (uint32_t)(q0 & 15u)) & 15u);
+      const uint32_t h = hh < nq ? hh : nq;
+      if ((uint32_t)lane < h) o[lane] = (uint8_t)(add + ev((uint32_t)lane));
+      const uint32_t m = nq - h, g = m >> 4;
+      const uint32_t a8 = (uint32_t)add & 0xFFu;
+      for (uint32_t t = (uint32_t)lane; t < g; t += kWave) {
+        const uint32_t i = h + 16u * t;
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t b0 = (a8 + ev(i + 4u * e)) & 0xFFu, b1 = (a8 + ev(i + 4u * e + 1u)) & 0xFFu;
+          const uint32_t b2 = (a8 + ev(i + 4u * e + 2u)) & 0xFFu, b3 = (a8 + ev(i + 4u * e + 3u)) & 0xFFu;
+          w[e] = b0 | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        }
+        const v4u pk = {w[0], w[1], w[2], w[3]};
+        __builtin_nontemporal_store(pk, reinterpret_cast<v4u*>(o + i));
+      }
+      for (uint32_t t = h + 16u * g + (uint32_t)lane; t < nq; t += kWave) o[t] = (uint8_t)(add + ev(t));
+      return false;
+    }
+  }
   for (uint32_t t = (uint32_t)lane; t < nq; t += kWave) {
     const uint64_t q = q0 + t;
     const uint64_t val = add + ev(r0 + t * k);
@@ -994,16 +1063,15 @@ __device__ __forceinline__ bool place_delims(const ScanArgs& A, Ev&& ev, uint32_
 template <int MODE, int OUT64>
 __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t s, int wave, int lane,
                                         uint32_t& ev_tail) {
-  typedef typename std::conditional<OUT64 == 1, uint64_t,
-                                    typename std::conditional<OUT64 == 2, uint16_t, uint32_t>::type>::type OutT;
+  typedef OutOf<OUT64> OutT;
   const WaveRec& rr = sh.rec[s][wave];
   const uint64_t wbase = rfl64(rr.wbase);
   const uint32_t fl = rfl(rr.fl), ev0 = rfl(rr.ev0), nev = rfl(rr.nev);
   const uint64_t P = rfl64(sh.P[s][wave]);
   const uint32_t S = rfl(sh.S[s][wave]);
   ev_tail = ev0 + nev;
-  if constexpr (MODE == kDelim && OUT64 == 2) {
-    // uint16 low words: the entries before every 64 KiB boundary that starts a wave range (the ranges are
+  if constexpr (MODE == kDelim && OUT64 >= 2) {
+    // uint16 / uint8 low words: the entries before every 64 KiB boundary that starts a wave range (the ranges are
     // split at the first such boundary, so every later one starts a range) locate each entry's block
     // Written only by the range whose chunk holds the boundary byte itself (lo_w == 0, hi_w > 0): a range
     // past the end of a chunk's last unit would write the count at that chunk's end, and the first range of
@@ -1036,8 +1104,12 @@ __device__ __forceinline__ void phase_b(const ScanArgs& A, Shared& sh, uint32_t 
       put<OutT>(A.out, slot < last ? slot : last, val);
     }
   } else {
-    ovf = place_delims<OUT64>(A, [&](uint32_t i) { return (uint32_t)evw[(ev0 + i) & kEvMask]; }, nev, P, obj_off,
-                              lane);
+    auto ev = [&](uint32_t i) { return (uint32_t)evw[(ev0 + i) & kEvMask]; };
+    ovf = place_delims<OUT64>(A, ev, nev, P, obj_off, lane);
+    if constexpr (OUT64 == 3) {
+      const uint32_t lohi = rfl(rr.lohi);
+      place_subs(A, ev, nev, P, obj_off, (int)(lohi & 0xFFFFu), (int)(lohi >> 16), lane);
+    }
   }
   if (ovf) atomicOr(A.err, kErrOverflow);
 }
@@ -2180,7 +2252,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
     if (lane == 0) {
       if (gq.z & kLineLast) A.chunk_end[gq.w] = Pw + n;
       if (gq.z & kLineEnd) A.total[0] = Pw + n;
-      if constexpr (OUT64 == 2) {
+      if constexpr (OUT64 >= 2) {
         // the entries before every 64 KiB boundary that starts a range of this chunk (phase_b)
         const uint64_t j = (off0 >> 16) - A.tab_j0;
         if ((off0 & 0xFFFFull) == 0 && lo_w == 0 && hi_w != 0 && off0 >= (A.tab_j0 << 16) && j < A.tab_n)
@@ -2192,8 +2264,10 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) line_kernel(LineArgs L, 
       return;
     }
     const uint16_t* evw = sh.ev[s][w];
+    auto ev = [&](uint32_t i) { return (uint32_t)evw[i]; };
     // (uint64 output without the paired stores: their registers would push this kernel past 128 VGPRs)
-    ovf |= place_delims<OUT64, false>(A, [&](uint32_t i) { return (uint32_t)evw[i]; }, n, Pw, off0, lane);
+    ovf |= place_delims<OUT64, false>(A, ev, n, Pw, off0, lane);
+    if constexpr (OUT64 == 3) place_subs(A, ev, n, Pw, off0, (int)lo_w, (int)hi_w, lane);
   };
   // (wave 0) step q's AGG: the group's count from its 16 ranges (lanes 0..15), with every range's exclusive prefix
   auto publish_agg = [&](uint32_t q) {
@@ -2742,11 +2816,13 @@ struct dp_ctx {
 
 std::atomic<uint64_t> g_dev_allocs{0}, g_host_allocs{0};
 
-// The newline kernels of a launch scanning `span` bytes: 1 line_kernel, 3 one-pass, or 0 when the launch's own bytes
-// decide on the device (auto above delim_line_max)
-static int delim_form_for(const dp_ctx* c, uint64_t span) {
+// The newline kernels of a launch scanning `span` bytes into `out_mode`: 1 line_kernel, 3 one-pass, or 0 when the
+// launch's own bytes decide on the device (auto above delim_line_max).  The uint8 index (out_mode 4) takes line_kernel
+// at every size: the one-pass kernel's phase B, on its data waves' path, pays for the 256-byte counts (VCF 16 GiB
+// 2,740 vs line_kernel's 2,639 us, profiles/r05/u8).
+static int delim_form_for(const dp_ctx* c, uint64_t span, int out_mode) {
   if (c->delim_form == (int)kFormLine || c->delim_form == (int)kFormOne) return c->delim_form;
-  return span <= c->delim_line_max ? (int)kFormLine : 0;
+  return span <= c->delim_line_max || out_mode == 4 ? (int)kFormLine : 0;
 }
 
 namespace {
@@ -2991,6 +3067,8 @@ int enq_scan(dp_ctx* c, hipStream_t ss, int mode, int kind, const ScanArgs& a) {
     hipLaunchKernelGGL((scan_kernel<kFasta, 1>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else if (kind == 2)
     hipLaunchKernelGGL((scan_kernel<kDelim, 2>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
+  else if (kind == 3)
+    hipLaunchKernelGGL((scan_kernel<kDelim, 3>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else if (kind == 0)
     hipLaunchKernelGGL((scan_kernel<kDelim, 0>), dim3(grid), dim3(kThreads), 0, ss, a, tlo, thi, tu0);
   else
@@ -3083,6 +3161,7 @@ int enq_line(dp_ctx* c, hipStream_t ss, int kind, const ScanArgs& a, uint64_t nr
   const dim3 grid(map_grid(c, nranges)), blk(kWave * kMapWaves);
   if (kind == 1) hipLaunchKernelGGL((line_kernel<1>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
   else if (kind == 2) hipLaunchKernelGGL((line_kernel<2>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
+  else if (kind == 3) hipLaunchKernelGGL((line_kernel<3>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
   else hipLaunchKernelGGL((line_kernel<0>), grid, blk, 0, ss, L, a, tlo, thi, tr0);
   HIPCHK(hipGetLastError());
   ++c->line_launches;
@@ -3368,28 +3447,33 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   if (c->inflight >= 0) return fail(DP_ERR_INVALID, "a scan is already in flight on this ctx");
   if (every_k == 0) return fail(DP_ERR_INVALID, "every_k must be >= 1");
   if (delim > 255) return fail(DP_ERR_INVALID, "delim must be a byte");
-  if (out_mode < 0 || out_mode > 3)
-    return fail(DP_ERR_INVALID, "out_mode must be 0 (uint32), 1 (uint64), 2 (uint32 low words) or 3 (uint16 + blocks)");
+  if (out_mode < 0 || out_mode > 4)
+    return fail(DP_ERR_INVALID, "out_mode must be 0 (uint32), 1 (uint64), 2 (uint32 low words), 3 (uint16 + blocks) or "
+                                "4 (uint8 + 256-byte counts + blocks)");
   if (nranges == 0 || !ranges) return fail(DP_ERR_INVALID, "no ranges");
-  // the block table holds delimiter ordinals before each 64 KiB boundary: entry indexes only when every
-  // delimiter is an entry, and the low 16 bits locate an entry in its block only without an added offset
-  if (out_mode == 3 && (every_k != 1 || emit_add != 0))
-    return fail(DP_ERR_INVALID, "out_mode 3 needs every_k == 1 and emit_add == 0");
+  const bool blocked = out_mode >= 3;
+  const std::string om = "out_mode " + std::to_string(out_mode);
+  // the block tables hold delimiter ordinals before each 64 KiB / 256-byte boundary: entry indexes only when every
+  // delimiter is an entry, and the low 16 / 8 bits locate an entry in its block only without an added offset
+  if (blocked && (every_k != 1 || emit_add != 0))
+    return fail(DP_ERR_INVALID, om + " needs every_k == 1 and emit_add == 0");
   for (uint64_t i = 0; i < nranges; ++i) {
     if (ranges[2 * i + 1] > ranges[2 * i] && !d_buf) return fail(DP_ERR_INVALID, "null buffer");
     if (ranges[2 * i + 1] < ranges[2 * i]) return fail(DP_ERR_INVALID, "range end before its start");
     if (i && ranges[2 * i] < ranges[2 * i - 1]) return fail(DP_ERR_INVALID, "ranges must ascend without overlap");
-    if (out_mode == 3 && i && ranges[2 * i] != ranges[2 * i - 1])
-      return fail(DP_ERR_INVALID, "out_mode 3 needs contiguous ranges");
+    if (blocked && i && ranges[2 * i] != ranges[2 * i - 1])
+      return fail(DP_ERR_INVALID, om + " needs contiguous ranges");
   }
   if (cap && !d_out) return fail(DP_ERR_INVALID, "null output with cap > 0");
-  // out_mode 3: split each range at its first 64 KiB boundary, so that every later boundary starts a wave
-  // range (the kernel records the entries before it there); the block table follows the entries in d_out
+  // out_mode 3 / 4: split each range at its first 64 KiB boundary, so that every later boundary starts a wave
+  // range (the kernel records the entries before it there); the block table follows the entries in d_out, and for
+  // out_mode 4 the 256-byte table follows the block table
   std::vector<uint64_t> rg(ranges, ranges + 2 * nranges);
   c->range_map.clear();
   unsigned long long* tab = nullptr;
-  uint64_t j0 = 0, ntab = 0;
-  if (out_mode == 3) {
+  uint16_t* sub = nullptr;
+  uint64_t j0 = 0, ntab = 0, s0 = 0, nsub = 0;
+  if (blocked) {
     rg.clear();
     for (uint64_t i = 0; i < nranges; ++i) {
       const uint64_t lo = ranges[2 * i], hi = ranges[2 * i + 1];
@@ -3403,25 +3487,36 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
     }
     // wave ranges start 16-byte aligned in buffer coordinates: object offsets must share that alignment
     if ((((uintptr_t)d_buf) - buf_base) & 15u)
-      return fail(DP_ERR_INVALID, "out_mode 3 needs d_buf and buf_base congruent mod 16 (place the bytes at "
-                                  "an address whose low 4 bits equal buf_base's)");
+      return fail(DP_ERR_INVALID, om + " needs d_buf and buf_base congruent mod 16 (place the bytes at "
+                                       "an address whose low 4 bits equal buf_base's)");
     const uint64_t first = ranges[0], last = ranges[2 * nranges - 1];
     j0 = first >> 16;
     ntab = last > first ? ((last - 1) >> 16) - j0 + 1 : 1;
-    tab = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(d_out) + ((2 * cap + 15) & ~15ull));
-    if (!d_out) return fail(DP_ERR_INVALID, "out_mode 3 needs an output buffer (entries + block table)");
-    if (((uintptr_t)d_out) & 15u) return fail(DP_ERR_INVALID, "out_mode 3 needs a 16-byte aligned output buffer");
+    const uint64_t item = out_mode == 3 ? 2 : 1;
+    const uint64_t tab_off = (item * cap + 15) & ~15ull;
+    tab = reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(d_out) + tab_off);
+    if (out_mode == 4) {
+      s0 = first >> 8;
+      nsub = last > first ? ((last - 1) >> 8) - s0 + 1 : 1;
+      sub = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(d_out) + ((tab_off + 8 * ntab + 15) & ~15ull));
+    }
+    if (!d_out) return fail(DP_ERR_INVALID, om + " needs an output buffer (entries + block tables)");
+    if (((uintptr_t)d_out) & 15u) return fail(DP_ERR_INVALID, om + " needs a 16-byte aligned output buffer");
   }
   const uint64_t nr = rg.size() / 2;
   uint64_t nr16 = 0, units = 0, span = 0;
   for (uint64_t i = 0; i < nr; ++i) span += rg[2 * i + 1] - rg[2 * i];
-  const int kind = out_mode == 1 ? 1 : (out_mode == 3 ? 2 : 0);
-  const int dform = delim_form_for(c, span);
+  const int kind = out_mode == 1 ? 1 : out_mode == 3 ? 2 : out_mode == 4 ? 3 : 0;
+  const int dform = delim_form_for(c, span, out_mode);
   rc = stage_chunks(c, d_buf, buf_len, buf_base, rg.data(), nr, &nr16, &units);
   if (rc) return rc;
   auto args = [&](uint64_t nu) {
-    return scan_args(c, d_buf, buf_base, nr, nu, d_out, kind, cap, delim, every_k, emit_add, carry, out_mode == 2, tab,
-                     j0, ntab);
+    ScanArgs a = scan_args(c, d_buf, buf_base, nr, nu, d_out, kind, cap, delim, every_k, emit_add, carry, out_mode == 2,
+                           tab, j0, ntab);
+    a.subtab = sub;
+    a.sub_s0 = s0;
+    a.sub_n = nsub;
+    return a;
   };
   const uint64_t ngroups = (nr16 + kMapWaves - 1) / kMapWaves;
   if (!nr16) {
@@ -3659,9 +3754,9 @@ int dp_last_delim_form(dp_ctx* c, int* form) {
   return DP_OK;
 }
 
-int dp_scan_delim_form(dp_ctx* c, uint64_t span, int* form) {
+int dp_scan_delim_form(dp_ctx* c, uint64_t span, int out_mode, int* form) {
   if (!c || !form) return fail(DP_ERR_INVALID, "null");
-  *form = delim_form_for(c, span);
+  *form = delim_form_for(c, span, out_mode);
   return DP_OK;
 }
 

@@ -27,7 +27,10 @@ _BLOCK = 8192                      # entries per cached block for large indexes
 def store_line_index(cloud_object, offsets) -> dict:
     """PUT the index at ``<key>.lines``; returns the attributes that describe it.
 
-    * ``scan.objects.BlockedOffsets`` (the default build, ``line_index_dtype="u16b"``): uint16 LE low words,
+    * ``scan.objects.ByteOffsets`` (``line_index_dtype="u8s"``): uint8 low bytes, the 256-byte counts (uint16 LE) at
+      ``<key>.lines.sub`` and the 64 KiB block table (uint64 LE) at ``<key>.lines.blocks``, their first boundaries in
+      the attributes;
+    * ``scan.objects.BlockedOffsets`` (``line_index_dtype="u16b"``): uint16 LE low words,
       the 64 KiB block table (uint64 LE) at ``<key>.lines.blocks``, its first block in the attributes;
     * ``scan.objects.PagedOffsets`` (``"u32p"``): uint32 LE low words, the 4 GiB page counts in the attributes;
     * a plain array: uint64 LE."""
@@ -35,7 +38,14 @@ def store_line_index(cloud_object, offsets) -> dict:
     st, bucket = cloud_object.storage, cloud_object.meta_path.bucket
     meta = {"dataplug": __version__}
     attrs = {"line_index_key": key, "num_lines": int(len(offsets))}
-    if hasattr(offsets, "table"):
+    if hasattr(offsets, "sub"):
+        st.put_object(Body=np.ascontiguousarray(offsets.low, np.uint8).data, Bucket=bucket, Key=key, Metadata=meta)
+        skey, bkey = key + ".sub", key + ".blocks"
+        st.put_object(Body=np.ascontiguousarray(offsets.sub, "<u2").data, Bucket=bucket, Key=skey, Metadata=meta)
+        st.put_object(Body=np.ascontiguousarray(offsets.table, "<u8").data, Bucket=bucket, Key=bkey, Metadata=meta)
+        attrs.update(line_index_dtype="u8s", line_index_sub_key=skey, line_index_sub0=int(offsets.s0),
+                     line_index_blocks_key=bkey, line_index_block0=int(offsets.j0))
+    elif hasattr(offsets, "table"):
         st.put_object(Body=np.ascontiguousarray(offsets.low, "<u2").tobytes(), Bucket=bucket, Key=key, Metadata=meta)
         bkey = key + ".blocks"
         st.put_object(Body=np.ascontiguousarray(offsets.table, "<u8").tobytes(), Bucket=bucket, Key=bkey,
@@ -53,17 +63,19 @@ class LineIndex:
     """Sorted newline offsets; ``nxt(x)`` = 1 + first '\n' at or after x (None if none).
 
     Reads every stored form (uint64 words; uint32 low words + 4 GiB page counts; uint16 low words + 64 KiB
-    block table), fetching blocks of entries by ranged GETs when the index is large."""
+    block table; uint8 low bytes + 256-byte counts + 64 KiB block table), fetching blocks of entries by ranged GETs
+    when the index is large (for the uint8 form with the 256-byte counts of the blocks they span)."""
 
     def __init__(self, offsets: Optional[np.ndarray] = None, storage=None, bucket: str = "", key: str = "",
                  count: Optional[int] = None, pages: Optional[list] = None, blocks: Optional[np.ndarray] = None,
-                 block0: int = 0):
+                 block0: int = 0, sub_key: Optional[str] = None, sub0: int = 0):
         self._arr = None if offsets is None else np.asarray(offsets, dtype=np.uint64)
         self._storage, self._bucket, self._key = storage, bucket, key
         self._pages = None if pages is None else np.asarray(pages, np.int64)
         self._blocks_tab = None if blocks is None else np.asarray(blocks, np.int64)
         self._block0 = int(block0)
-        self._item = 2 if blocks is not None else (4 if pages is not None else 8)
+        self._sub_key, self._sub0 = sub_key, int(sub0)
+        self._item = 1 if sub_key is not None else (2 if blocks is not None else (4 if pages is not None else 8))
         self._blocks: "OrderedDict[int, np.ndarray]" = OrderedDict()
         if self._arr is None:
             if count is None:
@@ -84,11 +96,14 @@ class LineIndex:
         kw = {}
         if dt == "u32p":
             kw["pages"] = list(getattr(attrs, "line_index_pages"))
-        elif dt == "u16b":
+        elif dt in ("u16b", "u8s"):
             res = cloud_object.storage.get_object(Bucket=cloud_object.meta_path.bucket,
                                                   Key=getattr(attrs, "line_index_blocks_key"))
             kw["blocks"] = np.frombuffer(res["Body"].read(), "<u8")
             kw["block0"] = int(getattr(attrs, "line_index_block0"))
+            if dt == "u8s":
+                kw["sub_key"] = getattr(attrs, "line_index_sub_key")
+                kw["sub0"] = int(getattr(attrs, "line_index_sub0"))
         return cls(storage=cloud_object.storage, bucket=cloud_object.meta_path.bucket, key=key,
                    count=getattr(attrs, "num_lines", None), **kw)
 
@@ -104,6 +119,19 @@ class LineIndex:
         if it == 4:
             page = np.searchsorted(self._pages, idx, side="right").astype(np.uint64)
             return (page << np.uint64(32)) | np.frombuffer(raw, dtype="<u4").astype(np.uint64)
+        if it == 1:
+            # the 256-byte boundaries of the 64 KiB blocks entries i0 .. i1 - 1 lie in, and the counts before them
+            from ..scan.objects import sub_counts
+            ja = int(np.searchsorted(self._blocks_tab, i0, side="right")) - 1
+            jb = int(np.searchsorted(self._blocks_tab, i1 - 1, side="right")) - 1
+            s0 = self._sub0
+            sa = max(0, ((self._block0 + ja) << 8) - s0)
+            sb = ((self._block0 + jb + 1) << 8) - s0
+            res = self._storage.get_object(Bucket=self._bucket, Key=self._sub_key, Range=f"bytes={2 * sa}-{2 * sb - 1}")
+            sub = np.frombuffer(res["Body"].read(), dtype="<u2")
+            c = sub_counts(sub, self._blocks_tab.astype(np.uint64), s0, self._block0, sa)
+            s = np.searchsorted(c, idx.astype(np.uint64), side="right").astype(np.uint64) - np.uint64(1) + np.uint64(sa)
+            return ((s + np.uint64(s0)) << np.uint64(8)) | np.frombuffer(raw, dtype=np.uint8).astype(np.uint64)
         blk = np.searchsorted(self._blocks_tab, idx, side="right").astype(np.uint64) - np.uint64(1)
         return ((blk + np.uint64(self._block0)) << np.uint64(16)) | np.frombuffer(raw, dtype="<u2").astype(np.uint64)
 

@@ -26,7 +26,7 @@ logger = logging.getLogger(__name__)
 
 
 def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index: bool = True,
-                   index_format: str = "u16b") -> PreprocessingMetadata:
+                   index_format: str = "u8s") -> PreprocessingMetadata:
     import pandas as pd
 
     top = []

@@ -59,7 +59,7 @@ def parse_vcf_header(f):
     return header, meta, columns, pos
 
 
-def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True, index_format: str = "u16b") -> PreprocessingMetadata:
+def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True, index_format: str = "u8s") -> PreprocessingMetadata:
     with cloud_object.open("rb") as f:
         header, meta, columns, body_offset = parse_vcf_header(f)
     attrs = {"columns": columns, "vcf_attributes": meta, "body_offset": body_offset}

@@ -72,7 +72,7 @@ SIGNATURES = [
     ("dp_alloc_counts", _c.c_int, [_u64p, _u64p]),
     ("dp_ctx_set_form", _c.c_int, [_p, _c.c_int, _u64]),
     ("dp_ctx_get_form", _c.c_int, [_p, _c.c_int, _u64p]),
-    ("dp_scan_delim_form", _c.c_int, [_p, _u64, _c.POINTER(_c.c_int)]),
+    ("dp_scan_delim_form", _c.c_int, [_p, _u64, _c.c_int, _c.POINTER(_c.c_int)]),
     ("dp_last_delim_form", _c.c_int, [_p, _c.POINTER(_c.c_int)]),
     ("dp_scan_geometry", _c.c_int, [_p, _c.POINTER(_c.c_int), _c.POINTER(_c.c_int)]),
 ]

@@ -254,27 +254,54 @@ class ScanContext:
         return j0, (((last - 1) >> 16) - j0 + 1) if last > first else 1
 
     @staticmethod
+    def sub_table_size(ranges: np.ndarray) -> Tuple[int, int]:
+        """(s0, entries) of the 256-byte table out_mode 4 writes for these ranges."""
+        first, last = int(ranges[0]), int(ranges[-1])
+        s0 = first >> 8
+        return s0, (((last - 1) >> 8) - s0 + 1) if last > first else 1
+
+    @staticmethod
+    def _tab_off(cap: int, out_mode: int) -> int:
+        return ((2 if out_mode == 3 else 1) * cap + 15) & ~15
+
+    @staticmethod
+    def _sub_off(cap: int, ranges: np.ndarray) -> int:
+        return (ScanContext._tab_off(cap, 4) + 8 * ScanContext.block_table_size(ranges)[1] + 15) & ~15
+
+    @staticmethod
     def out_bytes(cap: int, out_mode: int, ranges: np.ndarray) -> int:
-        """Bytes of a dp_delim_ranges output buffer for ``cap`` entries (out_mode 3: + the block table)."""
+        """Bytes of a dp_delim_ranges output buffer for ``cap`` entries (out_mode 3: + the block table; 4: + the
+        block table and the 256-byte table)."""
         if out_mode == 3:
-            return ((2 * cap + 15) & ~15) + 8 * ScanContext.block_table_size(ranges)[1] + 16
+            return ScanContext._tab_off(cap, 3) + 8 * ScanContext.block_table_size(ranges)[1] + 16
+        if out_mode == 4:
+            return ScanContext._sub_off(cap, ranges) + 2 * ScanContext.sub_table_size(ranges)[1] + 16
         return cap * (8 if out_mode == 1 else 4) + 16
 
-    def block_table(self, d_out: int, cap: int, ranges: np.ndarray) -> np.ndarray:
-        """The 64 KiB block table of an out_mode 3 result: entries before (j0 + j) * 64 KiB (this launch)."""
+    def block_table(self, d_out: int, cap: int, ranges: np.ndarray, out_mode: int = 3) -> np.ndarray:
+        """The 64 KiB block table of an out_mode 3 / 4 result: entries before (j0 + j) * 64 KiB (this launch)."""
         j0, nt = self.block_table_size(ranges)
-        tab = self.d2h(np.empty(nt, np.uint64), d_out + ((2 * cap + 15) & ~15))
+        tab = self.d2h(np.empty(nt, np.uint64), d_out + self._tab_off(cap, out_mode))
         if int(ranges[0]) & 0xFFFF:
             tab[0] = 0                                   # the boundary below the first byte: not a range start
         return tab
 
+    def sub_table(self, d_out: int, cap: int, ranges: np.ndarray) -> np.ndarray:
+        """The 256-byte table of an out_mode 4 result: low 16 bits of the entries before (s0 + s) * 256."""
+        s0, ns = self.sub_table_size(ranges)
+        sub = self.d2h(np.empty(ns, np.uint16), d_out + self._sub_off(cap, ranges))
+        if int(ranges[0]) & 0xFF:
+            sub[0] = 0                                   # the boundary below the first byte
+        return sub
+
     def delim_ranges(self, d_buf: int, buf_len: int, buf_base: int, ranges, delim: int = 10, every_k: int = 1,
                      emit_add: int = 0, carry: int = 0, out_mode: int = 1, cap: Optional[int] = None):
         """Synchronous dp_delim_ranges: (offsets, delimiters seen, per-range cumulative counts); out_mode 1
-        uint64, 0 uint32, 2 uint32 low words, 3 uint16 low words (+ ``block_table``, returned as a 4th item)."""
+        uint64, 0 uint32, 2 uint32 low words, 3 uint16 low words (+ ``block_table``, returned as a 4th item), 4 uint8
+        low bytes (+ ``block_table`` and ``sub_table``, a 4th and 5th item)."""
         rg = np.ascontiguousarray(np.asarray(ranges, dtype=np.uint64).reshape(-1))
         span = int(sum(int(rg[2 * i + 1]) - int(rg[2 * i]) for i in range(len(rg) // 2)))
-        dtype = {0: np.uint32, 1: np.uint64, 2: np.uint32, 3: np.uint16}[out_mode]
+        dtype = {0: np.uint32, 1: np.uint64, 2: np.uint32, 3: np.uint16, 4: np.uint8}[out_mode]
         if cap is None:
             cap = span // (16 * every_k) + 1024
         while True:
@@ -289,6 +316,8 @@ class ScanContext:
             vals = self.d2h(np.empty(n, dtype), out.ptr)
             if out_mode == 3:
                 return vals, nd, ends, self.block_table(out.ptr, cap, rg)
+            if out_mode == 4:
+                return vals, nd, ends, self.block_table(out.ptr, cap, rg, 4), self.sub_table(out.ptr, cap, rg)
             return vals, nd, ends
 
     def find_delim(self, d_buf: int, buf_len: int, buf_base: int, start: int, delim: int = 10) -> int:
@@ -350,11 +379,11 @@ class ScanContext:
                    1: "line_kernel<DELIM> (lockstep one pass)",
                    3: "scan_kernel<DELIM> (one-pass look-back)"}
 
-    def delim_form(self, span: int) -> int:
-        """The kernels a newline launch of ``span`` bytes takes (dp_scan_delim_form: 1 line, 3 one-pass; 0: the
-        launch's own bytes decide on the device)."""
+    def delim_form(self, span: int, out_mode: int = 3) -> int:
+        """The kernels a newline launch of ``span`` bytes into ``out_mode`` takes (dp_scan_delim_form: 1 line,
+        3 one-pass; 0: the launch's own bytes decide on the device)."""
         f = ctypes.c_int(0)
-        check(self.lib.dp_scan_delim_form(self.handle, int(span), ctypes.byref(f)))
+        check(self.lib.dp_scan_delim_form(self.handle, int(span), int(out_mode), ctypes.byref(f)))
         return int(f.value)
 
     def last_delim_form(self) -> int:

@@ -427,7 +427,40 @@ class BlockedOffsets:
         return ((blk + np.uint64(self.j0)) << np.uint64(16)) | self.low[i0:i1].astype(np.uint64)
 
 
-INDEX_FORMATS = ("u16b", "u32p", "u64")
+def sub_counts(sub: np.ndarray, table: np.ndarray, s0: int, j0: int, sa: int = 0) -> np.ndarray:
+    """Entries before each 256-byte boundary (s0 + sa + i) << 8 of a uint8 index, as uint64: the block table's count
+    at the boundary's 64 KiB block plus the 16-bit difference the sub-block table holds (a 64 KiB block's 256
+    boundaries differ from its first by less than 2^16 entries)."""
+    s = np.arange(sa, sa + len(sub), dtype=np.int64)
+    base = table[((s0 + s) >> 8) - j0].astype(np.uint64)
+    return base + ((sub.astype(np.uint64) - base) & np.uint64(0xFFFF))
+
+
+@dataclass
+class ByteOffsets:
+    """Sorted object offsets as uint8 low bytes, a table of the entries before every 256-byte boundary (their low
+    16 bits) and the 64 KiB block table: offset i = ((s0 + s) << 8) | low[i] with s = bisect_right(C, i) - 1, C the
+    counts before the 256-byte boundaries (``sub_counts``), table[0] / sub[0] = 0 for the boundaries at or below the
+    first byte.  An eighth of the bytes of a uint64 index plus 2 B per 256 input bytes, written by the GPU directly
+    (dp_delim_ranges out_mode 4)."""
+    low: np.ndarray
+    sub: np.ndarray
+    table: np.ndarray
+    s0: int
+    j0: int
+
+    def __len__(self) -> int:
+        return len(self.low)
+
+    def to_u64(self, i0: int = 0, i1: Optional[int] = None) -> np.ndarray:
+        i1 = len(self.low) if i1 is None else i1
+        c = sub_counts(self.sub, self.table, self.s0, self.j0)
+        idx = np.arange(i0, i1, dtype=np.uint64)
+        s = np.searchsorted(c, idx, side="right").astype(np.uint64) - np.uint64(1)
+        return ((s + np.uint64(self.s0)) << np.uint64(8)) | self.low[i0:i1].astype(np.uint64)
+
+
+INDEX_FORMATS = ("u8s", "u16b", "u32p", "u64")
 
 
 def line_parts(begin: int, end: int, n_devices: int, part_bytes: int = 16 << 30) -> List[Tuple[int, int]]:
@@ -453,6 +486,9 @@ def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_
         rg = page_ranges(lo, hi)
         low, nd, ends = ctx.delim_ranges(dp, n, lo, rg, delim=delim, out_mode=2)
         return low, [(r, int(e)) for r, e in zip(rg, ends)]
+    if fmt == "u8s":
+        low, nd, ends, tab, sub = ctx.delim_ranges(dp, n, lo, [(lo, hi)], delim=delim, out_mode=4)
+        return low, tab, sub
     low, nd, ends, tab = ctx.delim_ranges(dp, n, lo, [(lo, hi)], delim=delim, out_mode=3)
     return low, tab
 
@@ -461,7 +497,8 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
                       max_devices: Optional[int] = None, part_bytes: int = 16 << 30, fmt: str = "u64"):
     """Sorted offsets of every ``delim`` byte of object bytes [begin, end) in one of ``INDEX_FORMATS``:
     ``u64`` a uint64 array; ``u32p`` a ``PagedOffsets`` (uint32 low words + 4 GiB page counts); ``u16b`` a
-    ``BlockedOffsets`` (uint16 low words + a 64 KiB block table) — the GPU writes 8, 4 or 2 bytes per offset.
+    ``BlockedOffsets`` (uint16 low words + a 64 KiB block table); ``u8s`` a ``ByteOffsets`` (uint8 low bytes + the
+    256-byte counts + the 64 KiB block table) — the GPU writes 8, 4, 2 or 1 bytes per offset.
 
     The range is cut into independent parts (at most ``part_bytes`` each, at least one per GPU) scanned
     round-robin on the GPUs and concatenated in order."""
@@ -470,7 +507,9 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
     end = co.size if end is None else end
     if end <= begin:
         return {"u64": np.zeros(0, np.uint64), "u32p": PagedOffsets(np.zeros(0, np.uint32), []),
-                "u16b": BlockedOffsets(np.zeros(0, np.uint16), np.zeros(1, np.uint64), begin >> 16)}[fmt]
+                "u16b": BlockedOffsets(np.zeros(0, np.uint16), np.zeros(1, np.uint64), begin >> 16),
+                "u8s": ByteOffsets(np.zeros(0, np.uint8), np.zeros(1, np.uint16), np.zeros(1, np.uint64), begin >> 8,
+                                   begin >> 16)}[fmt]
     devs = devices(max_devices, co)
     bounds = line_parts(begin, end, len(devs), part_bytes)
 
@@ -492,8 +531,8 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
     entries = sorted(by_dev)
     run_on_devices([devs[e] for e in entries], [partial(worker, by_dev[e]) for e in entries])
     if fmt == "u64":
-        return np.concatenate(out)
-    low = np.concatenate([o[0] for o in out])
+        return out[0] if len(out) == 1 else np.concatenate(out)
+    low = out[0][0] if len(out) == 1 else np.concatenate([o[0] for o in out])
     if fmt == "u32p":
         # pages[p - 1] = offsets before p * 2^32: 0 for the boundaries at or below begin, then the running
         # count at every boundary inside (begin, end) — each starts one of the parts' page ranges
@@ -506,17 +545,29 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
                 before += cum - prev
                 prev = cum
         return PagedOffsets(low, pages)
-    # u16b: table[j - J0] = offsets before j * 64 KiB; a boundary inside part k comes from part k's own table
-    # (its count within the part) plus every earlier part's count
+    # u16b / u8s: table[j - J0] = offsets before j * 64 KiB; a boundary inside part k comes from part k's own table
+    # (its count within the part) plus every earlier part's count; so do u8s's 256-byte counts (low 16 bits, wrapping).
+    # A part's boundaries at or after its first byte are all of its table but the first entry when the part starts
+    # off a boundary: slices, no per-entry index arrays (a 16 GiB part has 64 Mi 256-byte counts).
     J0, J1 = begin >> 16, (end - 1) >> 16
+    S0, S1 = begin >> 8, (end - 1) >> 8
+    if len(out) == 1:                                    # one part: [begin, end) itself, its tables as they are
+        o = out[0]
+        return ByteOffsets(low, o[2], o[1], S0, J0) if fmt == "u8s" else BlockedOffsets(low, o[1], J0)
     table = np.zeros(J1 - J0 + 1, np.uint64)
+    subs = np.zeros(S1 - S0 + 1, np.uint16) if fmt == "u8s" else None
     before = 0
-    for (lo, hi), (lw, tab) in zip(bounds, out):
-        j0 = lo >> 16
-        js = np.arange(max(j0, J0), ((hi - 1) >> 16) + 1, dtype=np.int64)
-        inside = (js << 16) >= lo                        # boundaries at or after the part's first byte
-        table[js[inside] - J0] = np.uint64(before) + tab[js[inside] - j0]
-        before += len(lw)
+    for (lo, hi), o in zip(bounds, out):
+        a, b = (lo >> 16) + (1 if lo & 0xFFFF else 0), (hi - 1) >> 16
+        if b >= a:
+            table[a - J0:b - J0 + 1] = o[1][a - (lo >> 16):b - (lo >> 16) + 1] + np.uint64(before)
+        if subs is not None:
+            a, b = (lo >> 8) + (1 if lo & 0xFF else 0), (hi - 1) >> 8
+            if b >= a:
+                subs[a - S0:b - S0 + 1] = o[2][a - (lo >> 8):b - (lo >> 8) + 1] + np.uint16(before & 0xFFFF)
+        before += len(o[0])
+    if subs is not None:
+        return ByteOffsets(low, subs, table, S0, J0)
     return BlockedOffsets(low, table, J0)
 
 

@@ -125,6 +125,19 @@ int dp_delim_result(dp_ctx* ctx, uint64_t* n_out, uint64_t* n_delims);
  *     - d_out must be 16-byte aligned and hold (2 * cap + 15) & ~15 + 8 * J bytes;
  *     - ranges must be contiguous (range i + 1 starts where range i ends), and d_buf and buf_base must be
  *       congruent mod 16 (the kernel's 16-byte lanes then sit on object-aligned 64 KiB boundaries).
+ *   out_mode 4: uint8 low bytes, the low 16 bits of the entries before every 256-byte boundary, and the 64 KiB block
+ *   table -- an eighth of the uint64 index's bytes plus 2 B per 256 input bytes (round 5's stored CSV/VCF index:
+ *   <key>.lines, <key>.lines.sub, <key>.lines.blocks).  Same requirements as out_mode 3, and:
+ *     - d_out[0 .. n_out) are uint8: entry i = offset_i & 0xFF;
+ *     - the block table (as out_mode 3) at byte offset (cap + 15) & ~15 of d_out;
+ *     - then, at byte offset (((cap + 15) & ~15) + 8 * J + 15) & ~15, uint16 sub[s] for s = 0 .. S-1,
+ *       S = ((last - 1) >> 8) - s0 + 1 (1 if last == first), s0 = first >> 8: sub[s] = (entries before object offset
+ *       (s0 + s) << 8) & 0xFFFF.  Within a 64 KiB block the counts before its 256-byte boundaries exceed the block's
+ *       tab entry by less than 2^16, so the full count is tab[j] + ((sub[s] - tab[j]) mod 2^16) for the block j
+ *       holding the boundary, and entry i's offset is ((s0 + s) << 8) + low byte for the s with
+ *       count(s) <= i < count(s + 1).  When `first` is not a multiple of 256, sub[0] stands for a boundary below the
+ *       first byte and is not written: read it as 0;
+ *     - d_out must hold that offset + 2 * S bytes.
  *   range_end (host array of nranges, may be NULL): delimiters up to and including range i.
  */
 int dp_delim_ranges_async(dp_ctx* ctx, const uint8_t* d_buf, uint64_t buf_len, uint64_t buf_base,
@@ -164,13 +177,13 @@ int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
 /* The kernels a ctx's scans take.  The defaults are the shipped choices; a library reads no environment
  * variable, so only these calls change them (tests and same-box A/B runs):
  *   DP_FORM_FASTA           0 = map + placement kernels (default), 1 = the one-pass look-back kernel;
- *   DP_FORM_DELIM           0 = auto (default), 1 = line_kernel (lockstep one pass), 2 = map + placement
- *                           kernels, 3 = the one-pass look-back kernel, at every launch size;
+ *   DP_FORM_DELIM           0 = auto (default), 1 = line_kernel (lockstep one pass), 3 = the one-pass look-back
+ *                           kernel, at every launch size (2, round 3's map + placement form, was removed in round 5);
  *   DP_FORM_DELIM_LINE_MAX  auto: launches of up to this many bytes (the sum of the ranges) run line_kernel
  *                           (default 4 GiB);
- *   DP_FORM_DELIM_DENSE     auto, above that size: a density probe kernel counts the delimiters of 256 KiB
- *                           sampled evenly from the launch's own bytes and picks line_kernel at this many or
- *                           more delimiters per KiB x 1000 (default 20000: CSV-like), the one-pass kernel below.
+ *   DP_FORM_DELIM_DENSE     auto, above that size (out_mode 0-3): a density probe kernel counts the delimiters of
+ *                           256 KiB sampled evenly from the launch's own bytes and picks line_kernel at this many
+ *                           or more delimiters per KiB x 1000 (default 20000: CSV-like), the one-pass kernel below.
  * Every form writes the same output.  Not while a scan is in flight on the ctx. */
 #define DP_FORM_FASTA 0
 #define DP_FORM_DELIM 1
@@ -178,10 +191,10 @@ int dp_alloc_counts(uint64_t* device_allocs, uint64_t* host_allocs);
 #define DP_FORM_DELIM_DENSE 3
 int dp_ctx_set_form(dp_ctx* ctx, int what, uint64_t value);
 int dp_ctx_get_form(dp_ctx* ctx, int what, uint64_t* value);
-/* The kernels the ctx's next newline launch scanning `span` bytes takes: 1 = line_kernel, 2 = map + placement
- * kernels, 3 = the one-pass look-back kernel, 0 = decided on the device from the launch's bytes (auto above
- * DP_FORM_DELIM_LINE_MAX). */
-int dp_scan_delim_form(dp_ctx* ctx, uint64_t span, int* form);
+/* The kernels the ctx's next newline launch scanning `span` bytes into `out_mode` takes: 1 = line_kernel, 3 = the
+ * one-pass look-back kernel, 0 = decided on the device from the launch's bytes (auto above DP_FORM_DELIM_LINE_MAX;
+ * out_mode 4, the uint8 index, runs line_kernel at every size under auto). */
+int dp_scan_delim_form(dp_ctx* ctx, uint64_t span, int out_mode, int* form);
 /* The kernels the ctx's last collected newline launch ran (1, 2 or 3; 0 before any): the probe's pick read back
  * with the launch's results. */
 int dp_last_delim_form(dp_ctx* ctx, int* form);

@@ -58,14 +58,35 @@ def _header_text():
 
 
 def test_every_out_mode_is_documented():
-    """dp_delim_ranges_async's out_mode values the library accepts (0-3) are each described in the header."""
+    """dp_delim_ranges_async's out_mode values the library accepts (0-4) are each described in the header."""
     doc = _header_text()
     src = open(os.path.join(REPO, "dataplug_amd", "csrc", "dpscan.hip")).read()
-    assert "out_mode < 0 || out_mode > 3" in src                  # what the library accepts
-    for m in ("out_mode 0: uint32", "1: uint64", "2: uint32 low words", "out_mode 3: uint16 low words"):
+    assert "out_mode < 0 || out_mode > 4" in src                  # what the library accepts
+    for m in ("out_mode 0: uint32", "1: uint64", "2: uint32 low words", "out_mode 3: uint16 low words",
+              "out_mode 4: uint8 low bytes"):
         assert m in doc, m
-    assert "(2 * cap + 15) & ~15" in doc and "((2 * cap + 15) & ~15ull)" in src
+    assert "(2 * cap + 15) & ~15" in doc and "(cap + 15) & ~15" in doc
+    assert "(item * cap + 15) & ~15ull" in src and "(tab_off + 8 * ntab + 15) & ~15ull" in src
     assert "congruent mod 16" in doc
+
+
+@pytest.mark.parametrize("first,last,cap", [(0, 1 << 20, 1000), (70_000, 200_001, 17), (65_536, 65_537, 1),
+                                            (5, 5, 0), ((1 << 32) + 3, (1 << 32) + (9 << 16), 12_345)])
+def test_out_mode4_layout_matches_header(first, last, cap):
+    """The block-table and 256-byte-table offsets and sizes the header documents equal what ScanContext allocates and
+    reads for out_mode 4."""
+    import numpy as np
+    from dataplug_amd.scan.device import ScanContext
+    ranges = np.array([first, (first + last) // 2, (first + last) // 2, last], np.uint64)
+    j0 = first >> 16
+    J = ((last - 1) >> 16) - j0 + 1 if last > first else 1
+    s0 = first >> 8
+    S = ((last - 1) >> 8) - s0 + 1 if last > first else 1
+    tab_off = (cap + 15) & ~15
+    sub_off = (tab_off + 8 * J + 15) & ~15
+    assert ScanContext.block_table_size(ranges) == (j0, J) and ScanContext.sub_table_size(ranges) == (s0, S)
+    assert ScanContext._tab_off(cap, 4) == tab_off and ScanContext._sub_off(cap, ranges) == sub_off
+    assert ScanContext.out_bytes(cap, 4, ranges) >= sub_off + 2 * S
 
 
 @pytest.mark.parametrize("first,last,cap", [(0, 1 << 20, 1000), (70_000, 200_001, 17), (65_536, 65_537, 1),

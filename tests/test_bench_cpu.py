@@ -52,3 +52,31 @@ def test_verify_blocked(begin, end):
         t2 = tab.copy()
         t2[j] += np.uint64(1)
         assert not bench._verify_blocked(obj, begin, end, got, t2, n), j
+
+
+def _byte_index(obj, begin, end):
+    from test_partition_golden import byte_offsets
+    exp = np.concatenate(list(obj.delims_range(begin, end)))
+    bo = byte_offsets(exp, begin, end)
+    return bo.low, bo.sub, bo.table
+
+
+@pytest.mark.parametrize("begin,end", [(0, 3 << 20), (777, (3 << 20) - 5), (65536, 65536 * 40 + 1), (100, 9000),
+                                       (256 * 7, 256 * 700)])
+def test_verify_bytes(begin, end):
+    obj = synth.tiled_csv(3 << 20, seed=5, block=(100 << 10) - 7)
+    got, sub, tab = _byte_index(obj, begin, end)
+    n = len(got)
+    assert bench._verify_bytes(obj, begin, end, got, sub, tab, n)
+    assert not bench._verify_bytes(obj, begin, end, got[:-1], sub, tab, n - 1)      # one entry short
+    g2 = got.copy()
+    g2[n // 2] ^= 1
+    assert not bench._verify_bytes(obj, begin, end, g2, sub, tab, n)               # a wrong low byte
+    for j in range(0, len(sub), max(1, len(sub) // 50)):                          # wrong 256-byte entries
+        s2 = sub.copy()
+        s2[j] += np.uint16(1)
+        assert not bench._verify_bytes(obj, begin, end, got, s2, tab, n), j
+    for j in range(len(tab)):                                                      # any wrong table entry
+        t2 = tab.copy()
+        t2[j] += np.uint64(1)
+        assert not bench._verify_bytes(obj, begin, end, got, sub, t2, n), j

@@ -141,7 +141,7 @@ def test_line_parts_cover_in_order():
     assert page_ranges(4 * G, 8 * G) == [(4 * G, 8 * G)]
 
 
-@pytest.mark.parametrize("fmt", ["u16b", "u32p"])
+@pytest.mark.parametrize("fmt", ["u8s", "u16b", "u32p"])
 def test_line_index_parts_merge(monkeypatch, fmt):
     """line_index_object's merge of per-part GPU outputs (parts at unaligned cuts, one per 'device'),
     with each part's scan replaced by what the kernel returns for it (host logic only): the merged index
@@ -155,6 +155,10 @@ def test_line_index_parts_merge(monkeypatch, fmt):
 
     def fake_group(dev, co, lo, hi, delim, every_k, emit_add, fmt="u64"):
         sel = off[(off >= lo) & (off < hi)]
+        if fmt == "u8s":
+            from test_partition_golden import byte_offsets
+            bo = byte_offsets(sel, lo, hi)
+            return bo.low, bo.table, bo.sub
         if fmt == "u32p":
             rg = objects.page_ranges(lo, hi)
             counts = np.cumsum([int(((sel >= a) & (sel < b)).sum()) for a, b in rg])

@@ -46,9 +46,10 @@ def _index(co):
 
 
 def _lines_u64(co):
-    """The stored newline index (uint16 low words + 64 KiB block table) as uint64 offsets."""
+    """The stored newline index (the default u8s: uint8 low bytes + 256-byte counts + 64 KiB block table) as uint64
+    offsets."""
     from dataplug_amd.formats._lines import LineIndex
-    assert co.attributes.line_index_dtype == "u16b"
+    assert co.attributes.line_index_dtype == "u8s"
     li = LineIndex.of(co)
     return li._fetch(0, li.count)
 

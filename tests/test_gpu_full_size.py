@@ -116,10 +116,13 @@ def _check_delims(ctx, obj, lo, hi, d_ptr, stage):
     return nd
 
 
-def test_csv_32gib_configs2_every_offset(ctx):
-    """BASELINE configs[2]: the newline index of a 32 GiB cities.csv-shaped object in one launch, in the
-    stored form (uint16 low words + 64 KiB block table, out_mode 3); every one of its ~963 M offsets, rebuilt
-    from the two, compared with the object's analytic newline positions."""
+@pytest.mark.parametrize("out_mode", [4, 3])
+def test_csv_32gib_configs2_every_offset(ctx, out_mode):
+    """BASELINE configs[2]: the newline index of a 32 GiB cities.csv-shaped object in one launch, in a stored
+    form (out_mode 4, the default u8s: uint8 low bytes + 256-byte counts + 64 KiB block table; out_mode 3, u16b:
+    uint16 low words + the block table); every one of its ~963 M offsets, rebuilt from them, compared with the
+    object's analytic newline positions."""
+    from dataplug_amd.scan.objects import sub_counts
     size = 32 * GiB
     obj = synth.tiled_csv(size, seed=9)
     d = ctx.workspace("full_in", size + 64)
@@ -128,13 +131,25 @@ def test_csv_32gib_configs2_every_offset(ctx):
         ctx.h2d(d.ptr + p, obj.bytes_range(p, min(size, p + 4 * GiB), out=stage))
     del stage
     n_exp = obj.count_range(0, size)
-    low, nd, ends, tab = ctx.delim_ranges(d.ptr, size, 0, [(0, size)], out_mode=3, cap=n_exp + 64)
+    r = ctx.delim_ranges(d.ptr, size, 0, [(0, size)], out_mode=out_mode, cap=n_exp + 64)
+    low, nd, tab = r[0], r[1], r[3]
     assert nd == len(low) == n_exp > 900_000_000
+    if out_mode == 4:
+        c = sub_counts(r[4], tab, 0, 0)              # entries before every 256-byte boundary
+        assert c[0] == 0 and (np.diff(c) >= 0).all() and c[-1] <= n_exp
+        unit = np.repeat(np.arange(len(c), dtype=np.uint32), np.diff(np.append(c, np.uint64(n_exp))).astype(np.int64))
+        shift = np.uint64(8)
+    else:
+        unit = None
+        shift = np.uint64(16)
     i = 0
     for piece in obj.delims_range(0, size):
-        idx = np.arange(i, i + len(piece), dtype=np.int64)
-        blk = np.searchsorted(tab.astype(np.int64), idx, side="right").astype(np.uint64) - np.uint64(1)
-        assert np.array_equal((blk << np.uint64(16)) | low[i:i + len(piece)].astype(np.uint64), piece), i
+        if unit is not None:
+            u = unit[i:i + len(piece)].astype(np.uint64)
+        else:
+            idx = np.arange(i, i + len(piece), dtype=np.int64)
+            u = np.searchsorted(tab.astype(np.int64), idx, side="right").astype(np.uint64) - np.uint64(1)
+        assert np.array_equal((u << shift) | low[i:i + len(piece)].astype(np.uint64), piece), i
         i += len(piece)
     assert i == nd
 

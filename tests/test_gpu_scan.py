@@ -402,12 +402,25 @@ def test_delim_low_words_across_4gib_boundary(ctx):
     assert np.array_equal((page << np.uint64(32)) | low.astype(np.uint64), exp)
 
 
+def _rebuild(r, mode, first):
+    """uint64 offsets from an out_mode 3 (uint16 + 64 KiB table) or 4 (uint8 + 256-byte + 64 KiB tables) result."""
+    from dataplug_amd.scan.objects import ByteOffsets
+    if mode == 3:
+        low, _, _, tab = r
+        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right").astype(np.uint64) - np.uint64(1)
+        return ((blk + np.uint64(first >> 16)) << np.uint64(16)) | low.astype(np.uint64)
+    low, _, _, tab, sub = r
+    return ByteOffsets(low, sub, tab, first >> 8, first >> 16).to_u64()
+
+
+@pytest.mark.parametrize("mode", [3, 4])
 @pytest.mark.parametrize("base", [0, 1337, (1 << 32) - (5 << 20) - 3])
-def test_delim_u16_blocks(ctx, base):
-    """out_mode 3 (the stored CSV/VCF index): uint16 low words plus the entries before every 64 KiB
-    boundary; the library splits each range at its first boundary so every later one starts a wave range.
-    Rebuilt offsets equal the oracle's, for unaligned starts, several contiguous ranges, offsets past 2^32,
-    dense blocks (every byte a newline) and empty blocks (none)."""
+def test_delim_u16_blocks(ctx, base, mode):
+    """out_mode 3 (uint16 low words plus the entries before every 64 KiB boundary) and out_mode 4 (uint8 low bytes,
+    the low 16 bits of the entries before every 256-byte boundary, the 64 KiB table): the library splits each range
+    at its first 64 KiB boundary so every later one starts a wave range.  Rebuilt offsets equal the oracle's, for
+    unaligned starts, several contiguous ranges, offsets past 2^32, dense blocks (every byte a newline: the
+    one-pass kernel's rescan) and empty blocks (none); the tables equal the counts the oracle's offsets give."""
     a = synth.csv((9 << 20) + 17, seed=15)
     a[(2 << 20):(2 << 20) + 70_000] = 10                     # dense: > kDenseMax events per wave range
     a[(5 << 20):(5 << 20) + 300_000] = ord("x")               # several blocks without a newline
@@ -416,20 +429,25 @@ def test_delim_u16_blocks(ctx, base):
     ctx.h2d(dp, a)
     n = len(a)
     with pytest.raises(Exception):
-        ctx.delim_ranges(d.ptr + ((base + 1) & 15), n, base, [(base, base + n)], out_mode=3)
-    for ranges in ([(base, base + n)], [(base, base + 4097), (base + 4097, base + (3 << 20) + 5),
-                                       (base + (3 << 20) + 5, base + n)], [(base, base + 65540),
-                                       (base + 65540, base + n)]):
-        low, nd, ends, tab = ctx.delim_ranges(dp, n, base, ranges, out_mode=3)
-        exp = dpref.delim(a, 0, n)[0] + np.uint64(base)
-        assert nd == len(exp) and len(low) == len(exp)
-        j0 = base >> 16
-        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right").astype(np.uint64) - np.uint64(1)
-        got = ((blk + np.uint64(j0)) << np.uint64(16)) | low.astype(np.uint64)
-        assert np.array_equal(got, exp)
-        bounds = np.arange(j0, ((base + n - 1) >> 16) + 1, dtype=np.uint64) << np.uint64(16)
-        assert np.array_equal(tab[1:], np.searchsorted(exp, bounds[1:]).astype(np.uint64))
-        assert ends[-1] == nd
+        ctx.delim_ranges(d.ptr + ((base + 1) & 15), n, base, [(base, base + n)], out_mode=mode)
+    exp = dpref.delim(a, 0, n)[0] + np.uint64(base)
+    for form in (dict(delim=1), dict(delim=3)):                 # line_kernel, the one-pass kernel
+        ctx.set_form(**form)
+        for ranges in ([(base, base + n)], [(base, base + 4097), (base + 4097, base + (3 << 20) + 5),
+                                           (base + (3 << 20) + 5, base + n)], [(base, base + 65540),
+                                           (base + 65540, base + n)]):
+            r = ctx.delim_ranges(dp, n, base, ranges, out_mode=mode)
+            low, nd, ends, tab = r[:4]
+            assert nd == len(exp) and len(low) == len(exp) and ends[-1] == nd
+            assert np.array_equal(_rebuild(r, mode, base), exp), (form, ranges)
+            j0 = base >> 16
+            bounds = np.arange(j0, ((base + n - 1) >> 16) + 1, dtype=np.uint64) << np.uint64(16)
+            assert np.array_equal(tab[1:], np.searchsorted(exp, bounds[1:]).astype(np.uint64))
+            if mode == 4:
+                s0 = base >> 8
+                sb = np.arange(s0, ((base + n - 1) >> 8) + 1, dtype=np.uint64) << np.uint64(8)
+                assert np.array_equal(r[4][1:], (np.searchsorted(exp, sb[1:]) & 0xFFFF).astype(np.uint16))
+    ctx.set_form(delim=0)
 
 
 
@@ -534,26 +552,23 @@ def test_newline_forms_equal(size):
         for k, add, carry in ((1, 0, 0), (4, 1, 2), (3, 0, 7)):
             sel = np.arange(len(full), dtype=np.uint64) + np.uint64(carry)
             exp = full[(sel % np.uint64(k)) == np.uint64(k - 1)] + np.uint64(add)
-            for mode in (1, 0, 3):
+            for mode in (1, 0, 3, 4):
                 outs = []
                 for c, dp, want in ((one, d1.ptr + 3, 3), (line, d2.ptr + 3, 1), (auto_l, d3.ptr + 3, 1),
                                     (auto_o, d4.ptr + 3, 3)):
-                    if mode == 3 and (k != 1 or add != 0):
-                        # the block table counts delimiters: an entry index only when every delimiter is one
-                        with pytest.raises(DPScanError, match="out_mode 3 needs every_k == 1"):
+                    if mode >= 3 and (k != 1 or add != 0):
+                        # the block tables count delimiters: an entry index only when every delimiter is one
+                        with pytest.raises(DPScanError, match=f"out_mode {mode} needs every_k == 1"):
                             c.delim_ranges(dp, n, base, [(base, base + n)], every_k=k, emit_add=add, carry=carry,
                                            out_mode=mode)
                         continue
                     r = c.delim_ranges(dp, n, base, [(base, base + n)], every_k=k, emit_add=add, carry=carry,
                                        out_mode=mode)
-                    assert c.last_delim_form() == want
+                    # auto takes line_kernel for the uint8 index at every size
+                    assert c.last_delim_form() == (1 if mode == 4 and c is auto_o else want)
                     outs.append(r)
-                    if mode == 3:
-                        low, _, _, tab = r
-                        j0 = base >> 16
-                        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right")
-                        got = ((blk.astype(np.uint64) - np.uint64(1) + np.uint64(j0)) << np.uint64(16)) | low.astype(np.uint64)
-                        assert np.array_equal(got, exp)
+                    if mode >= 3:
+                        assert np.array_equal(_rebuild(r, mode, base), exp), (k, add, carry, mode)
                     else:
                         assert np.array_equal(r[0].astype(np.uint64), exp), (k, add, carry, mode)
                 if not outs:
@@ -561,8 +576,8 @@ def test_newline_forms_equal(size):
                 for o in outs[1:]:
                     assert np.array_equal(outs[0][0], o[0]) and outs[0][1] == o[1]
                     assert np.array_equal(np.asarray(outs[0][2]), np.asarray(o[2]))
-                    if mode == 3:                                 # the forms' block tables too
-                        assert np.array_equal(outs[0][3], o[3])
+                    if mode >= 3:                                 # the forms' block tables too
+                        assert all(np.array_equal(x, y) for x, y in zip(outs[0][3:], o[3:]))
     finally:
         for c in (one, line, auto_l, auto_o):
             c.close()
@@ -589,17 +604,11 @@ def test_forms_alternate_on_one_context():
         fexp = dpref.fasta_pairs(f, plan)
         for it in range(6):
             for j, (lo, hi) in enumerate(((0, 700_000), (0, n), (1000, 900_000), (5, n - 7))):
-                for mode in (1, 3):
+                for mode in (1, 3, 4):
                     c.set_form(**forms[(it + j + mode) % len(forms)])
                     r = c.delim_ranges(d.ptr, n, 0, [(lo, hi)], out_mode=mode)
                     exp = full[(full >= lo) & (full < hi)]
-                    if mode == 3:
-                        low, _, _, tab = r
-                        blk = np.searchsorted(tab.astype(np.int64), np.arange(len(low)), side="right")
-                        got = ((blk.astype(np.uint64) - np.uint64(1) + np.uint64(lo >> 16)) << np.uint64(16)) | \
-                            low.astype(np.uint64)
-                    else:
-                        got = r[0]
+                    got = _rebuild(r, mode, lo) if mode >= 3 else r[0]
                     assert np.array_equal(got, exp), (it, lo, hi, mode)
             if it % 2:
                 c.set_form(fasta=(it // 2) % 2)
@@ -622,6 +631,7 @@ def test_form_follows_delimiter_density():
         dens = {k: len(dpref.delim(a, 0, len(a))[0]) * 1024 / len(a) for k, a in objs.items()}
         assert dens["csv"] >= 20 > dens["vcf"], dens
         assert c.delim_form(4 << 20) == 0 and c.delim_form(1 << 20) == 1 and c.last_delim_form() == 0
+        assert c.delim_form(4 << 20, out_mode=4) == 1     # the uint8 index: line_kernel at every size
         for name, lim, want in (("vcf", None, 3), ("csv", None, 1), ("csv", None, 1), ("vcf", None, 3),
                                 ("vcf", 1 << 20, 1), ("csv", 1 << 20, 1), ("vcf", None, 3)):
             a = objs[name]
@@ -631,5 +641,7 @@ def test_form_follows_delimiter_density():
             r = c.delim_ranges(d.ptr, len(a), 0, [(0, n)], out_mode=1)
             assert np.array_equal(r[0], dpref.delim(a, 0, n)[0]), (name, n)
             assert c.last_delim_form() == want, (name, n, c.last_delim_form())
+            r4 = c.delim_ranges(d.ptr, len(a), 0, [(0, n)], out_mode=4)
+            assert c.last_delim_form() == 1 and r4[1] == len(r[0]), (name, n)
     finally:
         c.close()

@@ -15,8 +15,8 @@ from dataplug_amd import isa_guard
 from dataplug_amd.scan import _lib
 
 SHIPPED = ["scan_kernel<0,0>", "scan_kernel<0,1>", "scan_kernel<1,0>", "scan_kernel<1,1>", "scan_kernel<1,2>",
-           "map_kernel", "fasta_place_kernel<0>", "fasta_place_kernel<1>", "line_kernel<0>",
-           "line_kernel<1>", "line_kernel<2>", "density_probe_kernel", "fasta_resolve_kernel",
+           "scan_kernel<1,3>", "map_kernel", "fasta_place_kernel<0>", "fasta_place_kernel<1>", "line_kernel<0>",
+           "line_kernel<1>", "line_kernel<2>", "line_kernel<3>", "density_probe_kernel", "fasta_resolve_kernel",
            "find_kernel", "stream_kernel", "stream_rw_kernel"]
 
 

@@ -18,7 +18,7 @@ from dataplug_amd import synth
 from dataplug_amd.cloudobject import CloudObject
 from dataplug_amd.entities import get_slices
 from dataplug_amd.formats._lines import SliceError, store_line_index
-from dataplug_amd.scan.objects import BlockedOffsets, PagedOffsets
+from dataplug_amd.scan.objects import BlockedOffsets, ByteOffsets, PagedOffsets
 from dataplug_amd.preprocessing.handler import upload_metadata
 from dataplug_amd.preprocessing.metadata import PreprocessingMetadata
 from dataplug_amd.storage import MemoryStore
@@ -40,7 +40,25 @@ def _as_format(off: np.ndarray, fmt):
         j1 = int(off[-1]) >> 16 if len(off) else 0
         tab = np.searchsorted(off, np.arange(j0, j1 + 1, dtype=np.uint64) << np.uint64(16)).astype(np.uint64)
         return BlockedOffsets((off & np.uint64(0xFFFF)).astype(np.uint16), tab, j0)
+    if fmt == "u8s":
+        return byte_offsets(off, int(off[0]) if len(off) else 0, int(off[-1]) + 1 if len(off) else 1)
     return off
+
+
+def byte_offsets(off: np.ndarray, first: int, last: int) -> ByteOffsets:
+    """The uint8 index (out_mode 4) of sorted offsets in [first, last), as the GPU writes it: low bytes, the low 16
+    bits of the entries before every 256-byte boundary, the entries before every 64 KiB boundary (boundaries at or
+    below ``first`` read as 0)."""
+    s0, s1 = first >> 8, (last - 1) >> 8
+    j0, j1 = first >> 16, (last - 1) >> 16
+    sb = np.arange(s0, s1 + 1, dtype=np.uint64) << np.uint64(8)
+    sub = (np.searchsorted(off, sb) & 0xFFFF).astype(np.uint16)
+    if first & 0xFF:
+        sub[0] = 0
+    tab = np.searchsorted(off, np.arange(j0, j1 + 1, dtype=np.uint64) << np.uint64(16)).astype(np.uint64)
+    if first & 0xFFFF:
+        tab[0] = 0
+    return ByteOffsets((off & np.uint64(0xFF)).astype(np.uint8), sub, tab, s0, j0)
 
 
 def _co(fmt, name: str, data: bytes, attrs: dict, meta: bytes = None, nl=True, begin=0, paged="u16b"):
@@ -94,7 +112,7 @@ def _vcf_objects():
         yield rec, data
 
 
-@pytest.mark.parametrize("paged", ["u16b", "u32p", "u64"])
+@pytest.mark.parametrize("paged", ["u8s", "u16b", "u32p", "u64"])
 def test_csv_partitions_match_reference(paged):
     from dataplug_amd.formats.generic import csv as fcsv
     checked = 0
@@ -118,7 +136,7 @@ def test_csv_partitions_match_reference(paged):
     assert checked > 100
 
 
-@pytest.mark.parametrize("paged", ["u16b", "u32p", "u64"])
+@pytest.mark.parametrize("paged", ["u8s", "u16b", "u32p", "u64"])
 def test_vcf_partitions_match_reference(paged):
     from dataplug_amd.formats.genomics import vcf as fvcf
     for rec, data in _vcf_objects():
@@ -242,6 +260,43 @@ def test_blocked_line_index_sparse_and_dense_blocks(monkeypatch, preload):
                           count=attrs["num_lines"], blocks=blocks, block0=attrs["line_index_block0"])
     assert np.array_equal(li._fetch(0, li.count), off)
     for x in [0, 5 * G, 5 * G + 123, 5 * G + 65536, 6 * G, int(off[9999]), int(off[-1]), int(off[-1]) + 1, 8 * G]:
+        i = int(np.searchsorted(off, np.uint64(x)))
+        assert li.nxt(x) == (int(off[i]) + 1 if i < len(off) else None), x
+        assert li.contains(x) == (i < len(off) and int(off[i]) == x)
+
+
+@pytest.mark.parametrize("preload", [True, False])
+@pytest.mark.parametrize("first_delta", [0, 123, 256])
+def test_byte_line_index_sparse_and_dense(monkeypatch, preload, first_delta):
+    """uint8 low bytes + 256-byte counts + 64 KiB block table (out_mode 4), read back by LineIndex (preloaded, or block
+    by block with the 256-byte counts of the blocks they span): 64 KiB blocks of nearly every byte a newline (their
+    256-byte counts wrap 16 bits within the index), empty blocks, offsets past 2^32, first bytes on and off 256-byte
+    and 64 KiB boundaries."""
+    from dataplug_amd.formats import _lines
+    if not preload:
+        monkeypatch.setattr(_lines, "_PRELOAD_BYTES", 1024)
+    rng = np.random.default_rng(5)
+    G = 1 << 30
+    first = 5 * G + first_delta
+    full = np.arange(first + 70_000, first + 70_000 + 65_535 * 3, dtype=np.uint64)        # every byte: dense blocks
+    sparse = rng.integers(first + 400_000, 7 * G, 3_000).astype(np.uint64)
+    mid = rng.integers(first, first + 70_000, 500).astype(np.uint64)
+    off = np.unique(np.concatenate([np.asarray([first], np.uint64), mid, full, sparse]))
+    last = int(off[-1]) + 1 + 1000
+    bo = byte_offsets(off, first, last)
+    assert np.array_equal(bo.to_u64(), off)
+    co = _co(_lines_fmt(), "bytes", b"x" * 16, {}, nl=False)
+    attrs = store_line_index(co, bo)
+    assert attrs["line_index_dtype"] == "u8s"
+    blocks = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=attrs["line_index_blocks_key"])
+                           ["Body"].read(), "<u8")
+    li = _lines.LineIndex(storage=co.storage, bucket=co.meta_path.bucket, key=attrs["line_index_key"],
+                          count=attrs["num_lines"], blocks=blocks, block0=attrs["line_index_block0"],
+                          sub_key=attrs["line_index_sub_key"], sub0=attrs["line_index_sub0"])
+    assert np.array_equal(li._fetch(0, li.count), off)
+    assert np.array_equal(li._fetch(1000, 70_000), off[1000:70_000])
+    for x in [0, first, first + 1, first + 70_000, first + 70_000 + 65_535, 6 * G, int(off[9999]), int(off[-1]),
+              int(off[-1]) + 1, 8 * G]:
         i = int(np.searchsorted(off, np.uint64(x)))
         assert li.nxt(x) == (int(off[i]) + 1 if i < len(off) else None), x
         assert li.contains(x) == (i < len(off) and int(off[i]) == x)

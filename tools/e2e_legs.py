@@ -131,10 +131,10 @@ def _stages(co, kind: str, size: int, chunk_size: int):
     else:
         rg = np.asarray([0, size], np.uint64)
         cap = size // 16 + 1024
-        out = ctx.workspace("e2e_out", ctx.out_bytes(cap, 3, rg))
+        out = ctx.workspace("e2e_out", ctx.out_bytes(cap, 4, rg))
 
-        def scan():
-            ctx.delim_ranges_async(d.ptr, size, 0, rg, 10, 1, 0, 0, out.ptr, 3, cap)
+        def scan():                                  # the stored form, u8s (out_mode 4)
+            ctx.delim_ranges_async(d.ptr, size, 0, rg, 10, 1, 0, 0, out.ptr, 4, cap)
             return ctx.delim_ranges_result(1)[0]
         n = scan()
         ctx.timing(True)
@@ -143,7 +143,7 @@ def _stages(co, kind: str, size: int, chunk_size: int):
             scan()
         ms, nl = ctx.timing_read()
         ctx.timing(False)
-        idx_bytes = 2 * n
+        idx_bytes = n + 2 * ctx.sub_table_size(rg)[1] + 8 * ctx.block_table_size(rg)[1]
         host = np.empty(idx_bytes, np.uint8)
     t_d2h = _timed(lambda: ctx.d2h(host, out.ptr), 2)
     mb = co.meta_path.bucket
@@ -166,17 +166,24 @@ def _verify_fasta(co, host: np.ndarray, chunk_size: int) -> bool:
     return bool(np.array_equal(got, exp))
 
 
-def _verify_csv(co, obj, size: int, verify_blocked) -> bool:
+def _verify_csv(co, obj, size: int, verify_blocked, verify_bytes) -> bool:
+    """The stored newline index (u8s: low bytes + 256-byte counts + block table, or u16b: low words + block table)
+    against the object's analytic newline positions."""
     st, mb = co.storage, co.meta_path.bucket
-    key = co.get_attribute("line_index_key")
-    low = np.frombuffer(st.get_object(Bucket=mb, Key=key)["Body"].read(), "<u2")
-    tab = np.frombuffer(st.get_object(Bucket=mb, Key=co.get_attribute("line_index_blocks_key"))["Body"].read(), "<u8")
+
+    def get(attr, dt):
+        return np.frombuffer(st.get_object(Bucket=mb, Key=co.get_attribute(attr))["Body"].read(), dt)
     n = int(co.get_attribute("num_lines"))
-    return bool(n == obj.count_range(0, size) and verify_blocked(obj, 0, size, low, tab, n))
+    tab = get("line_index_blocks_key", "<u8")
+    if co.get_attribute("line_index_dtype") == "u8s":
+        ok = verify_bytes(obj, 0, size, get("line_index_key", "u1"), get("line_index_sub_key", "<u2"), tab, n)
+    else:
+        ok = verify_blocked(obj, 0, size, get("line_index_key", "<u2"), tab, n)
+    return bool(n == obj.count_range(0, size) and ok)
 
 
 def e2e_leg(fasta_size: int = 4 << 30, csv_size: int = 4 << 30, reps: int = 2, port: int = 19071,
-            verify_blocked=None, verify: bool = True, log=print) -> dict:
+            verify_blocked=None, verify_bytes=None, verify: bool = True, log=print) -> dict:
     """The ``e2e`` sub-object (see the module doc)."""
     from dataplug_amd import synth
     from dataplug_amd.cloudobject import CloudObject
@@ -213,7 +220,7 @@ def e2e_leg(fasta_size: int = 4 << 30, csv_size: int = 4 << 30, reps: int = 2, p
                 res["config"] = f"BASELINE configs[1]: {size / GiB:g} GiB FASTA, chunk_size={cs} (size/4), uint32 index"
             else:
                 res["config"] = (f"configs[2]-shaped CSV (cities.csv rows) of {size / GiB:g} GiB, newline index stored as "
-                                 f"uint16 low words + 64 KiB block table")
+                                 f"uint8 low bytes + 256-byte counts + 64 KiB block table (u8s)")
             for src in ("memory", "loopback_http"):
                 if src == "loopback_http" and not ready:
                     srv.wait_ready()                        # (it generated its copies while this process did)
@@ -226,7 +233,7 @@ def e2e_leg(fasta_size: int = 4 << 30, csv_size: int = 4 << 30, reps: int = 2, p
                 t = _timed(call, reps)
                 ok = None
                 if verify:
-                    ok = _verify_fasta(co, host, cs) if kind == "fasta" else _verify_csv(co, obj, size, verify_blocked)
+                    ok = _verify_fasta(co, host, cs) if kind == "fasta" else _verify_csv(co, obj, size, verify_blocked, verify_bytes)
                 res[src] = {"preprocess_s": round(t, 4), "value": round(size / t / GiB, 2), "verified": ok}
                 log(f"e2e {kind} {src}: {res[src]}")
             co = CloudObject.from_s3(fmt, f"s3://{bucket}/{key}", s3_config={"endpoint_url": "memory://bench_e2e"})

@@ -9,6 +9,10 @@ Per size: mean / median / min / max of every form, its roofline fraction on algo
 byte for byte.
 
     python tools/form_sweep.py [--content vcf,csv] [--sizes-gib 2,4,8,16,32,64] [--reps 10] [--forms line,one,default]
+
+A form may name its own out_mode (``--forms line:4,one:3,default:4``: 3 uint16 + blocks, 4 uint8 + 256-byte counts +
+blocks); forms of one out_mode are compared byte for byte, forms of different modes through the decoded offsets'
+count and a checksum of the first and last 1 Mi entries.
 """
 from __future__ import annotations
 
@@ -24,15 +28,25 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from dataplug_amd import synth  # noqa: E402
 from dataplug_amd.scan import ScanContext  # noqa: E402
+from dataplug_amd.scan.objects import BlockedOffsets, ByteOffsets  # noqa: E402
 
 FORM_IDS = {"line": 1, "one": 3, "default": 0}
 
 
 def make_ctx(form: str) -> ScanContext:
     ctx = ScanContext(0)
-    if form != "default":
-        ctx.set_form(delim=FORM_IDS[form])
+    kind = form.split(":")[0]
+    if kind != "default":
+        ctx.set_form(delim=FORM_IDS[kind])
     return ctx
+
+
+def form_mode(form: str, default: int) -> int:
+    return int(form.split(":")[1]) if ":" in form else default
+
+
+def alg_bytes(size, n, mode, ntab, nsub):
+    return size + (2 if mode == 3 else 1) * n + 8 * ntab + (2 * nsub if mode == 4 else 0)
 
 
 def stats(ts):
@@ -48,6 +62,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--forms", default="line,one,default")
     ap.add_argument("--no-stream", action="store_true")
+    ap.add_argument("--out-mode", type=int, default=3, choices=[3, 4], help="3: uint16 + blocks, 4: uint8 + 256 B + blocks")
     args = ap.parse_args()
     sizes = [int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")]
     top = max(sizes)
@@ -67,8 +82,9 @@ def main():
         print(json.dumps({"content": content, "gen_s": round(time.perf_counter() - t0, 2)}), flush=True)
         # every context's output buffer sized for the largest launch once, before any is timed
         top_cap = obj.count_range(0, top) + 1024
-        ob_top = ScanContext.out_bytes(top_cap, 3, np.asarray([0, top], np.uint64))
-        outs = {k: c.workspace("out", ob_top) for k, c in ctxs.items()}
+        modes = {k: form_mode(k, args.out_mode) for k in names}
+        outs = {k: c.workspace("out", ScanContext.out_bytes(top_cap, modes[k], np.asarray([0, top], np.uint64)))
+                for k, c in ctxs.items()}
         for size in sizes:
             n_exp = obj.count_range(0, size)
             cap = n_exp + 1024
@@ -79,10 +95,10 @@ def main():
 
             def run(k):
                 c = ctxs[k]
-                c.delim_ranges_async(d.ptr, top, 0, ranges, 10, 1, 0, 0, outs[k].ptr, 3, cap)
+                c.delim_ranges_async(d.ptr, top, 0, ranges, 10, 1, 0, 0, outs[k].ptr, modes[k], cap)
                 r = c.delim_ranges_result(1)
-                if k == "default":
-                    chosen.setdefault("default", []).append(c.last_delim_form())
+                if k.startswith("default"):
+                    chosen.setdefault(k, []).append(c.last_delim_form())
                 return r
 
             for k in names:                       # warm (code objects, workspace) and the first result
@@ -105,19 +121,31 @@ def main():
                 c.timing(False)
             res = {}
             for k, c in ctxs.items():
-                words = c.d2h(np.empty(n, np.uint16), outs[k].ptr)
-                res[k] = (n, words, c.block_table(outs[k].ptr, cap, ranges))
-            vals = list(res.values())
-            a = vals[0]
-            equal = bool(a[0] == n_exp and all(b[0] == a[0] and np.array_equal(a[1], b[1]) and
-                                               np.array_equal(a[2], b[2]) for b in vals[1:]))
-            alg = size + 2 * n_exp + 8 * len(a[2])
-            line = {"content": content, "size_gib": size / (1 << 30), "entries": n_exp, "equal": equal}
+                mode = modes[k]
+                words = c.d2h(np.empty(n, np.uint16 if mode == 3 else np.uint8), outs[k].ptr)
+                res[k] = (n, words, c.block_table(outs[k].ptr, cap, ranges, mode)) + \
+                    ((c.sub_table(outs[k].ptr, cap, ranges),) if mode == 4 else ())
+            equal = all(r[0] == n_exp for r in res.values())
+            for m in sorted(set(modes.values())):
+                same = [res[k] for k in names if modes[k] == m]
+                equal = equal and all(all(np.array_equal(x, y) for x, y in zip(same[0][1:], b[1:])) for b in same[1:])
+            if len(set(modes.values())) > 1:
+                ends = set()
+                for k in names:
+                    r = res[k]
+                    o = ByteOffsets(r[1], r[3], r[2], 0, 0) if len(r) > 3 else BlockedOffsets(r[1], r[2], 0)
+                    m = min(n, 1 << 20)
+                    ends.add((int(o.to_u64(0, m).sum()), int(o.to_u64(n - m, n).sum())))
+                equal = equal and len(ends) == 1
+            line = {"content": content, "size_gib": size / (1 << 30), "out_modes": modes, "entries": n_exp,
+                    "equal": bool(equal)}
             if st:
                 s = stats(st)
                 line["stream_us"] = s
                 line["stream_TBps_median"] = round(size / (s["median"] * 1e-6) / 1e12, 3)
             for k in names:
+                r = res[k]
+                alg = alg_bytes(size, n_exp, modes[k], len(r[2]), len(r[3]) if len(r) > 3 else 0)
                 s = stats(times[k])
                 line[f"{k}_us"] = s
                 line[f"{k}_frac_median"] = round(alg / (s["median"] * 1e-6) / 8e12, 4)
@@ -125,10 +153,10 @@ def main():
                 if st:
                     line[f"{k}_over_stream"] = round(s["median"] / stats(st)["median"], 4)
                 line[f"{k}_all_us"] = [round(t, 1) for t in times[k]]
-            if "default" in chosen:
-                line["default_forms"] = sorted(set(chosen["default"]))
+            for k, v in chosen.items():
+                line[f"{k}_forms"] = sorted(set(v))
             print(json.dumps(line), flush=True)
-            del res, vals, a
+            del res
             if not equal:
                 print("MISMATCH", flush=True)
                 sys.exit(1)
