@@ -3693,7 +3693,7 @@ int dp_timing_read(dp_ctx* c, double* total_ms, uint64_t* launches) {
 }
 
 int dp_debug_profile(dp_ctx* c, uint64_t* host_words, uint64_t n_words, int* slots, int* waves) {
-#ifdef DP_STAMPS
+#ifdef DP_DIAG
   if (!c || !host_words) return fail(DP_ERR_INVALID, "dp_debug_profile: null argument");
   const uint64_t n = n_words < kProfWords ? n_words : kProfWords;
   HIPCHK(hipSetDevice(c->device));

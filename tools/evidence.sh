@@ -10,8 +10,11 @@ if [ -z "$NO_SWEEPS" ]; then
   step size_sweep
   timeout -k 10 300 python -u tools/size_sweep.py --sizes-gib 0.0625,0.125,0.25,0.5,1,2,4,8 > $O/size_sweep.log 2>&1 || { tail -5 $O/size_sweep.log; exit 1; }
   tail -3 $O/size_sweep.log
-  step form_sweep
-  timeout -k 10 600 python -u tools/form_sweep.py --content vcf,csv --sizes-gib 2,4,8,16,32,64 --reps 10 > $O/form_sweep.log 2>&1 || { tail -5 $O/form_sweep.log; exit 1; }
+  if [ -z "$NO_FORM_SWEEP" ]; then
+    step form_sweep
+    timeout -k 10 900 python -u tools/form_sweep.py --content vcf,csv --sizes-gib 2,4,8,16,32,64 --reps 6 --forms line:4,default:4,one:3,line:3 > $O/form_sweep.log 2>&1 || { tail -5 $O/form_sweep.log; exit 1; }
+    python3 tools/sweep_table.py $O/form_sweep.log > $O/form_sweep_table.txt
+  fi
 fi
 for leg in $LEGS; do
   step prof_$leg

@@ -62,6 +62,9 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--forms", default="line,one,default")
     ap.add_argument("--no-stream", action="store_true")
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--begin", type=int, default=0, help="every launch scans [begin, size) of the resident object "
+                    "(e.g. 482: a VCF body behind its header, ranges off the 256-byte grid)")
     ap.add_argument("--out-mode", type=int, default=3, choices=[3, 4], help="3: uint16 + blocks, 4: uint8 + 256 B + blocks")
     args = ap.parse_args()
     sizes = [int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")]
@@ -72,7 +75,7 @@ def main():
     d = ctx0.workspace("in", top + 64)
     for content in args.content.split(","):
         t0 = time.perf_counter()
-        obj = (synth.tiled_csv if content == "csv" else synth.tiled_vcf)(top, seed=1)
+        obj = (synth.tiled_csv if content == "csv" else synth.tiled_vcf)(top, seed=args.seed)
         step = 2 << 30
         stage = np.empty(min(step, top), np.uint8)
         for p in range(0, top, step):
@@ -86,9 +89,10 @@ def main():
         outs = {k: c.workspace("out", ScanContext.out_bytes(top_cap, modes[k], np.asarray([0, top], np.uint64)))
                 for k, c in ctxs.items()}
         for size in sizes:
-            n_exp = obj.count_range(0, size)
+            b0 = args.begin
+            n_exp = obj.count_range(b0, size)
             cap = n_exp + 1024
-            ranges = np.asarray([0, size], np.uint64)
+            ranges = np.asarray([b0, size], np.uint64)
             times = {k: [] for k in names}
             chosen = {}
             st = []
@@ -133,11 +137,12 @@ def main():
                 ends = set()
                 for k in names:
                     r = res[k]
-                    o = ByteOffsets(r[1], r[3], r[2], 0, 0) if len(r) > 3 else BlockedOffsets(r[1], r[2], 0)
+                    o = ByteOffsets(r[1], r[3], r[2], b0 >> 8, b0 >> 16) if len(r) > 3 else BlockedOffsets(r[1], r[2], b0 >> 16)
                     m = min(n, 1 << 20)
                     ends.add((int(o.to_u64(0, m).sum()), int(o.to_u64(n - m, n).sum())))
                 equal = equal and len(ends) == 1
-            line = {"content": content, "size_gib": size / (1 << 30), "out_modes": modes, "entries": n_exp,
+            line = {"content": content, "size_gib": size / (1 << 30), "begin": b0, "seed": args.seed, "out_modes": modes,
+                    "entries": n_exp,
                     "equal": bool(equal)}
             if st:
                 s = stats(st)
@@ -145,7 +150,7 @@ def main():
                 line["stream_TBps_median"] = round(size / (s["median"] * 1e-6) / 1e12, 3)
             for k in names:
                 r = res[k]
-                alg = alg_bytes(size, n_exp, modes[k], len(r[2]), len(r[3]) if len(r) > 3 else 0)
+                alg = alg_bytes(size - b0, n_exp, modes[k], len(r[2]), len(r[3]) if len(r) > 3 else 0)
                 s = stats(times[k])
                 line[f"{k}_us"] = s
                 line[f"{k}_frac_median"] = round(alg / (s["median"] * 1e-6) / 8e12, 4)

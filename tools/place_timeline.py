@@ -40,6 +40,17 @@ def main():
     for _ in range(3):
         ctx.fasta_index_async(d.ptr, n, 0, n, chunks, out.ptr, False, n // 256)
         ctx.fasta_result(len(chunks) // 2)
+    ctx.stream_read(d.ptr, n)                   # the read-only calibration kernel over the same bytes
+    ctx.sync()
+    ctx.timing(True)
+    ctx.timing_read()
+    ctx.stream_read(d.ptr, n)
+    ctx.sync()
+    stream_ms, _ = ctx.timing_read()
+    ctx.fasta_index_async(d.ptr, n, 0, n, chunks, out.ptr, False, n // 256)   # the launch the stamps describe
+    ctx.fasta_result(len(chunks) // 2)
+    span_ms, _ = ctx.timing_read()
+    ctx.timing(False)
     words = 1024 * 16 * 8
     buf = np.zeros(words, np.uint64)
     sl, wv = ctypes.c_int(), ctypes.c_int()
@@ -56,7 +67,8 @@ def main():
     q = lambda a: [round(float(x), 1) for x in np.percentile(a, [0, 50, 100])]
     st = (mp[:, :, 0][live] - t0) / 100.0
     en = (mp[:, :, 1][live] - t0) / 100.0
-    res = {"map_last_wave_end": round(map_end, 1), "blocks": int(len(pl)),
+    res = {"span_us": round(span_ms * 1e3, 1), "stream_us": round(stream_ms * 1e3, 1),
+           "map_last_wave_end": round(map_end, 1), "blocks": int(len(pl)),
            "map_wave_start_q0_50_90_100": [round(float(x), 1) for x in np.percentile(st, [0, 50, 90, 100])],
            "map_wave_end_q0_10_50_100": [round(float(x), 1) for x in np.percentile(en, [0, 10, 50, 100])]}
     if len(pl) == 0 or (pl[:, 0] == 0).all():
