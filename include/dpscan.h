@@ -195,7 +195,7 @@ int dp_ctx_get_form(dp_ctx* ctx, int what, uint64_t* value);
  * one-pass look-back kernel, 0 = decided on the device from the launch's bytes (auto above DP_FORM_DELIM_LINE_MAX;
  * out_mode 4, the uint8 index, runs line_kernel at every size under auto). */
 int dp_scan_delim_form(dp_ctx* ctx, uint64_t span, int out_mode, int* form);
-/* The kernels the ctx's last collected newline launch ran (1, 2 or 3; 0 before any): the probe's pick read back
+/* The kernels the ctx's last collected newline launch ran (1 or 3; 0 before any): the probe's pick read back
  * with the launch's results. */
 int dp_last_delim_form(dp_ctx* ctx, int* form);
 
