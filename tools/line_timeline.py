@@ -34,25 +34,26 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--content", default="sparse", choices=["sparse", "csv", "vcf"])
     ap.add_argument("--gib", type=float, default=2.0)
+    ap.add_argument("--mode", type=int, default=4, choices=[3, 4], help="csv/vcf out_mode: 4 u8s (stored), 3 u16b")
     args = ap.parse_args()
     n = int(args.gib * (1 << 30))
     ctx = ScanContext(0)
     if args.content == "sparse":                              # the size sweep's '>' index, uint64 offsets
         host = synth.tiled_fasta_host(n, seed=1)
-    else:                                                     # the stored '\n' index (uint16 + blocks)
+    else:                                                     # the stored '\n' index (out_mode 4 or 3)
         host = (synth.tiled_csv if args.content == "csv" else synth.tiled_vcf)(n, seed=1).bytes_range(0, n)
     d = ctx.workspace("in", n + 64)
     ctx.h2d(d.ptr, host)
     del host
     cap = n // 16
     ranges = np.asarray([0, n], np.uint64)
-    out = ctx.workspace("out", max(n // 2, ScanContext.out_bytes(cap, 3, ranges)))
+    out = ctx.workspace("out", max(n // 2, ScanContext.out_bytes(cap, args.mode, ranges)))
     for _ in range(3):
         if args.content == "sparse":
             ctx.delim_index_async(d.ptr, n, 0, 0, n, 62, 1, 0, out.ptr, True, n // 256)
             ctx.delim_result()
         else:
-            ctx.delim_ranges_async(d.ptr, n, 0, ranges, 10, 1, 0, 0, out.ptr, 3, cap)
+            ctx.delim_ranges_async(d.ptr, n, 0, ranges, 10, 1, 0, 0, out.ptr, args.mode, cap)
             ctx.delim_ranges_result(1)
     words = BASE + 256 * STEPS * WAVES * 8
     buf = np.zeros(words, np.uint64)

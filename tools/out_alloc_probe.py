@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--reps", type=int, default=8)
     ap.add_argument("--mode", type=int, default=4)
     ap.add_argument("--fragment-gib", type=float, default=0, help="allocate and free this much in 1.5 GiB pieces first")
+    ap.add_argument("--contexts", type=int, default=1, help="spread the buffers over this many scan contexts (each "
+                    "with its own chunk table and look-back descriptors)")
     args = ap.parse_args()
     size = int(args.size_gib * (1 << 30))
     ctx = ScanContext(0)
@@ -47,25 +49,35 @@ def main():
     cap = n_exp + 1024
     rg = np.asarray([0, size], np.uint64)
     ob = ScanContext.out_bytes(cap, args.mode, rg)
-    outs = [ctx.workspace(f"out{k}", ob) for k in range(args.buffers)]
+    ctxs = [ctx] + [ScanContext(0) for _ in range(args.contexts - 1)]
+    cx = [ctxs[k % len(ctxs)] for k in range(args.buffers)]
+    outs = [c.workspace(f"out{k}", ob) for k, c in enumerate(cx)]
     times = [[] for _ in outs]
+    st = []
 
-    def run(o):
-        ctx.delim_ranges_async(d.ptr, size, 0, rg, 10, 1, 0, 0, o.ptr, args.mode, cap)
-        return ctx.delim_ranges_result(1)[0]
-    for o in outs:
-        assert run(o) == n_exp
-    ctx.timing(True)
-    ctx.timing_read()
+    def run(c, o):
+        c.delim_ranges_async(d.ptr, size, 0, rg, 10, 1, 0, 0, o.ptr, args.mode, cap)
+        return c.delim_ranges_result(1)[0]
+    for c, o in zip(cx, outs):
+        assert run(c, o) == n_exp
+    for c in ctxs:
+        c.timing(True)
+        c.timing_read()
     for rep in range(args.reps):
-        for k, o in enumerate(outs):
-            run(o)
-            ms, _ = ctx.timing_read()
+        ctx.stream_read(d.ptr, size)
+        ctx.sync()
+        ms, _ = ctx.timing_read()
+        st.append(round(ms * 1e3, 1))
+        for k, (c, o) in enumerate(zip(cx, outs)):
+            run(c, o)
+            ms, _ = c.timing_read()
             times[k].append(round(ms * 1e3, 1))
-    ctx.timing(False)
+    for c in ctxs:
+        c.timing(False)
     res = {"content": args.content, "size_gib": args.size_gib, "mode": args.mode, "fragment_gib": args.fragment_gib,
-           "buffers": [{"addr_mod_2m": o.ptr % (2 << 20), "addr_gib": round(o.ptr / (1 << 30), 3),
-                        "median_us": float(np.median(t)), "all_us": t} for o, t in zip(outs, times)]}
+           "stream_median_us": float(np.median(st)),
+           "buffers": [{"ctx": k % len(ctxs), "addr_mod_2m": o.ptr % (2 << 20), "addr_gib": round(o.ptr / (1 << 30), 3),
+                        "median_us": float(np.median(t)), "all_us": t} for k, (o, t) in enumerate(zip(outs, times))]}
     print(json.dumps(res), flush=True)
 
 
