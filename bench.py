@@ -15,16 +15,17 @@ Workloads (synthetic bytes of the named shapes, resident in HBM before any timed
     (``scan.objects.fasta_split``: byte-balanced groups, chunks cut where a boundary falls inside one, no
     collective; the reference runs chunks as independent map jobs, preprocess.py:39-51).
   * CSV (configs[2]): a 32 GiB cities.csv-shaped object per GPU (weak), the newline index as co.preprocess
-    stores it (uint16 low words + 64 KiB block table, dp_delim_ranges out_mode 3).
+    stores it (u8s: uint8 low bytes + 256-byte counts + 64 KiB block table, dp_delim_ranges out_mode 4).
   * VCF (configs[3]): ONE 64 GiB VCF whose body is cut into one byte part per GPU (strong: the 1/2/4/8-GPU
     curve of north_star), same index form.
 
 One step = on every GPU, one scan call over its bytes: FASTA = dp_fasta_index_async + dp_fasta_result (the
 chunk-table check, the two scan kernels -- map_kernel<FASTA> over 16 KiB ranges, then fasta_place_kernel --,
 the split-header resolve kernel, the read-back of count / pending / chunk ends); newline = dp_delim_ranges
-(one launch: the lockstep line_kernel up to 4 GiB, above it the kernel a density probe picks on the device from
-the launch's own bytes -- line_kernel for CSV-dense input, the one-pass look-back scan_kernel for sparser; the kernel
-that ran, dp_last_delim_form, is named in each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
+(one launch: the lockstep line_kernel for the stored u8s form at every size; for the other forms (--index-dtype) up
+to 4 GiB, above it the kernel a density probe picks on the device from the launch's own bytes -- line_kernel for
+CSV-dense input, the one-pass look-back scan_kernel for sparser; the kernel that ran, dp_last_delim_form, is named in
+each leg's roofline).  The index stays in HBM (the H2D/D2H-inclusive end-to-end
 rate is DESIGN.md §6).  Steps
 alternate between two contexts and step k + 1 is enqueued before step k's result is collected; the library
 runs one scan at a time per GPU (its scan stream), so ``value`` is this pipelined rate provided
@@ -752,8 +753,9 @@ def _verify_bytes(obj, begin, end, got, sub, tab, n_out):
 def delim_worker(args, team, leg, k, world, dev):
     """configs[2] (csv: a 32 GiB cities.csv-shaped object per GPU, weak scaling) and configs[3] (vcf: ONE
     64 GiB VCF whose body [body_offset, size) is cut into one raw byte range per GPU, strong scaling): the
-    newline index as co.preprocess builds it (uint16 low words + 64 KiB block table, dp_delim_ranges out_mode
-    3; --index-dtype u32p / u64: the other forms) -- device-resident, timed like the FASTA leg."""
+    newline index as co.preprocess builds it (u8s: uint8 low bytes + 256-byte counts + 64 KiB block table,
+    dp_delim_ranges out_mode 4; --index-dtype u16b / u32p / u64: the other forms) -- device-resident, timed like the
+    FASTA leg."""
     from dataplug_amd import synth
     from dataplug_amd.dist import rank_byte_range
     from dataplug_amd.scan import ScanContext

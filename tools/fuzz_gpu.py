@@ -3,14 +3,16 @@ oracle (oracle/dpref.c) on random inputs, chunk plans, device misalignments and 
 
     python tools/fuzz_gpu.py [--seconds 240] [--seed 1] [--mode kernel|object] [--out gpurun_out/fuzz.json]
 
-``--mode object`` runs co.preprocess() end to end instead (see object_mode).
+``--mode object`` runs co.preprocess() end to end instead (see object_mode); ``--mode lines`` the CSV newline index
+through co.preprocess() in its stored forms (see lines_mode).
 
 FASTA: token soups and structured records (header lines 1 B - 300 KB, so headers span wave ranges, units and
 chunks; '\\r'; '>' inside sequence lines; runs of '>' or '\\n'), object sizes log-uniform in [1 B, 48 MiB],
 chunk plans of the reference (preprocess.py:38 floor plan with the tail dropped, including the
 chunk_size == num_chunks - 1 quirk of handler.py:37 that sends every chunk to EOF), uint32 or uint64 output.
 Every pair and every per-chunk count must equal the oracle's.  DELIM: random delimiter byte, [begin, end),
-every_k 1-5, emit_add 0/1, uint64 or uint32 output.  Exits non-zero on the first mismatch and keeps the case
+every_k 1-5, emit_add 0/1, uint64 or uint32 output; when every delimiter is an entry, sometimes the stored forms
+(out_mode 4 u8s, 3 u16b) at a random object base, decoded.  Exits non-zero on the first mismatch and keeps the case
 in gpurun_out/fuzz_fail.npz.
 """
 from __future__ import annotations
@@ -27,6 +29,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from dataplug_amd.scan import ScanContext  # noqa: E402
+from dataplug_amd.scan.objects import BlockedOffsets, ByteOffsets  # noqa: E402
 from oracle import cpu_ref, dpref  # noqa: E402
 
 
@@ -170,18 +173,89 @@ def object_mode(args, rng):
     return stats
 
 
+def csv_like(rng, size):
+    """A CSV body that pandas reads: a 3-column header, then rows of 3 fields of random length (a field up to
+    1 B - 200 KB, so rows span 256-byte and 64 KiB boundaries and wave ranges), some rows empty of text."""
+    fmax = int(rng.choice([4, 40, 400, 20000, 200000]))
+    parts, total = [b"a,b,c\n"], 6
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789 .", np.uint8)
+    while total < size:
+        fl = rng.integers(0, fmax + 1, 3)
+        row = alpha[rng.integers(0, len(alpha), int(fl.sum()))].tobytes()
+        row = row[:fl[0]] + b"," + row[fl[0]:fl[0] + fl[1]] + b"," + row[fl[0] + fl[1]:] + b"\n"
+        parts.append(row)
+        total += len(row)
+    a = np.frombuffer(b"".join(parts), np.uint8)[:max(size, 6)].copy()
+    return a
+
+
+def lines_mode(args, rng):
+    """The CSV newline index through co.preprocess() in a random stored form (u8s, u16b, u32p, u64), the object split
+    into 1-9 parts on this GPU (dataplug_devices=[0]*g: each part its own launch, the tables merged on the host),
+    read back through LineIndex (preloaded or block by block) against the oracle's newline offsets."""
+    from dataplug_amd.cloudobject import CloudObject
+    from dataplug_amd.formats import _lines
+    from dataplug_amd.formats.generic.csv import CSV
+    from dataplug_amd.storage import MemoryStore
+    stats = {"line_cases": 0, "lines": 0, "bytes": 0, "forms": {}, "groups": {}, "block_fetch_cases": 0}
+    t0 = last = time.time()
+    i = 0
+    while time.time() - t0 < args.seconds:
+        size = int(math.exp(rng.uniform(math.log(64), math.log(getattr(args, "max_size", 24 << 20)))))
+        a = csv_like(rng, size)
+        fmt = str(rng.choice(["u8s", "u8s", "u16b", "u32p", "u64"]))
+        groups = int(rng.integers(1, 10))
+        name = f"fl{i}"
+        MemoryStore._named.pop(name, None)
+        cfg = {"endpoint_url": f"memory://{name}"}
+        co = CloudObject.from_s3(CSV, f"s3://data/k{i}.csv", fetch=False, s3_config=cfg)
+        co.storage.create_bucket(Bucket="data")
+        co.storage.put_object(Body=a.tobytes(), Bucket="data", Key=f"k{i}.csv")
+        co = CloudObject.from_s3(CSV, f"s3://data/k{i}.csv", s3_config=cfg)
+        co.preprocess(parallel_config={"dataplug_devices": [0] * groups}, extra_args={"index_format": fmt})
+        preload = rng.random() < 0.5
+        saved = _lines._PRELOAD_BYTES
+        if not preload:
+            _lines._PRELOAD_BYTES = 1024
+            stats["block_fetch_cases"] += 1
+        try:
+            li = _lines.LineIndex.of(co)
+            got = li._fetch(0, li.count) if li.count else np.zeros(0, np.uint64)
+        finally:
+            _lines._PRELOAD_BYTES = saved
+        exp = dpref.delim(a, 0, len(a))[0]
+        MemoryStore._named.pop(name, None)
+        dtype_ok = getattr(co.attributes, "line_index_dtype", None) == (None if fmt == "u64" else fmt)
+        if not dtype_ok or not np.array_equal(np.asarray(got, np.uint64), exp):
+            _save_fail(data=a, groups=groups)
+            print(json.dumps({"FAIL": "lines", "size": int(len(a)), "format": fmt, "groups": groups,
+                              "got": int(len(got)), "expected": int(len(exp))}), flush=True)
+            raise SystemExit(1)
+        stats["line_cases"] += 1
+        stats["lines"] += int(len(exp))
+        stats["bytes"] += int(len(a))
+        stats["forms"][fmt] = stats["forms"].get(fmt, 0) + 1
+        stats["groups"][groups] = stats["groups"].get(groups, 0) + 1
+        i += 1
+        if time.time() - last > 20:
+            last = time.time()
+            print(json.dumps({"t": round(last - t0), **{k: v for k, v in stats.items() if k not in ("forms", "groups")}}),
+                  flush=True)
+    return stats
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=240)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--mode", choices=["kernel", "object"], default="kernel")
+    ap.add_argument("--mode", choices=["kernel", "object", "lines"], default="kernel")
     ap.add_argument("--out", default="gpurun_out/fuzz.json")
     args = ap.parse_args()
     os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
     rng = np.random.default_rng(args.seed)
-    if args.mode == "object":
-        stats = object_mode(args, rng)
-        stats.update({"seconds": args.seconds, "seed": args.seed, "ok": True, "mode": "object"})
+    if args.mode in ("object", "lines"):
+        stats = (object_mode if args.mode == "object" else lines_mode)(args, rng)
+        stats.update({"seconds": args.seconds, "seed": args.seed, "ok": True, "mode": args.mode})
         with open(args.out, "w") as f:
             json.dump(stats, f)
         print(json.dumps(stats), flush=True)
@@ -199,7 +273,7 @@ def kernel_mode(args, rng):
     """The kernels through the C ABI on random objects, chunk plans, misalignments and output forms."""
     ctx = ScanContext(0)
     stats = {"fasta_cases": 0, "fasta_pairs": 0, "quirk_cases": 0, "delim_cases": 0, "delim_offsets": 0,
-             "bytes": 0, "kinds": {}, "delim_forms": {}}
+             "bytes": 0, "kinds": {}, "delim_forms": {}, "stored_cases": 0}
     # the newline launch's kernels, drawn per case (dp_ctx_set_form): the default (line_kernel at these sizes), the
     # auto form's density probe at every size (line_max 0) with its threshold at random (either pick), or a form
     # pinned to line_kernel / the one-pass kernel
@@ -250,7 +324,16 @@ def kernel_mode(args, rng):
             add = int(rng.integers(0, 2))
             du64 = bool(rng.random() < 0.7)
             ctx.set_form(**delim_forms[int(rng.integers(0, len(delim_forms)))])
-            got, nd = ctx.delim_index(buf.ptr + off, size, 0, b0, b1, delim, k, add, u64=du64)
+            stored = k == 1 and add == 0 and b1 > b0 and rng.random() < 0.4
+            if stored:                                # u8s / u16b at object base `off` (congruent to the address)
+                mode = int(rng.choice([3, 4]))
+                r = ctx.delim_ranges(buf.ptr + off, size, off, [(b0 + off, b1 + off)], delim=delim, out_mode=mode)
+                f0 = b0 + off
+                o = ByteOffsets(r[0], r[4], r[3], f0 >> 8, f0 >> 16) if mode == 4 else BlockedOffsets(r[0], r[3], f0 >> 16)
+                got, nd = o.to_u64() - np.uint64(off), r[1]
+                stats["stored_cases"] += 1
+            else:
+                got, nd = ctx.delim_index(buf.ptr + off, size, 0, b0, b1, delim, k, add, u64=du64)
             if b1 > b0:
                 f = str(ctx.last_delim_form())
                 stats["delim_forms"][f] = stats["delim_forms"].get(f, 0) + 1
