@@ -1627,9 +1627,11 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
   uint32_t r = s_grp[0] * kMapWaves + (uint32_t)wave;
   Cursor cur{0, 0, 0, 0, 0, 0};
   Geo g = range_geo(T, nchunks, nranges, r, cur);
+  ScanArgs SA{};                                     // the input loads' base (the map kernel needs nothing else of it)
+  SA.base = M.base;
   BufN b[kBufs];
 #pragma unroll
-  for (int h = 0; h < kBufs; ++h) load_bufx(b[h], ScanArgs{M.base}, g, lane, h);
+  for (int h = 0; h < kBufs; ++h) load_bufx(b[h], SA, g, lane, h);
   for (uint32_t it = 0;; ++it) {
     __syncthreads();
     const uint32_t gnext = s_grp[(it + 1) % kGrpQ];
@@ -1663,7 +1665,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
       const uint32_t la = lookahead_s(M.base, g, h, interior, hi);
       if (interior) fasta_rows<true>(x, la, h, lo, hi, lane, st, keep);
       else fasta_rows<false>(x, la, h, lo, hi, lane, st, keep);
-      if (h + 1 < kBufs) load_bufx(b[h], ScanArgs{M.base}, gn, lane, h);
+      if (h + 1 < kBufs) load_bufx(b[h], SA, gn, lane, h);
     }
     const bool dense = st.nev > kSpillCap;
     const uint32_t n = dense ? 0u : st.nev;
@@ -1692,7 +1694,7 @@ __global__ void __launch_bounds__(kWave * kMapWaves, 4) map_kernel(MapArgs M, co
         flush();
       }
     }
-    load_bufx(b[kBufs - 1], ScanArgs{M.base}, gn, lane, kBufs - 1);
+    load_bufx(b[kBufs - 1], SA, gn, lane, kBufs - 1);
 #ifdef DP_DIAG
     n_done += (g.fl & kGeoValid) ? 1u : 0u;
 #endif
