@@ -28,9 +28,11 @@ from dataplug_amd.scan._lib import check  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=4 << 30)
+    ap.add_argument("--form", type=int, default=0, help="DP_FORM_FASTA: 0 map + placement kernels, 2 fused")
     args = ap.parse_args()
     n = args.size
     ctx = ScanContext(0)
+    ctx.set_form(fasta=args.form)
     host = synth.tiled_fasta_host(n, seed=1)
     d = ctx.workspace("in", n + 64)
     ctx.h2d(d.ptr, host)
