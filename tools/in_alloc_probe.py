@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--alloc", default="", help="comma list per buffer: d (library hipMalloc) | c (hipExtMallocWithFlags "
                     "contiguous) | u (uncached) | f (fine-grained); default all d")
     ap.add_argument("--out-alloc", default="d", help="d | c | u: the output and stream_rw buffers' allocation")
+    ap.add_argument("--lib-b", default=None, help="a second libdpscan build: its stream_rw timed beside (same buffers)")
     ap.add_argument("--wpr", type=float, default=0.025, help="stream_rw's write bytes per read byte (0: reads only, "
                     "in the same lockstep group pattern)")
     args = ap.parse_args()
@@ -87,6 +88,22 @@ def main():
     ctx.timing_read()
     st = [[] for _ in bufs]
     rw = [[] for _ in bufs]
+    rwb = [[] for _ in bufs]
+    nlb = [[] for _ in bufs]
+    ctx_b = None
+    if args.lib_b:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from lib_ab import context_on
+        ctx_b = context_on(args.lib_b)
+        out_b = ctx_b.workspace("out", ScanContext.out_bytes(max(cap, 1), args.mode, rg))
+
+        def run_b(b):
+            ctx_b.delim_ranges_async(b.ptr, size, 0, rg, 10, 1, 0, 0, out_b.ptr, args.mode, cap)
+            return ctx_b.delim_ranges_result(1)[0]
+        for b in bufs:
+            assert run_b(b) == n_exp
+        ctx_b.timing(True)
+        ctx_b.timing_read()
     nl = [[] for _ in bufs]
     wpr = args.wpr                                    # 0.025: the u8s index's write bytes per read byte on VCF
     mix = alloc("mix", int(wpr * size) + (1 << 20), args.out_alloc)
@@ -98,14 +115,23 @@ def main():
             ctx.stream_rw(b.ptr, size, mix.ptr, wpr)
             ctx.sync()
             rw[k].append(round(ctx.timing_read()[0] * 1e3, 1))
+            if ctx_b is not None:
+                ctx_b.stream_rw(b.ptr, size, mix.ptr, wpr)
+                ctx_b.sync()
+                rwb[k].append(round(ctx_b.timing_read()[0] * 1e3, 1))
             run(b)
             nl[k].append(round(ctx.timing_read()[0] * 1e3, 1))
+            if ctx_b is not None:
+                run_b(b)
+                nlb[k].append(round(ctx_b.timing_read()[0] * 1e3, 1))
     ctx.timing(False)
     print(json.dumps({"content": args.content, "size_gib": args.size_gib, "mode": args.mode, "cap0": args.cap0,
                       "buffers": [{"gib": round(b.nbytes / (1 << 30), 2), "kind": b.kind, "addr_gib": round(b.ptr / (1 << 30), 2),
                                    "stream_us": float(np.median(s)), "stream_rw_us": float(np.median(w)),
+                                   "stream_rw_b_us": float(np.median(wb)) if wb else None,
+                                   "newline_b_us": float(np.median(tb)) if tb else None,
                                    "newline_us": float(np.median(t)), "newline_all": t}
-                                  for b, s, w, t in zip(bufs, st, rw, nl)]}), flush=True)
+                                  for b, s, w, wb, t, tb in zip(bufs, st, rw, rwb, nl, nlb)]}), flush=True)
 
 
 if __name__ == "__main__":
