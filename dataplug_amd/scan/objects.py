@@ -25,9 +25,9 @@ _HALO0 = 64 << 10             # first look-ahead window when a header line cross
 # HBM one FASTA launch may hold: a GPU's chunk group whose bytes plus scan workspace exceed this (an object far
 # beyond 288 GB x GPUs, or a small budget set for tests) is scanned in several passes of whole chunks
 MAX_LAUNCH_BYTES = 64 << 30
-# the two-kernel scan's workspace per input byte (libdpscan ensure_ranges): a 32-byte record and a 1 KiB spill
-# slot per 16 KiB range, grown with 1/8 headroom -- 7.3 % on top of the input bytes
-WORKSPACE_PER_BYTE = (2 * 16 + 512 * 2) / 16384 * 1.125
+# the FASTA scan's workspace per input byte (libdpscan ensure_ranges): a 16-byte range record and a 1 KiB spill
+# slot per 16 KiB range, grown with 1/8 headroom -- 7.1 % on top of the input bytes
+WORKSPACE_PER_BYTE = (16 + 512 * 2) / 16384 * 1.125
 
 
 def max_launch_bytes() -> int:
