@@ -2,15 +2,17 @@
 
 The reference finds CSV/VCF slice boundaries at ``get()`` time by scanning a padded byte range in Python
 (csv.py:52-105, vcf.py:88-149).  Here ``preprocess`` builds the sorted offsets of every ``'\\n'`` on the GPU
-once — as uint16 low words plus the entry count below each 64 KiB boundary (the GPU writes a quarter of the
-bytes of a uint64 index; the block table is a separate small object) — stores them at
-``s3://<bucket>.meta/<key>.lines``,
+once — by default as uint8 low bytes plus the 16-bit entry counts before every 256-byte boundary and the
+entry count below each 64 KiB boundary (u8s: the GPU writes about an eighth of the bytes of a uint64 index; the
+counts and the block table are separate small objects) — stores them at ``s3://<bucket>.meta/<key>.lines``,
 and a partition strategy resolves each
 slice's exact byte range from that index, reproducing the reference's ``get()`` output (SURVEY.md §8(a)
 formulas, restated below with the clamps the reference's buffer arithmetic implies).
 """
 from __future__ import annotations
 
+import concurrent.futures as cf
+import threading
 from collections import OrderedDict
 from typing import Optional, Tuple
 
@@ -22,6 +24,19 @@ from ..version import __version__
 LINES_SUFFIX = ".lines"
 _PRELOAD_BYTES = 256 << 20
 _BLOCK = 8192                      # entries per cached block for large indexes
+
+
+_POOL = None
+_POOL_LOCK = threading.Lock()
+
+
+def _put_pool() -> cf.ThreadPoolExecutor:
+    """One persistent thread for an index's side PUTs (a thread-local HTTP connection kept across calls)."""
+    global _POOL
+    with _POOL_LOCK:
+        if _POOL is None:
+            _POOL = cf.ThreadPoolExecutor(1, thread_name_prefix="dp-index-put")
+        return _POOL
 
 
 def store_line_index(cloud_object, offsets) -> dict:
@@ -39,10 +54,16 @@ def store_line_index(cloud_object, offsets) -> dict:
     meta = {"dataplug": __version__}
     attrs = {"line_index_key": key, "num_lines": int(len(offsets))}
     if hasattr(offsets, "sub"):
-        st.put_object(Body=np.ascontiguousarray(offsets.low, np.uint8).data, Bucket=bucket, Key=key, Metadata=meta)
         skey, bkey = key + ".sub", key + ".blocks"
-        st.put_object(Body=np.ascontiguousarray(offsets.sub, "<u2").data, Bucket=bucket, Key=skey, Metadata=meta)
-        st.put_object(Body=np.ascontiguousarray(offsets.table, "<u8").data, Bucket=bucket, Key=bkey, Metadata=meta)
+        # the counts and the table go up beside the low bytes (two requests in flight over HTTP)
+        side = _put_pool().submit(lambda: [
+            st.put_object(Body=np.ascontiguousarray(offsets.sub, "<u2").data, Bucket=bucket, Key=skey, Metadata=meta),
+            st.put_object(Body=np.ascontiguousarray(offsets.table, "<u8").data, Bucket=bucket, Key=bkey,
+                          Metadata=meta)])
+        try:
+            st.put_object(Body=np.ascontiguousarray(offsets.low, np.uint8).data, Bucket=bucket, Key=key, Metadata=meta)
+        finally:
+            side.result()
         attrs.update(line_index_dtype="u8s", line_index_sub_key=skey, line_index_sub0=int(offsets.s0),
                      line_index_blocks_key=bkey, line_index_block0=int(offsets.j0))
     elif hasattr(offsets, "table"):

@@ -90,14 +90,21 @@ def _meta_from(extra_args: Optional[dict]) -> Dict[str, str]:
     return dict((extra_args or {}).get("Metadata") or {})
 
 
-def _body_bytes(body) -> bytes:
+def _body_bytes(body):
+    """A PUT body as bytes, or as a flat byte view of a contiguous buffer (no copy: an HTTP request sends it as it
+    is, the memory store copies it into its own bytes)."""
     if body is None:
         return b""
     if isinstance(body, str):
         return body.encode("utf-8")
     if hasattr(body, "read"):
         return body.read()
-    return bytes(body)
+    if isinstance(body, bytes):
+        return body
+    try:
+        return memoryview(body).cast("B")
+    except TypeError:                             # (a non-contiguous buffer)
+        return bytes(body)
 
 
 class _ClientBase:

@@ -98,8 +98,12 @@ class MemoryStore:
             raise ClientError("NoSuchBucket", op, bucket, 404)
         return b
 
-    def put(self, bucket: str, key: str, data, metadata: Optional[Dict[str, str]] = None) -> StoredObject:
-        obj = StoredObject(bytes(data), dict(metadata or {}))
+    def put(self, bucket: str, key: str, data, metadata: Optional[Dict[str, str]] = None,
+            owned: bool = False) -> StoredObject:
+        """Store a copy of ``data``; ``owned``: a bytes / bytearray the caller hands over (kept as it is, never
+        written again: the loopback server's request bodies)."""
+        keep = data if owned and isinstance(data, (bytes, bytearray)) else bytes(data)
+        obj = StoredObject(keep, dict(metadata or {}))
         with self._lock:
             self._bucket(bucket, "PutObject")[key] = obj
         return obj

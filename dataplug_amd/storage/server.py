@@ -62,7 +62,7 @@ class _Handler(BaseHTTPRequestHandler):
         self._send(status, b"" if head_only else body, {"Content-Type": "application/xml"} if not head_only else {},
                    head_only=head_only)
 
-    def _read_body(self) -> bytes:
+    def _read_body(self) -> bytearray:
         n = int(self.headers.get("Content-Length") or 0)
         if self.headers.get("Transfer-Encoding", "").lower() == "chunked":
             raise ClientError("NotImplemented", "PutObject", "chunked uploads are not supported", 501)
@@ -74,7 +74,7 @@ class _Handler(BaseHTTPRequestHandler):
             if not r:
                 raise ClientError("IncompleteBody", "PutObject", f"{got} of {n} bytes", 400)
             got += r
-        return bytes(buf)
+        return buf                                  # (the store keeps it: no second copy of the body)
 
     # ---------------------------------------------------------------- verbs
     def do_HEAD(self):
@@ -140,7 +140,7 @@ class _Handler(BaseHTTPRequestHandler):
                 return self._send(200, headers={"Location": f"/{b}"})
             meta = {h[len("x-amz-meta-"):].lower(): v for h, v in self.headers.items()
                     if h.lower().startswith("x-amz-meta-")}
-            o = self.store.put(b, k, body, meta)
+            o = self.store.put(b, k, body, meta, owned=True)
             self._send(200, headers={"ETag": o.etag})
         except ClientError as e:
             self._error(e)
