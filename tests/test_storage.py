@@ -116,3 +116,59 @@ def test_proxy_requires_endpoint(monkeypatch):
     monkeypatch.delenv("DATAPLUG_S3_ENDPOINT", raising=False)
     with pytest.raises(ValueError):
         PickleableS3ClientProxy()
+
+
+def test_put_buffer_bodies(client):
+    """Array bodies go up without a copy on the client side (a flat byte view) and read back as their bytes;
+    the stored object does not follow later writes to the caller's array."""
+    import numpy as np
+    client.create_bucket(Bucket="arr")
+    a = np.arange(1000, dtype="<u8")
+    client.put_object(Body=a.data, Bucket="arr", Key="c")
+    client.put_object(Body=a[::3], Bucket="arr", Key="s")              # non-contiguous: copied
+    client.put_object(Body=np.zeros(0, np.uint8), Bucket="arr", Key="e")
+    want = a.tobytes()
+    a[:] = 7
+    assert client.get_object(Bucket="arr", Key="c")["Body"].read() == want
+    assert client.get_object(Bucket="arr", Key="s")["Body"].read() == np.arange(1000, dtype="<u8")[::3].tobytes()
+    assert client.get_object(Bucket="arr", Key="e")["Body"].read() == b""
+    assert client.head_object(Bucket="arr", Key="c")["ContentLength"] == 8000
+
+
+def test_memory_store_owned_put():
+    st = MemoryStore()
+    st.create_bucket("b")
+    src = bytearray(b"abc")
+    assert st.put("b", "copied", src).data == b"abc"
+    src[0] = ord("x")
+    assert st.get("b", "copied").data == b"abc"                          # a copy unless handed over
+    kept = bytearray(b"def")
+    assert st.put("b", "owned", kept, owned=True).data is kept
+
+
+def test_store_line_index_u8s(client):
+    """The u8s index's three objects (low bytes here, counts and block table on the side thread) and its
+    attributes; a failed PUT (no such bucket) raises from the call."""
+    import numpy as np
+    from dataplug_amd.formats._lines import store_line_index
+    from dataplug_amd.scan.objects import ByteOffsets
+    from dataplug_amd.storage import S3Path
+
+    class Co:
+        storage = client
+        meta_path = S3Path.from_bucket_key("idx.meta", "obj")
+    client.create_bucket(Bucket="idx.meta")
+    off = ByteOffsets(np.arange(5, dtype=np.uint8), np.asarray([0, 5], np.uint16), np.asarray([0], np.uint64), 0, 0)
+    attrs = store_line_index(Co, off)
+    assert attrs["line_index_dtype"] == "u8s" and attrs["num_lines"] == 5
+
+    def get(key):
+        return client.get_object(Bucket="idx.meta", Key=key)["Body"].read()
+    assert get(attrs["line_index_key"]) == bytes(range(5))
+    assert get(attrs["line_index_sub_key"]) == np.asarray([0, 5], "<u2").tobytes()
+    assert get(attrs["line_index_blocks_key"]) == np.zeros(1, "<u8").tobytes()
+
+    class Missing(Co):
+        meta_path = S3Path.from_bucket_key("no-such-bucket.meta", "obj")
+    with pytest.raises(ClientError):
+        store_line_index(Missing, off)
