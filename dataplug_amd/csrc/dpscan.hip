@@ -3202,7 +3202,7 @@ int collect_ctrl(dp_ctx* c) {
 
 extern "C" {
 
-int dp_abi_version(void) { return 1; }
+int dp_abi_version(void) { return DP_ABI_VERSION; }
 
 const char* dp_last_error(void) { return g_err.c_str(); }
 
@@ -3233,7 +3233,8 @@ int dp_ctx_create(int device, dp_ctx** out) {
   int occ = 0;
   HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (scan_kernel<kFasta, 0>), kThreads, 0));
   const void* others[] = {(const void*)scan_kernel<kFasta, 1>, (const void*)scan_kernel<kDelim, 0>,
-                          (const void*)scan_kernel<kDelim, 1>, (const void*)scan_kernel<kDelim, 2>};
+                          (const void*)scan_kernel<kDelim, 1>, (const void*)scan_kernel<kDelim, 2>,
+                          (const void*)scan_kernel<kDelim, 3>};
   for (const void* k : others) {
     int o = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, k, kThreads, 0));

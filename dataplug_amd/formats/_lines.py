@@ -12,6 +12,7 @@ formulas, restated below with the clamps the reference's buffer arithmetic impli
 from __future__ import annotations
 
 import concurrent.futures as cf
+import os
 import threading
 from collections import OrderedDict
 from typing import Optional, Tuple
@@ -27,16 +28,28 @@ _BLOCK = 8192                      # entries per cached block for large indexes
 
 
 _POOL = None
+_POOL_PID = None
 _POOL_LOCK = threading.Lock()
 
 
 def _put_pool() -> cf.ThreadPoolExecutor:
-    """One persistent thread for an index's side PUTs (a thread-local HTTP connection kept across calls)."""
-    global _POOL
+    """One persistent thread for an index's side PUTs (a thread-local HTTP connection kept across calls).  A
+    forked child inherits the executor but not its thread, so a new one is made whenever the pid changes."""
+    global _POOL, _POOL_PID
     with _POOL_LOCK:
-        if _POOL is None:
+        if _POOL is None or _POOL_PID != os.getpid():
             _POOL = cf.ThreadPoolExecutor(1, thread_name_prefix="dp-index-put")
+            _POOL_PID = os.getpid()
         return _POOL
+
+
+def _reset_pool_in_child():
+    global _POOL, _POOL_PID, _POOL_LOCK
+    _POOL, _POOL_PID, _POOL_LOCK = None, None, threading.Lock()
+
+
+if hasattr(os, "register_at_fork"):
+    os.register_at_fork(after_in_child=_reset_pool_in_child)
 
 
 def store_line_index(cloud_object, offsets) -> dict:
@@ -62,8 +75,10 @@ def store_line_index(cloud_object, offsets) -> dict:
                           Metadata=meta)])
         try:
             st.put_object(Body=np.ascontiguousarray(offsets.low, np.uint8).data, Bucket=bucket, Key=key, Metadata=meta)
-        finally:
-            side.result()
+        except BaseException:
+            side.exception()                  # let the side PUTs finish; the low bytes' error is the one raised
+            raise
+        side.result()
         attrs.update(line_index_dtype="u8s", line_index_sub_key=skey, line_index_sub0=int(offsets.s0),
                      line_index_blocks_key=bkey, line_index_block0=int(offsets.j0))
     elif hasattr(offsets, "table"):
@@ -93,7 +108,7 @@ class LineIndex:
         self._arr = None if offsets is None else np.asarray(offsets, dtype=np.uint64)
         self._storage, self._bucket, self._key = storage, bucket, key
         self._pages = None if pages is None else np.asarray(pages, np.int64)
-        self._blocks_tab = None if blocks is None else np.asarray(blocks, np.int64)
+        self._blocks_tab = None if blocks is None else np.asarray(blocks, np.uint64)   # converted once
         self._block0 = int(block0)
         self._sub_key, self._sub0 = sub_key, int(sub0)
         self._item = 1 if sub_key is not None else (2 if blocks is not None else (4 if pages is not None else 8))
@@ -102,7 +117,10 @@ class LineIndex:
             if count is None:
                 count = int(storage.head_object(Bucket=bucket, Key=key)["ContentLength"]) // self._item
             self.count = int(count)
-            if self.count * self._item <= _PRELOAD_BYTES:
+            # a preload of the uint8 form also reads every 256-byte count (2 B per 256 object bytes, whatever the
+            # number of entries): a sparse index of a large object is read block by block instead
+            side = 2 * 256 * len(self._blocks_tab) if self._item == 1 else 0
+            if self.count * self._item + side <= _PRELOAD_BYTES:
                 self._arr = self._fetch(0, self.count)
         else:
             self.count = len(self._arr)
@@ -141,20 +159,31 @@ class LineIndex:
             page = np.searchsorted(self._pages, idx, side="right").astype(np.uint64)
             return (page << np.uint64(32)) | np.frombuffer(raw, dtype="<u4").astype(np.uint64)
         if it == 1:
-            # the 256-byte boundaries of the 64 KiB blocks entries i0 .. i1 - 1 lie in, and the counts before them
-            from ..scan.objects import sub_counts
-            ja = int(np.searchsorted(self._blocks_tab, i0, side="right")) - 1
-            jb = int(np.searchsorted(self._blocks_tab, i1 - 1, side="right")) - 1
-            s0 = self._sub0
-            sa = max(0, ((self._block0 + ja) << 8) - s0)
-            sb = ((self._block0 + jb + 1) << 8) - s0
-            res = self._storage.get_object(Bucket=self._bucket, Key=self._sub_key, Range=f"bytes={2 * sa}-{2 * sb - 1}")
-            sub = np.frombuffer(res["Body"].read(), dtype="<u2")
-            c = sub_counts(sub, self._blocks_tab.astype(np.uint64), s0, self._block0, sa)
-            s = np.searchsorted(c, idx.astype(np.uint64), side="right").astype(np.uint64) - np.uint64(1) + np.uint64(sa)
-            return ((s + np.uint64(s0)) << np.uint64(8)) | np.frombuffer(raw, dtype=np.uint8).astype(np.uint64)
+            return self._decode_bytes(idx, np.frombuffer(raw, dtype=np.uint8))
         blk = np.searchsorted(self._blocks_tab, idx, side="right").astype(np.uint64) - np.uint64(1)
         return ((blk + np.uint64(self._block0)) << np.uint64(16)) | np.frombuffer(raw, dtype="<u2").astype(np.uint64)
+
+    _SUB_GAP = 4                      # needed 64 KiB blocks at most this many apart share one ranged GET of counts
+
+    def _decode_bytes(self, idx: np.ndarray, low: np.ndarray) -> np.ndarray:
+        """Offsets of entries ``idx`` (ascending) of the uint8 form from their low bytes: the 256-byte counts are
+        read only for the 64 KiB blocks the entries lie in (runs of nearby blocks coalesced into one GET), so the
+        bytes read follow the entries, not the object bytes they span."""
+        from ..scan.objects import sub_counts
+        tab, s0, j0 = self._blocks_tab, self._sub0, self._block0
+        blk = np.searchsorted(tab, idx.astype(np.uint64), side="right").astype(np.int64) - 1
+        need = np.unique(blk)
+        cut = np.flatnonzero(np.diff(need) > self._SUB_GAP) + 1
+        s = np.empty(len(idx), np.uint64)
+        for run in np.split(need, cut):
+            ja, jb = int(run[0]), int(run[-1])
+            sa = max(0, ((j0 + ja) << 8) - s0)
+            sb = ((j0 + jb + 1) << 8) - s0
+            res = self._storage.get_object(Bucket=self._bucket, Key=self._sub_key, Range=f"bytes={2 * sa}-{2 * sb - 1}")
+            c = sub_counts(np.frombuffer(res["Body"].read(), dtype="<u2"), tab, s0, j0, sa)
+            a, b = np.searchsorted(blk, [ja, jb + 1])
+            s[a:b] = (np.searchsorted(c, idx[a:b].astype(np.uint64), side="right").astype(np.int64) + (sa - 1)).astype(np.uint64)
+        return ((s + np.uint64(s0)) << np.uint64(8)) | low.astype(np.uint64)
 
     def _block(self, b: int) -> np.ndarray:
         blk = self._blocks.get(b)

@@ -1,8 +1,9 @@
 """CSV format plugin (dataplug/formats/generic/csv.py) with a GPU-built newline index.
 
 ``preprocess_csv`` keeps the reference's attributes (``columns``/``dtypes`` from the first 20 lines,
-csv.py:20-36) and additionally stores the sorted ``uint64`` offsets of every ``'\\n'`` (scanned on the
-GPUs) at ``<key>.lines`` in the meta bucket (attributes ``num_lines``, ``line_index_key``).  The meta
+csv.py:20-36) and additionally stores the sorted offsets of every ``'\\n'`` (scanned on the GPUs) at
+``<key>.lines`` in the meta bucket (attributes ``num_lines``, ``line_index_key``, ``line_index_dtype``; with
+``index_format="auto"`` the u8s form, or u16b for objects with fewer than one newline per 128 bytes).  The meta
 object itself stays empty, as in the reference.  The partition strategies produce the reference's
 ``range_0``/``range_1`` and a ``get()`` with identical output, resolved from the index instead of a
 padded Python scan per slice (the reference's formulas: ``_lines.csv_body``).
@@ -26,7 +27,7 @@ logger = logging.getLogger(__name__)
 
 
 def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index: bool = True,
-                   index_format: str = "u8s") -> PreprocessingMetadata:
+                   index_format: str = "auto") -> PreprocessingMetadata:
     import pandas as pd
 
     top = []

@@ -2,8 +2,9 @@
 
 ``preprocess_vcf`` keeps the reference's header parse and outputs (attributes ``columns``,
 ``vcf_attributes``, ``body_offset``; meta object = the stripped header lines joined by '\\n',
-vcf.py:19-67) and adds the ``uint64`` offsets of every '\\n' in ``[body_offset, size)``, scanned on the GPUs
-in independent parts (one or more per GPU), stored at ``<key>.lines``.  ``partition_num_chunks`` gives
+vcf.py:19-67) and adds the offsets of every '\\n' in ``[body_offset, size)``, scanned on the GPUs in independent
+parts (one or more per GPU), stored at ``<key>.lines`` (``index_format="auto"``: the u8s form, or u16b for bodies
+with fewer than one newline per 128 bytes; ``_lines.store_line_index``).  ``partition_num_chunks`` gives
 the reference's ranges and a ``get()`` with identical output (formulas: ``_lines.vcf_body``).
 """
 from __future__ import annotations
@@ -59,7 +60,7 @@ def parse_vcf_header(f):
     return header, meta, columns, pos
 
 
-def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True, index_format: str = "u8s") -> PreprocessingMetadata:
+def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True, index_format: str = "auto") -> PreprocessingMetadata:
     with cloud_object.open("rb") as f:
         header, meta, columns, body_offset = parse_vcf_header(f)
     attrs = {"columns": columns, "vcf_attributes": meta, "body_offset": body_offset}

@@ -93,6 +93,7 @@ class DPCapacityError(DPScanError):
 
 
 _lib = None
+ABI_VERSION = 2                          # include/dpscan.h DP_ABI_VERSION: the oldest library these signatures fit
 
 
 def load():
@@ -108,6 +109,11 @@ def load():
         lib = ctypes.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover - depends on the ROCm runtime being present
         raise DPScanUnavailable(f"cannot load {LIB_PATH}: {e}") from e
+    lib.dp_abi_version.restype = ctypes.c_int
+    ver = int(lib.dp_abi_version())
+    if ver < ABI_VERSION and "DPSCAN_LIB" not in os.environ:
+        raise DPScanUnavailable(f"{LIB_PATH} has ABI version {ver}, this binding needs {ABI_VERSION} "
+                                f"(dp_scan_delim_form's argument list changed in 2): rebuild it")
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name, None)
         if fn is None:

@@ -461,6 +461,31 @@ class ByteOffsets:
 
 
 INDEX_FORMATS = ("u8s", "u16b", "u32p", "u64")
+# "auto" (the CSV / VCF plugins' default): u8s costs 1 B per entry + 2 B per 256 object bytes, u16b 2 B per entry
+# (both + 8 B per 64 KiB), so u8s is the smaller index and the cheaper read while there is a delimiter at least
+# every 128 bytes; sparser objects (multi-sample VCF rows of 100 KB) store u16b.
+AUTO_BYTES_PER_ENTRY = 128
+_AUTO_SAMPLES, _AUTO_SAMPLE_BYTES = 8, 64 << 10
+
+
+def line_index_form(co, begin: int, end: int, delim: int = 10) -> str:
+    """The stored form "auto" picks for object bytes [begin, end): u8s unless a sample of the object (8 ranged GETs
+    of 64 KiB spread evenly; the whole range when it is smaller) holds fewer than one delimiter per
+    ``AUTO_BYTES_PER_ENTRY`` bytes.  Either form stores the same offsets; this only sizes the index."""
+    n = end - begin
+    if n <= 0:
+        return "u8s"
+    if n <= _AUTO_SAMPLES * _AUTO_SAMPLE_BYTES:
+        spans = [(begin, end)]
+    else:
+        step = (n - _AUTO_SAMPLE_BYTES) // (_AUTO_SAMPLES - 1)
+        spans = [(begin + k * step, begin + k * step + _AUTO_SAMPLE_BYTES) for k in range(_AUTO_SAMPLES)]
+    seen = hits = 0
+    for a, b in spans:
+        raw = co.storage.get_object(Bucket=co.path.bucket, Key=co.path.key, Range=f"bytes={a}-{b - 1}")["Body"].read()
+        seen += len(raw)
+        hits += raw.count(bytes([delim]))
+    return "u8s" if hits * AUTO_BYTES_PER_ENTRY >= seen else "u16b"
 
 
 def line_parts(begin: int, end: int, n_devices: int, part_bytes: int = 16 << 30) -> List[Tuple[int, int]]:
@@ -498,13 +523,16 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
     """Sorted offsets of every ``delim`` byte of object bytes [begin, end) in one of ``INDEX_FORMATS``:
     ``u64`` a uint64 array; ``u32p`` a ``PagedOffsets`` (uint32 low words + 4 GiB page counts); ``u16b`` a
     ``BlockedOffsets`` (uint16 low words + a 64 KiB block table); ``u8s`` a ``ByteOffsets`` (uint8 low bytes + the
-    256-byte counts + the 64 KiB block table) — the GPU writes 8, 4, 2 or 1 bytes per offset.
+    256-byte counts + the 64 KiB block table) — the GPU writes 8, 4, 2 or 1 bytes per offset; ``auto`` u8s or
+    u16b by the object's delimiter density (``line_index_form``).
 
     The range is cut into independent parts (at most ``part_bytes`` each, at least one per GPU) scanned
     round-robin on the GPUs and concatenated in order."""
-    if fmt not in INDEX_FORMATS:
-        raise ValueError(f"index format must be one of {INDEX_FORMATS}, not {fmt!r}")
+    if fmt != "auto" and fmt not in INDEX_FORMATS:
+        raise ValueError(f"index format must be 'auto' or one of {INDEX_FORMATS}, not {fmt!r}")
     end = co.size if end is None else end
+    if fmt == "auto":
+        fmt = line_index_form(co, begin, end, delim)
     if end <= begin:
         return {"u64": np.zeros(0, np.uint64), "u32p": PagedOffsets(np.zeros(0, np.uint32), []),
                 "u16b": BlockedOffsets(np.zeros(0, np.uint16), np.zeros(1, np.uint64), begin >> 16),

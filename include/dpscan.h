@@ -44,7 +44,11 @@ extern "C" {
 
 typedef struct dp_ctx dp_ctx;
 
-int dp_abi_version(void);                                  /* returns the ABI version number */
+/* ABI version history: 1 (rounds 1-4); 2 (round 5): dp_scan_delim_form gained its out_mode argument, dp_scan_forms
+   was removed, dp_ctx_set_form / dp_ctx_get_form / dp_last_delim_form were added.  A binding checks
+   dp_abi_version() >= DP_ABI_VERSION before it binds anything (dataplug_amd/scan/_lib.py refuses older builds). */
+#define DP_ABI_VERSION 2
+int dp_abi_version(void);                                  /* returns DP_ABI_VERSION of the build */
 const char* dp_last_error(void);                           /* thread-local message of the last failure */
 int dp_device_count(int* n);
 int dp_ctx_create(int device, dp_ctx** out);               /* binds `device`, creates a non-blocking stream */

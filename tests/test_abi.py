@@ -38,7 +38,7 @@ def test_ctypes_table_matches_header():
 
 def test_abi_version_and_errors_without_gpu():
     lib = _lib.load()
-    assert lib.dp_abi_version() >= 1
+    assert lib.dp_abi_version() == _lib.ABI_VERSION == 2
     n = ctypes.c_int(-1)
     rc = lib.dp_device_count(ctypes.byref(n))
     assert rc in (0, _lib.DP_ERR_HIP)

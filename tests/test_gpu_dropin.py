@@ -46,10 +46,12 @@ def _index(co):
 
 
 def _lines_u64(co):
-    """The stored newline index (the default u8s: uint8 low bytes + 256-byte counts + 64 KiB block table) as uint64
-    offsets."""
+    """The stored newline index (index_format "auto": u8s, uint8 low bytes + 256-byte counts + 64 KiB block table, or
+    u16b for objects with fewer than one newline per 128 bytes) as uint64 offsets."""
     from dataplug_amd.formats._lines import LineIndex
-    assert co.attributes.line_index_dtype == "u8s"
+    from dataplug_amd.scan.objects import line_index_form
+    begin = int(getattr(co.attributes, "body_offset", 0) or 0)
+    assert co.attributes.line_index_dtype == line_index_form(co, begin, co.size)
     li = LineIndex.of(co)
     return li._fetch(0, li.count)
 

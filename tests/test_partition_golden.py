@@ -300,3 +300,89 @@ def test_byte_line_index_sparse_and_dense(monkeypatch, preload, first_delta):
         i = int(np.searchsorted(off, np.uint64(x)))
         assert li.nxt(x) == (int(off[i]) + 1 if i < len(off) else None), x
         assert li.contains(x) == (i < len(off) and int(off[i]) == x)
+
+
+def test_byte_line_index_sparse_reads_follow_entries(monkeypatch):
+    """a sparse uint8 index (1 MB lines over 2 GB) is not preloaded when its 256-byte counts (2 B per
+    256 object bytes) exceed the preload budget, and a block of entries reads the counts of the 64 KiB blocks those
+    entries lie in, not of every block they span."""
+    from dataplug_amd.formats import _lines
+    monkeypatch.setattr(_lines, "_PRELOAD_BYTES", 1 << 20)
+    rng = np.random.default_rng(11)
+    first = (3 << 30) + 77
+    off = np.unique((first + np.arange(2_000, dtype=np.int64) * 1_000_003 + rng.integers(0, 4096, 2_000))
+                    .astype(np.uint64))
+    bo = byte_offsets(off, first, int(off[-1]) + 1)
+    co = _co(_lines_fmt(), "sparse_u8s", b"x" * 16, {}, nl=False)
+    attrs = store_line_index(co, bo)
+    blocks = np.frombuffer(co.storage.get_object(Bucket=co.meta_path.bucket, Key=attrs["line_index_blocks_key"])
+                           ["Body"].read(), "<u8")
+    fetched = []
+    real_get = co.storage.get_object
+
+    def counting_get(**kw):
+        res = real_get(**kw)
+        if kw.get("Key") == attrs["line_index_sub_key"]:
+            body = res["Body"].read()
+            fetched.append(len(body))
+            res = dict(res, Body=__import__("io").BytesIO(body))
+        return res
+    monkeypatch.setattr(co.storage, "get_object", counting_get)
+    li = _lines.LineIndex(storage=co.storage, bucket=co.meta_path.bucket, key=attrs["line_index_key"],
+                          count=attrs["num_lines"], blocks=blocks, block0=attrs["line_index_block0"],
+                          sub_key=attrs["line_index_sub_key"], sub0=attrs["line_index_sub0"])
+    assert li._arr is None and not fetched                     # 16 MB of counts: not preloaded
+    for x in [0, first, int(off[7]), int(off[7]) + 1, int(off[1234]) - 5, int(off[-1]), int(off[-1]) + 1]:
+        i = int(np.searchsorted(off, np.uint64(x)))
+        assert li.nxt(x) == (int(off[i]) + 1 if i < len(off) else None), x
+    assert np.array_equal(li._fetch(0, li.count), off)
+    span = 2 * (len(bo.sub))
+    # each entry's 64 KiB block: 512 B of counts; two blocks at most per entry (a run never joins blocks > 4 apart)
+    assert sum(fetched) <= 2 * (2 * 512 * len(off)) < span / 3, (sum(fetched), span)
+
+
+def test_auto_index_form_follows_density():
+    """``index_format="auto"`` (the CSV / VCF default): u8s while the object holds a newline at least every 128 bytes
+    (a sample of 8 ranged GETs of 64 KiB), u16b for sparser objects; small objects are read whole."""
+    from dataplug_amd.scan.objects import line_index_form
+    rng = np.random.default_rng(3)
+
+    def obj(line_len, size):
+        data = rng.integers(65, 90, size, dtype=np.uint8)
+        data[line_len - 1::line_len] = 10
+        return _co(_lines_fmt(), f"dens{line_len}_{size}", data.tobytes(), {}, nl=False)
+    for line_len, size, want in [(36, 8 << 20, "u8s"), (127, 8 << 20, "u8s"), (129, 8 << 20, "u16b"),
+                                 (100_000, 8 << 20, "u16b"), (40, 100_000, "u8s"), (5_000, 100_000, "u16b")]:
+        co = obj(line_len, size)
+        assert line_index_form(co, 0, size) == want, (line_len, size)
+    co = obj(36, 1 << 20)
+    assert line_index_form(co, 5, 5) == "u8s"
+
+
+def test_index_put_error_is_the_low_bytes_error(monkeypatch):
+    """when the low-bytes PUT and a side PUT both fail, the low bytes' error is raised (the side PUTs are
+    waited for, never masking it)."""
+    from dataplug_amd.formats import _lines
+    off = np.arange(100, 5_000, 37, dtype=np.uint64)
+    co = _co(_lines_fmt(), "put_err", b"x" * 16, {}, nl=False)
+
+    def put(**kw):
+        raise RuntimeError("low" if kw["Key"].endswith(".lines") else "side")
+    monkeypatch.setattr(co.storage, "put_object", put)
+    with pytest.raises(RuntimeError, match="^low$"):
+        store_line_index(co, byte_offsets(off, 100, 5_000))
+
+
+def test_index_put_pool_after_fork():
+    """a forked child gets a new side-PUT executor (the parent's worker thread does not exist there)."""
+    from dataplug_amd.formats import _lines
+    assert _lines._put_pool().submit(lambda: 7).result(timeout=10) == 7
+    pid = os.fork()
+    if pid == 0:                                   # pragma: no cover - the child
+        try:
+            ok = _lines._put_pool().submit(lambda: 7).result(timeout=10) == 7
+        except BaseException:
+            ok = False
+        os._exit(0 if ok else 1)
+    _, status = os.waitpid(pid, 0)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0
