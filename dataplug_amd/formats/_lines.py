@@ -29,16 +29,17 @@ _BLOCK = 8192                      # entries per cached block for large indexes
 
 _POOL = None
 _POOL_PID = None
+_PUT_THREADS = 3
 _POOL_LOCK = threading.Lock()
 
 
 def _put_pool() -> cf.ThreadPoolExecutor:
-    """One persistent thread for an index's side PUTs (a thread-local HTTP connection kept across calls).  A
-    forked child inherits the executor but not its thread, so a new one is made whenever the pid changes."""
+    """The persistent threads of an index's side and part PUTs (thread-local HTTP connections kept across calls).
+    A forked child inherits the executor but not its threads, so a new one is made whenever the pid changes."""
     global _POOL, _POOL_PID
     with _POOL_LOCK:
         if _POOL is None or _POOL_PID != os.getpid():
-            _POOL = cf.ThreadPoolExecutor(1, thread_name_prefix="dp-index-put")
+            _POOL = cf.ThreadPoolExecutor(_PUT_THREADS, thread_name_prefix="dp-index-put")
             _POOL_PID = os.getpid()
         return _POOL
 
@@ -93,6 +94,123 @@ def store_line_index(cloud_object, offsets) -> dict:
     else:
         st.put_object(Body=np.ascontiguousarray(offsets, "<u8").tobytes(), Bucket=bucket, Key=key, Metadata=meta)
     return attrs
+
+
+PART_MIN = 16 << 20                # streamed index: bytes per multipart part (S3's minimum is 5 MiB)
+
+
+class MultipartWriter:
+    """Byte arrays appended in order to one object, uploaded while later ones are still being produced: parts of at
+    least ``part_min`` bytes go up as a multipart upload from the PUT threads as they fill; an object smaller than
+    one part is one ``put_object`` at ``close``.  ``abort`` (or an exception in ``close``) removes the upload."""
+
+    def __init__(self, storage, bucket: str, key: str, meta: dict, part_min: int = PART_MIN):
+        self.st, self.bucket, self.key, self.meta, self.part_min = storage, bucket, key, meta, part_min
+        self.pending, self.npend, self.size = [], 0, 0
+        self.uid, self.futs = None, []
+
+    def append(self, arr) -> None:
+        a = np.ascontiguousarray(arr).reshape(-1).view(np.uint8)
+        if a.nbytes:
+            self.pending.append(a)
+            self.npend += a.nbytes
+            self.size += a.nbytes
+        if self.npend >= self.part_min:
+            self._flush()
+
+    def _flush(self) -> None:
+        data = self.pending[0] if len(self.pending) == 1 else np.concatenate(self.pending)
+        self.pending, self.npend = [], 0
+        if self.uid is None:
+            self.uid = self.st.create_multipart_upload(Bucket=self.bucket, Key=self.key, Metadata=self.meta)["UploadId"]
+        n = len(self.futs) + 1
+        self.futs.append(_put_pool().submit(self.st.upload_part, Bucket=self.bucket, Key=self.key, PartNumber=n,
+                                            UploadId=self.uid, Body=data.data))
+
+    def close(self) -> int:
+        """Finish the object (waits for its parts); returns its size."""
+        if self.uid is None:
+            data = np.concatenate(self.pending) if len(self.pending) > 1 else \
+                (self.pending[0] if self.pending else np.zeros(0, np.uint8))
+            self.st.put_object(Body=data.data, Bucket=self.bucket, Key=self.key, Metadata=self.meta)
+            return self.size
+        try:
+            if self.npend:
+                self._flush()
+            for f in self.futs:
+                f.result()
+            self.st.complete_multipart_upload(Bucket=self.bucket, Key=self.key, UploadId=self.uid, MultipartUpload={
+                "Parts": [{"PartNumber": i + 1, "ETag": f.result()["ETag"]} for i, f in enumerate(self.futs)]})
+        except BaseException:
+            self.abort()
+            raise
+        return self.size
+
+    def abort(self) -> None:
+        cf.wait(self.futs)
+        if self.uid is not None:
+            try:
+                self.st.abort_multipart_upload(Bucket=self.bucket, Key=self.key, UploadId=self.uid)
+            except ClientError:
+                pass
+            self.uid = None
+
+
+def store_line_index_stream(cloud_object, pieces, fmt: str, merge) -> dict:
+    """``store_line_index`` for an index produced piece by piece (``scan.objects.line_index_pieces``): the low
+    bytes / words and the 256-byte counts go up as multipart uploads while later pieces are still being fetched and
+    scanned; the block table (8 B per 64 KiB) is PUT at the end.  Stores the same objects and returns the same
+    attributes as ``store_line_index`` of the merged index."""
+    key = cloud_object.meta_path.key + LINES_SUFFIX
+    st, bucket = cloud_object.storage, cloud_object.meta_path.bucket
+    meta = {"dataplug": __version__}
+    skey, bkey = key + ".sub", key + ".blocks"
+    low_w = MultipartWriter(st, bucket, key, meta)
+    sub_w = MultipartWriter(st, bucket, skey, meta) if fmt == "u8s" else None
+    tabs = [merge.head_table()]
+    if sub_w is not None:
+        sub_w.append(merge.head_sub().astype("<u2"))
+    try:
+        for low, tab, sub in pieces:
+            low_w.append(low.astype(np.uint8 if fmt == "u8s" else "<u2", copy=False))
+            if sub_w is not None:
+                sub_w.append(sub.astype("<u2", copy=False))
+            tabs.append(tab)
+        count = low_w.close() // (1 if fmt == "u8s" else 2)
+        if sub_w is not None:
+            sub_w.close()
+    except BaseException:
+        low_w.abort()
+        if sub_w is not None:
+            sub_w.abort()
+        raise
+    st.put_object(Body=np.ascontiguousarray(np.concatenate(tabs), "<u8").data, Bucket=bucket, Key=bkey, Metadata=meta)
+    attrs = {"line_index_key": key, "num_lines": int(count), "line_index_dtype": fmt, "line_index_blocks_key": bkey,
+             "line_index_block0": int(merge.J0)}
+    if fmt == "u8s":
+        attrs.update(line_index_sub_key=skey, line_index_sub0=int(merge.S0))
+    return attrs
+
+
+STREAM_PIECE = 512 << 20           # streamed index: object bytes per scanned piece
+
+
+def index_object(cloud_object, begin: int = 0, index_format: str = "auto", piece_bytes: int = STREAM_PIECE) -> dict:
+    """Build the newline index of object bytes [begin, size) on the GPUs and store it; returns its attributes.
+    ``index_format`` "auto" takes u8s or u16b by the object's newline density (``scan.objects.line_index_form``).
+    A u8s / u16b index of more than one piece is stored as it is produced (``store_line_index_stream``: the PUTs
+    overlap the later pieces' GETs, H2D copies and scans); other forms and single pieces are built, then stored."""
+    from ..scan import objects as so
+    end = cloud_object.size
+    fmt = so.line_index_form(cloud_object, begin, end) if index_format == "auto" else index_format
+    if fmt in ("u8s", "u16b") and end - begin > piece_bytes:
+        merge = so.PieceMerge(begin, end, fmt)
+        pieces = so.line_index_pieces(cloud_object, begin, end, fmt=fmt, piece_bytes=piece_bytes, merge=merge)
+        try:
+            return store_line_index_stream(cloud_object, pieces, fmt, merge)
+        finally:
+            pieces.close()
+    return store_line_index(cloud_object, so.line_index_object(cloud_object, begin=begin, end=end, fmt=fmt))
 
 
 class LineIndex:

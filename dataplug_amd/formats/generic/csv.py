@@ -17,8 +17,7 @@ from typing import TYPE_CHECKING, List, Optional
 
 from ...entities import CloudDataFormat, CloudObjectSlice, PartitioningStrategy
 from ...preprocessing.metadata import PreprocessingMetadata
-from ...scan import objects as scan_objects
-from .._lines import LineIndex, SliceError, csv_body, slice_error, store_line_index
+from .._lines import LineIndex, SliceError, csv_body, index_object, slice_error
 
 if TYPE_CHECKING:
     from ...cloudobject import CloudObject
@@ -37,8 +36,7 @@ def preprocess_csv(cloud_object: "CloudObject", separator: str = ",", line_index
     df = pd.read_csv(io.StringIO("\n".join(top)), sep=separator)
     attrs = {"columns": df.columns.tolist(), "dtypes": df.dtypes.tolist()}
     if line_index:
-        offsets = scan_objects.line_index_object(cloud_object, fmt=index_format)
-        attrs.update(store_line_index(cloud_object, offsets))
+        attrs.update(index_object(cloud_object, 0, index_format))
     return PreprocessingMetadata(attributes=attrs)
 
 

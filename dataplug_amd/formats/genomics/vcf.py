@@ -16,8 +16,7 @@ from typing import TYPE_CHECKING, Dict, List, Optional, Union
 
 from ...entities import CloudDataFormat, CloudObjectSlice, PartitioningStrategy
 from ...preprocessing.metadata import PreprocessingMetadata
-from ...scan import objects as scan_objects
-from .._lines import LineIndex, SliceError, slice_error, store_line_index, vcf_body
+from .._lines import LineIndex, SliceError, index_object, slice_error, vcf_body
 
 if TYPE_CHECKING:
     from ...cloudobject import CloudObject
@@ -65,8 +64,7 @@ def preprocess_vcf(cloud_object: "CloudObject", line_index: bool = True, index_f
         header, meta, columns, body_offset = parse_vcf_header(f)
     attrs = {"columns": columns, "vcf_attributes": meta, "body_offset": body_offset}
     if line_index:
-        offsets = scan_objects.line_index_object(cloud_object, begin=body_offset, fmt=index_format)
-        attrs.update(store_line_index(cloud_object, offsets))
+        attrs.update(index_object(cloud_object, body_offset, index_format))
     return PreprocessingMetadata(attributes=attrs, metadata="\n".join(header).encode("utf-8"))
 
 

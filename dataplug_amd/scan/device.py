@@ -435,6 +435,14 @@ def get_context(device: int = 0) -> ScanContext:
     return c
 
 
+def close_context(device: int = 0) -> None:
+    """Close the calling thread's context for ``device``, if any (its stream, pinned staging and HBM workspace
+    are freed; the next ``get_context`` makes a new one)."""
+    c = getattr(_tls, "ctxs", {}).pop(device, None)
+    if c is not None:
+        c.close()
+
+
 def pick_device(i: int, devices: Optional[Iterable[int]] = None) -> int:
     """Round-robin device for job ``i`` over ``devices`` (default: every visible GPU)."""
     devs = list(devices) if devices is not None else list(range(max(1, device_count())))

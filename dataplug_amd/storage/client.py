@@ -3,7 +3,8 @@
 The indexing path uses this storage surface: ``head_object`` (404 → ``ClientError``
 code ``"404"``), ``head_bucket``, ``create_bucket``, ``get_object(Range="bytes=a-b")`` (inclusive; body
 with ``.read()``; status 200/206), ``put_object``, ``upload_fileobj``, ``upload_file``, ``download_file``,
-``delete_object``.  ``PickleableS3ClientProxy`` takes the reference's ``storage_config`` keywords
+``delete_object``, and the multipart upload calls (``create_multipart_upload``, ``upload_part``,
+``complete_multipart_upload``, ``abort_multipart_upload``) the streamed index PUT uses.  ``PickleableS3ClientProxy`` takes the reference's ``storage_config`` keywords
 (``picklableS3.py:49-84``) and re-creates its client after pickling, like the reference's proxy.
 
 Scope: unsigned requests to S3-compatible endpoints (the loopback server in ``server.py``, MinIO with
@@ -111,7 +112,9 @@ class _ClientBase:
     """boto3 method names and shapes on top of five primitives implemented by the subclasses."""
 
     # primitives: _head(b, k) -> (size, meta, etag, mtime); _get(b, k, rng) -> (body, size, total, meta, status);
-    # _put(b, k, data|file, size, meta); _delete(b, k); _head_bucket(b) -> bool; _create_bucket(b); _list(b, prefix)
+    # _put(b, k, data|file, size, meta); _delete(b, k); _head_bucket(b) -> bool; _create_bucket(b); _list(b, prefix);
+    # multipart: _mp_create(b, k, meta) -> id; _mp_part(b, k, id, n, data, size) -> etag; _mp_complete(b, k, id, [n]);
+    # _mp_abort(b, k, id)
 
     def head_bucket(self, Bucket: str, **_):
         if not self._head_bucket(Bucket):
@@ -139,6 +142,24 @@ class _ClientBase:
         data = _body_bytes(Body)
         self._put(Bucket, Key, data, len(data), dict(Metadata or {}))
         return {"ResponseMetadata": {"HTTPStatusCode": 200}}
+
+    def create_multipart_upload(self, Bucket: str, Key: str, Metadata: Optional[Dict[str, str]] = None, **_):
+        uid = self._mp_create(Bucket, Key, dict(Metadata or {}))
+        return {"Bucket": Bucket, "Key": Key, "UploadId": uid, "ResponseMetadata": {"HTTPStatusCode": 200}}
+
+    def upload_part(self, Bucket: str, Key: str, PartNumber: int, UploadId: str, Body=None, **_):
+        data = _body_bytes(Body)
+        etag = self._mp_part(Bucket, Key, UploadId, int(PartNumber), data, len(data))
+        return {"ETag": etag, "ResponseMetadata": {"HTTPStatusCode": 200}}
+
+    def complete_multipart_upload(self, Bucket: str, Key: str, UploadId: str, MultipartUpload: dict, **_):
+        numbers = [int(p["PartNumber"]) for p in MultipartUpload.get("Parts", [])]
+        self._mp_complete(Bucket, Key, UploadId, numbers)
+        return {"Bucket": Bucket, "Key": Key, "ResponseMetadata": {"HTTPStatusCode": 200}}
+
+    def abort_multipart_upload(self, Bucket: str, Key: str, UploadId: str, **_):
+        self._mp_abort(Bucket, Key, UploadId)
+        return {"ResponseMetadata": {"HTTPStatusCode": 204}}
 
     def delete_object(self, Bucket: str, Key: str, **_):
         self._delete(Bucket, Key)
@@ -204,11 +225,23 @@ class LocalS3Client(_ClientBase):
         o = self.store.get(b, k)
         r = parse_range(rng, len(o.data))
         lo, hi = r if r is not None else (0, len(o.data))
-        return (StreamingBody(memoryview(o.data)[lo:hi], hi - lo), hi - lo, len(o.data), dict(o.metadata),
+        return (StreamingBody(o.view(lo, hi), hi - lo), hi - lo, len(o.data), dict(o.metadata),
                 206 if r is not None else 200, lo)
 
     def _put(self, b, k, data, size, meta):
         self.store.put(b, k, data, meta)
+
+    def _mp_create(self, b, k, meta):
+        return self.store.create_multipart(b, k, meta)
+
+    def _mp_part(self, b, k, uid, n, data, size):
+        return self.store.upload_part(b, k, uid, n, data)
+
+    def _mp_complete(self, b, k, uid, numbers):
+        self.store.complete_multipart(b, k, uid, numbers)
+
+    def _mp_abort(self, b, k, uid):
+        self.store.abort_multipart(b, k, uid)
 
     def _delete(self, b, k):
         self.store.delete(b, k)
@@ -318,6 +351,44 @@ class HTTPS3Client(_ClientBase):
 
     def _delete(self, b, k):
         self._request("DELETE", self._path(b, k), op="DeleteObject")
+
+    def _mp_create(self, b, k, meta):
+        headers = {"Content-Length": "0"}
+        headers.update({f"x-amz-meta-{m}": str(v) for m, v in meta.items()})
+        resp, conn = self._request("POST", self._path(b, k, "uploads"), body=b"", headers=headers,
+                                   op="CreateMultipartUpload", stream=True)
+        payload = resp.read()
+        self._tls.conn = conn
+        root = ET.fromstring(payload)
+        uid = next((e.text for e in root.iter() if e.tag.endswith("UploadId")), None)
+        if not uid:
+            raise ClientError("InternalError", "CreateMultipartUpload", "no UploadId in the response", 500)
+        return uid
+
+    def _mp_part(self, b, k, uid, n, data, size):
+        q = urllib.parse.urlencode({"partNumber": str(n), "uploadId": uid})
+        resp, _ = self._request("PUT", self._path(b, k, q), body=data,
+                                headers={"Content-Length": str(size), "Content-Type": "binary/octet-stream"},
+                                op="UploadPart")
+        return resp.getheader("ETag", "")
+
+    def _mp_complete(self, b, k, uid, numbers):
+        body = ("<CompleteMultipartUpload>" + "".join(f"<Part><PartNumber>{n}</PartNumber></Part>" for n in numbers)
+                + "</CompleteMultipartUpload>").encode()
+        q = urllib.parse.urlencode({"uploadId": uid})
+        resp, conn = self._request("POST", self._path(b, k, q), body=body,
+                                   headers={"Content-Length": str(len(body)), "Content-Type": "application/xml"},
+                                   op="CompleteMultipartUpload", stream=True)
+        payload = resp.read()
+        self._tls.conn = conn
+        if b"<Error>" in payload:                 # S3 may answer 200 with an error document
+            root = ET.fromstring(payload)
+            raise ClientError(root.findtext("Code") or "InternalError", "CompleteMultipartUpload",
+                              root.findtext("Message") or "", 500)
+
+    def _mp_abort(self, b, k, uid):
+        self._request("DELETE", self._path(b, k, urllib.parse.urlencode({"uploadId": uid})),
+                      op="AbortMultipartUpload")
 
     def _list(self, b, prefix):
         q = urllib.parse.urlencode({"list-type": "2", "prefix": prefix})

@@ -1,33 +1,93 @@
 """In-memory object store: the backing of the loopback S3 server and of ``memory://`` clients.
 
-Objects are immutable ``bytes``; a ranged read hands out a zero-copy ``memoryview`` slice.  Named stores
+Objects are immutable byte buffers; a ranged read hands out a zero-copy ``memoryview`` slice.  An object made by a
+multipart upload keeps its parts as they were uploaded (``Segments``: no concatenation copy at completion); a
+ranged read inside one part is a view of it, one across parts a copy of the range.  Named stores
 (``MemoryStore.named("x")``) are process-global so that ``memory://x`` clients created independently
 (``CloudObject.open`` deep-copies its client, cloudobject.py:93-97) see the same objects.
 """
 from __future__ import annotations
 
+import bisect
 import hashlib
+import itertools
 import threading
 import time
 from dataclasses import dataclass, field
-from typing import Dict, Iterator, Optional, Tuple
+from typing import Dict, Iterator, List, Optional, Tuple
 
 from .errors import ClientError
 
 
+class Segments:
+    """An object's bytes as the consecutive buffers of its multipart upload (read only)."""
+
+    def __init__(self, parts: List):
+        self.parts = [memoryview(p).cast("B") for p in parts if len(p)]
+        self.starts = [0] + list(itertools.accumulate(len(p) for p in self.parts))
+
+    def __len__(self) -> int:
+        return self.starts[-1]
+
+    def view(self, lo: int, hi: int):
+        """Bytes [lo, hi): a view when they lie in one part, else a copy."""
+        if hi <= lo:
+            return memoryview(b"")
+        i = bisect.bisect_right(self.starts, lo) - 1
+        if hi <= self.starts[i + 1]:
+            return self.parts[i][lo - self.starts[i]:hi - self.starts[i]]
+        out = bytearray(hi - lo)
+        p = lo
+        while p < hi:
+            q = min(hi, self.starts[i + 1])
+            out[p - lo:q - lo] = self.parts[i][p - self.starts[i]:q - self.starts[i]]
+            p, i = q, i + 1
+        return memoryview(out)
+
+    def views(self, lo: int, hi: int, block: int):
+        """Views covering [lo, hi) in order, none longer than ``block`` (no copy)."""
+        i = bisect.bisect_right(self.starts, lo) - 1 if hi > lo else len(self.parts)
+        p = lo
+        while p < hi:
+            q = min(hi, self.starts[i + 1], p + block)
+            yield self.parts[i][p - self.starts[i]:q - self.starts[i]]
+            p = q
+            if p == self.starts[i + 1]:
+                i += 1
+
+    def __bytes__(self) -> bytes:
+        return b"".join(self.parts)
+
+
 @dataclass
 class StoredObject:
-    data: bytes
+    data: object                  # bytes / bytearray, or Segments (a multipart upload's parts)
     metadata: Dict[str, str] = field(default_factory=dict)
     last_modified: float = field(default_factory=time.time)
     _etag: Optional[str] = None
+
+    def view(self, lo: int, hi: int):
+        """Bytes [lo, hi) of the object (a zero-copy view unless they span two multipart parts)."""
+        if isinstance(self.data, Segments):
+            return self.data.view(lo, hi)
+        return memoryview(self.data)[lo:hi]
+
+    def views(self, lo: int, hi: int, block: int):
+        if isinstance(self.data, Segments):
+            yield from self.data.views(lo, hi, block)
+            return
+        v = memoryview(self.data)
+        for p in range(lo, hi, block):
+            yield v[p:min(hi, p + block)]
 
     @property
     def etag(self) -> str:
         if self._etag is None:
             # md5 of a multi-GiB body is slow; a size/time tag is enough for change detection here
-            h = hashlib.md5(self.data[:1 << 20]).hexdigest() if len(self.data) <= 1 << 20 else \
+            h = hashlib.md5(bytes(self.view(0, len(self.data)))).hexdigest() if len(self.data) <= 1 << 20 else \
                 f"{len(self.data):x}-{int(self.last_modified * 1e6):x}"
+            if isinstance(self.data, Segments):
+                h += f"-{len(self.data.parts)}"           # as S3 marks a multipart object's ETag
             self._etag = f'"{h}"'
         return self._etag
 
@@ -60,6 +120,8 @@ class MemoryStore:
     def __init__(self):
         self._lock = threading.RLock()
         self._buckets: Dict[str, Dict[str, StoredObject]] = {}
+        self._uploads: Dict[str, Tuple[str, str, Dict[str, str], Dict[int, object]]] = {}
+        self._upload_ids = itertools.count(1)
 
     @classmethod
     def named(cls, name: str) -> "MemoryStore":
@@ -107,6 +169,49 @@ class MemoryStore:
         with self._lock:
             self._bucket(bucket, "PutObject")[key] = obj
         return obj
+
+    # ---------------------------------------------------------------- multipart uploads (S3 semantics)
+    MIN_PART = 5 << 20                            # S3's minimum size of every part but the last
+
+    def create_multipart(self, bucket: str, key: str, metadata: Optional[Dict[str, str]] = None) -> str:
+        with self._lock:
+            self._bucket(bucket, "CreateMultipartUpload")
+            uid = f"mpu-{next(self._upload_ids):08d}"
+            self._uploads[uid] = (bucket, key, dict(metadata or {}), {})
+        return uid
+
+    def _upload(self, bucket: str, key: str, uid: str, op: str):
+        u = self._uploads.get(uid)
+        if u is None or u[0] != bucket or u[1] != key:
+            raise ClientError("NoSuchUpload", op, f"{bucket}/{key} upload {uid}", 404)
+        return u
+
+    def upload_part(self, bucket: str, key: str, uid: str, number: int, data, owned: bool = False) -> str:
+        """Store part ``number`` (1..10000) of an upload, a copy of ``data`` unless ``owned``; returns its ETag."""
+        if not 1 <= int(number) <= 10000:
+            raise ClientError("InvalidArgument", "UploadPart", f"part number {number}", 400)
+        keep = data if owned and isinstance(data, (bytes, bytearray)) else bytes(data)
+        with self._lock:
+            self._upload(bucket, key, uid, "UploadPart")[3][int(number)] = keep
+        return f'"{hashlib.md5(keep[:1 << 16]).hexdigest()}-{len(keep):x}"'
+
+    def complete_multipart(self, bucket: str, key: str, uid: str, numbers: List[int]) -> StoredObject:
+        """The object made of the listed parts in ascending order (every one but the last >= MIN_PART)."""
+        with self._lock:
+            _, _, meta, parts = self._upload(bucket, key, uid, "CompleteMultipartUpload")
+            if not numbers or list(numbers) != sorted(set(numbers)) or any(n not in parts for n in numbers):
+                raise ClientError("InvalidPart", "CompleteMultipartUpload", f"parts {list(numbers)[:8]}", 400)
+            if any(len(parts[n]) < self.MIN_PART for n in numbers[:-1]):
+                raise ClientError("EntityTooSmall", "CompleteMultipartUpload", "a part below 5 MiB", 400)
+            obj = StoredObject(Segments([parts[n] for n in numbers]), meta)
+            self._bucket(bucket, "CompleteMultipartUpload")[key] = obj
+            del self._uploads[uid]
+        return obj
+
+    def abort_multipart(self, bucket: str, key: str, uid: str) -> None:
+        with self._lock:
+            self._upload(bucket, key, uid, "AbortMultipartUpload")
+            del self._uploads[uid]
 
     def get(self, bucket: str, key: str, op: str = "GetObject") -> StoredObject:
         with self._lock:

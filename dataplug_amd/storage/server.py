@@ -2,7 +2,8 @@
 
 Stands in for the MinIO the reference's examples talk to (``examples/fasta_example.py:15-18``, endpoint
 ``http://127.0.0.1:9000``).  Path-style REST subset: HEAD/PUT bucket, HEAD/GET (``Range``)/PUT/DELETE
-object, ListObjectsV2, ListBuckets; user metadata as ``x-amz-meta-*``.  Unsigned.
+object, multipart uploads (POST ``?uploads``, PUT ``?partNumber&uploadId``, POST / DELETE ``?uploadId``),
+ListObjectsV2, ListBuckets; user metadata as ``x-amz-meta-*``.  Unsigned.
 
     python -m dataplug_amd.storage.server --port 9000 [--put bucket/key=path ...] [--synth bucket/key=kind,size,seed ...]
 
@@ -15,6 +16,7 @@ from __future__ import annotations
 import argparse
 import threading
 import urllib.parse
+import xml.etree.ElementTree as ET
 from email.utils import formatdate
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Optional
@@ -42,7 +44,7 @@ class _Handler(BaseHTTPRequestHandler):
         parts = u.path.lstrip("/").split("/", 1)
         bucket = urllib.parse.unquote(parts[0]) if parts[0] else None
         key = urllib.parse.unquote(parts[1]) if len(parts) > 1 and parts[1] != "" else None
-        return bucket, key, urllib.parse.parse_qs(u.query)
+        return bucket, key, urllib.parse.parse_qs(u.query, keep_blank_values=True)
 
     def _send(self, status: int, body: bytes = b"", headers: Optional[dict] = None, head_only: bool = False):
         self.send_response(status)
@@ -123,18 +125,21 @@ class _Handler(BaseHTTPRequestHandler):
             for m, v in o.metadata.items():
                 self.send_header(f"x-amz-meta-{m}", v)
             self.end_headers()
-            view = memoryview(o.data)
-            for p in range(lo, hi, _WRITE_BLOCK):
-                self.wfile.write(view[p:min(hi, p + _WRITE_BLOCK)])
+            for v in o.views(lo, hi, _WRITE_BLOCK):
+                self.wfile.write(v)
         except ClientError as e:
             self._error(e)
         except (BrokenPipeError, ConnectionResetError):
             self.close_connection = True
 
     def do_PUT(self):
-        b, k, _ = self._split()
+        b, k, q = self._split()
         try:
             body = self._read_body()
+            if k is not None and "uploadId" in q:
+                etag = self.store.upload_part(b, k, q["uploadId"][0], int(q.get("partNumber", ["0"])[0]), body,
+                                              owned=True)
+                return self._send(200, headers={"ETag": etag})
             if k is None:
                 self.store.create_bucket(b)
                 return self._send(200, headers={"Location": f"/{b}"})
@@ -145,9 +150,36 @@ class _Handler(BaseHTTPRequestHandler):
         except ClientError as e:
             self._error(e)
 
-    def do_DELETE(self):
-        b, k, _ = self._split()
+    def do_POST(self):
+        b, k, q = self._split()
         try:
+            body = self._read_body()
+            if k is None:
+                raise ClientError("NotImplemented", "Post", "POST on a bucket", 501)
+            if "uploads" in q:
+                meta = {h[len("x-amz-meta-"):].lower(): v for h, v in self.headers.items()
+                        if h.lower().startswith("x-amz-meta-")}
+                uid = self.store.create_multipart(b, k, meta)
+                return self._send(200, (f"<InitiateMultipartUploadResult><Bucket>{escape(b)}</Bucket><Key>{escape(k)}"
+                                        f"</Key><UploadId>{uid}</UploadId></InitiateMultipartUploadResult>").encode(),
+                                  {"Content-Type": "application/xml"})
+            if "uploadId" in q:
+                root = ET.fromstring(bytes(body))
+                numbers = [int(e.text) for e in root.iter() if e.tag.endswith("PartNumber")]
+                o = self.store.complete_multipart(b, k, q["uploadId"][0], numbers)
+                return self._send(200, (f"<CompleteMultipartUploadResult><Bucket>{escape(b)}</Bucket><Key>{escape(k)}"
+                                        f"</Key><ETag>{escape(o.etag)}</ETag></CompleteMultipartUploadResult>").encode(),
+                                  {"Content-Type": "application/xml"})
+            raise ClientError("NotImplemented", "Post", self.path, 501)
+        except ClientError as e:
+            self._error(e)
+
+    def do_DELETE(self):
+        b, k, q = self._split()
+        try:
+            if k is not None and "uploadId" in q:
+                self.store.abort_multipart(b, k, q["uploadId"][0])
+                return self._send(204)
             if k is None:
                 self.store.delete_bucket(b)
             else:

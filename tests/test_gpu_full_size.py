@@ -180,3 +180,49 @@ def test_vcf_64gib_configs3_eight_parts():
     with cf.ThreadPoolExecutor(4) as ex:            # 4 in flight: bounds host staging at 16 GiB
         counts = list(ex.map(run, range(8)))
     assert sum(counts) == obj.count_range(len(obj.head), size) > 800_000_000
+
+
+class _SynthStore:
+    """A read-only storage client over a ``synth.TiledText`` (ranged GETs generate the bytes): the product's
+    storage -> pinned -> HBM path without holding the object in host memory."""
+
+    def __init__(self, obj):
+        self.obj = obj
+
+    def get_object(self, Bucket, Key, Range=None):
+        import io
+        a, b = (int(x) for x in Range.split("=")[1].split("-"))
+        return {"Body": io.BytesIO(self.obj.bytes_range(a, min(b + 1, self.obj.size)).tobytes())}
+
+
+def test_vcf_64gib_configs3_stored_u8s_through_product(monkeypatch):
+    """verdict r5 #3: configs[3] through the product path in the stored form: ``line_index_object(fmt="u8s")``
+    fetches the 64 GiB VCF body by ranged GETs into pinned memory and HBM, cuts it into 8 parts (four device entries,
+    two parts each, as eight GPUs would take one each), scans each in out_mode 4 and merges the parts' low bytes,
+    256-byte counts and block tables; every one of the ~859 M offsets decoded from the merged tables equals the
+    object's analytic newline positions."""
+    from types import SimpleNamespace
+    from dataplug_amd.scan.objects import ByteOffsets, line_index_object, line_parts, release_workers, sub_counts
+    size = 64 * GiB
+    obj = synth.tiled_vcf(size, seed=9)
+    begin = len(obj.head)
+    monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0,0,0")
+    assert len(line_parts(begin, size, 4, part_bytes=8 * GiB)) == 8
+    co = SimpleNamespace(storage=_SynthStore(obj), path=SimpleNamespace(bucket="b", key="k.vcf"), size=size)
+    try:
+        bo = line_index_object(co, begin=begin, fmt="u8s", part_bytes=8 * GiB)
+    finally:
+        release_workers()                         # the four workers' 8 GiB pinned stages and HBM inputs
+    assert isinstance(bo, ByteOffsets) and bo.s0 == begin >> 8 and bo.j0 == begin >> 16
+    n_exp = obj.count_range(begin, size)
+    assert len(bo) == n_exp > 800_000_000
+    c = sub_counts(bo.sub, bo.table, bo.s0, bo.j0)
+    assert c[0] == 0 and (np.diff(c) >= 0).all() and c[-1] <= n_exp
+    unit = np.repeat(np.arange(len(c), dtype=np.uint32), np.diff(np.append(c, np.uint64(n_exp))).astype(np.int64))
+    del c
+    i = 0
+    for piece in obj.delims_range(begin, size):
+        u = unit[i:i + len(piece)].astype(np.uint64) + np.uint64(bo.s0)
+        assert np.array_equal((u << np.uint64(8)) | bo.low[i:i + len(piece)].astype(np.uint64), piece), i
+        i += len(piece)
+    assert i == n_exp
