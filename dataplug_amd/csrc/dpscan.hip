@@ -1733,8 +1733,54 @@ struct PlaceArgs {
   const uint16_t* spill;
   uint64_t nranges, nblocks;
   int count_only;              // no output buffer: counts, chunk ends and pending only
+  int in_order;                // blocks by blockIdx (nblocks <= kLbSlots), else claimed from the ticket
   unsigned int* map_ticket;    // the map kernel's group ticket, zeroed here for the next launch
 };
+
+// (in-order placement) look-back polls before the unpublished AGGs of a window are recomputed from the records
+constexpr uint32_t kPlacePolls = 4;
+// The AGG descriptor of placement block p from its range records (one wave: 16 consecutive records per lane,
+// composed in order, then the wave's inclusive scan), as the block itself publishes it.
+__device__ __forceinline__ uint64_t block_agg_from_records(const PlaceArgs& PA, const ScanArgs& A, uint32_t p, int lane) {
+  constexpr uint32_t kPer = kPlaceBlock / kWave;
+  const uint64_t r0 = (uint64_t)p * kPlaceBlock + (uint64_t)lane * kPer;
+  uint4 rc[kPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) rc[i] = r0 + i < PA.nranges ? PA.rec[r0 + i] : uint4{0u, 0u, 2u, 0u};
+  Func32 f{0u, 0u, 0u, 1u};
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i)
+    f = f32_then(f, Func32{rc[i].x & 0xFFFFu, rc[i].x >> 16, rc[i].z & 1u, (rc[i].z >> 1) & 1u});
+  const Func32 w = f32_wave_scan(f);
+  const Func agg{(uint32_t)__builtin_amdgcn_readlane((int)w.cF, kWave - 1), (uint32_t)__builtin_amdgcn_readlane((int)w.cT, kWave - 1),
+                 (uint32_t)__builtin_amdgcn_readlane((int)w.sF, kWave - 1) & 1u,
+                 (uint32_t)__builtin_amdgcn_readlane((int)w.sT, kWave - 1) & 1u};
+  return pack_agg(agg) | A.epoch;
+}
+
+// Every slot of a loaded look-back window of block b whose descriptor is unpublished gets that block's AGG,
+// recomputed from its records (one block at a time, the whole wave).
+__device__ __forceinline__ void lb_fill_from_records(const PlaceArgs& PA, const ScanArgs& A, uint32_t b, uint32_t W,
+                                                     int lane, uint64_t (&d)[kLbPer]) {
+  const uint32_t rl = (uint32_t)(kWave - 1 - lane);
+  for (;;) {
+    uint32_t mine = kLbPer;
+#pragma unroll
+    for (int j = kLbPer - 1; j >= 0; --j) {
+      const uint32_t k = kLbPer * rl + (uint32_t)j;
+      if (k < W && (d[j] & kStatMask) == 0ull) mine = (uint32_t)j;
+    }
+    const uint64_t bal = __ballot(mine < kLbPer);
+    if (bal == 0ull) return;
+    const int L = 63 - __builtin_clzll(bal);
+    const uint32_t j = (uint32_t)__builtin_amdgcn_readlane((int)mine, L);
+    const uint32_t k = kLbPer * (uint32_t)(kWave - 1 - L) + j;
+    const uint64_t agg = block_agg_from_records(PA, A, b - 1u - k, lane);
+#pragma unroll
+    for (int jj = 0; jj < kLbPer; ++jj)
+      if (lane == L && (uint32_t)jj == j) d[jj] = agg;
+  }
+}
 
 // LDS of one placement block
 struct PlaceShared {
@@ -1832,6 +1878,13 @@ __device__ __forceinline__ void fasta_place_block(const PlaceArgs& PA, const Sca
         uint64_t d[kLbPer];
         lb_load(A, b, W, lane, d);
         if (lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S)) break;
+        if (PA.in_order && spins >= kPlacePolls) {
+          // (blocks by blockIdx) never wait on a block that may not be running: the AGG of every predecessor
+          // still unpublished is recomputed from its records, and the window (which reaches the base: b <
+          // kLbSlots) then resolves
+          lb_fill_from_records(PA, A, b, W, lane, d);
+          if (lb_reduce(d, W, pack_prefix(0ull, 0u), lane, P, S)) break;
+        }
         if (wait_expired(spins, t0)) {
           if (lane == 0) atomicOr(A.err, kErrTimeout);
           break;
@@ -1998,8 +2051,12 @@ __global__ void __launch_bounds__(kPlaceBlock) fasta_place_kernel(PlaceArgs PA, 
   __shared__ PlaceShared ps;
   if (threadIdx.x == 0) {
     if (blockIdx.x == 0) PA.map_ticket[0] = 0u;       // the map kernel is done with it: ready for the next launch
-    ps.blk = atomicAdd(&A.ticket[0], 1u);            // claim order: a block only waits on lower,
-  }                                                   // already running or finished, blocks
+    // in order (at most kLbSlots blocks): block = blockIdx, no claim (the claims' atomics serialized ~3 us of
+    // block starts at 256 blocks); its look-back never waits on a predecessor that is not running (it
+    // recomputes such an AGG from the records).  Larger launches claim in order from the ticket: a block only
+    // waits on lower, already running or finished, blocks.
+    ps.blk = PA.in_order ? blockIdx.x : atomicAdd(&A.ticket[0], 1u);
+  }
   __syncthreads();
   const Tab T{(cu64*)tab_lo, (cu64*)tab_hi, (cu64*)tab_r0};
   fasta_place_block<OUT64>(PA, A, T, ps.blk, ps);
@@ -3131,6 +3188,7 @@ int enq_fasta2(dp_ctx* c, hipStream_t ss, int out_u64, const ScanArgs& a, uint64
   pa.nranges = nranges;
   pa.nblocks = nblocks;
   pa.count_only = count_only;
+  pa.in_order = nblocks <= kLbSlots;                 // every window then reaches the base (b < kLbSlots)
   const uint64_t* tlo = c->d_tab;
   const uint64_t* thi = c->d_tab + n;
   const uint64_t* tr0 = c->d_tab + 2 * n;

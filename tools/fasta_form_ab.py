@@ -3,6 +3,7 @@ same chunk plan, launches alternated rep by rep (HIP events on the scan stream),
 the first form's and, once, with the C oracle.  Same buffers for every form (DESIGN.md §5's placement effect alike).
 
     python tools/fasta_form_ab.py [--forms 0,2] [--sizes-gib 4,0.5] [--reps 10] [--chunks 4]
+    python tools/fasta_form_ab.py --lib-b dataplug_amd/lib/libdpscan_v_X.so   # form0: the shipped library, form1: X
 """
 from __future__ import annotations
 
@@ -28,13 +29,21 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--chunks", type=int, default=4)
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--lib-b", default=None, help="A/B of two builds (default form each): form0 = the shipped "
+                    "library, form1 = this one")
     args = ap.parse_args()
-    forms = [int(x) for x in args.forms.split(",")]
     ctxs = {}
-    for f in forms:
-        c = ScanContext(0)
-        c.set_form(fasta=f)
-        ctxs[f] = c
+    if args.lib_b:
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from lib_ab import context_on
+        forms = [0, 1]
+        ctxs = {0: ScanContext(0), 1: context_on(args.lib_b)}
+    else:
+        forms = [int(x) for x in args.forms.split(",")]
+        for f in forms:
+            c = ScanContext(0)
+            c.set_form(fasta=f)
+            ctxs[f] = c
     c0 = ctxs[forms[0]]
     for size in (int(float(x) * (1 << 30)) for x in args.sizes_gib.split(",")):
         host = synth.tiled_fasta_host(size, seed=1)

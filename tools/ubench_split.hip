@@ -41,15 +41,20 @@ __host__ __device__ __forceinline__ uint64_t e_of(uint64_t r, uint64_t wq16) { r
 // W loading waves per group; STORE: 0 none, 1 loading waves store, 2 wave 15 stores; SWAP: a wave reads its
 // range's second half first when (group ^ wave) is odd; NOBAR: no barrier per step (read only: free-running waves)
 // BURST: the runs of BURST consecutive steps stored together, after every BURST-th step (and the last)
-template <int W, int STORE, bool SWAP = false, bool NOBAR = false, int BURST = 1>
+// SEQ: workgroup b takes groups [b K, (b + 1) K) in order (each CU walks its own contiguous region: 256 regions
+// in flight across the buffer) instead of b, b + grid, ... (the grid walks one 64 MiB window)
+template <int W, int STORE, bool SWAP = false, bool NOBAR = false, int BURST = 1, bool SEQ = false>
 __global__ void __launch_bounds__(1024) split_kernel(const uint4* __restrict__ in, uint64_t nranges,
                                                      uint4* __restrict__ out, uint64_t wq16, unsigned* sink) {
   __shared__ uint32_t s_x[2][16];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const bool loader = wave < W;
-  const uint64_t ngroups = (nranges + W - 1) / W;
-  uint64_t g = blockIdx.x;
+  const uint64_t ngroups_all = (nranges + W - 1) / W;
+  const uint64_t K = (ngroups_all + gridDim.x - 1) / gridDim.x;
+  const uint64_t gstep = SEQ ? 1 : gridDim.x;
+  const uint64_t ngroups = SEQ ? ((blockIdx.x + 1) * K < ngroups_all ? (blockIdx.x + 1) * K : ngroups_all) : ngroups_all;
+  uint64_t g = SEQ ? blockIdx.x * K : blockIdx.x;
   if (g >= ngroups) return;
   uint32_t acc = 0;
   uint4 a[kHalf], b[kHalf];
@@ -70,7 +75,7 @@ __global__ void __launch_bounds__(1024) split_kernel(const uint4* __restrict__ i
     for (int i = 0; i < kHalf; ++i) b[i] = ld(p + other(g) + i * 64);
   }
   for (uint32_t k = 0;; ++k) {
-    const uint64_t gn = g + gridDim.x;
+    const uint64_t gn = g + gstep;
     const uint32_t par = k & 1u;
     if (loader) {
       const uint64_t gq = gn < ngroups ? gn : g;
@@ -91,8 +96,8 @@ __global__ void __launch_bounds__(1024) split_kernel(const uint4* __restrict__ i
     const bool flush = BURST == 1 || k % BURST == BURST - 1 || gn >= ngroups;
     for (int j = 0; flush && j < BURST; ++j) {
       const uint64_t back = (uint64_t)(BURST == 1 ? 0 : (gn >= ngroups ? k % BURST : BURST - 1) - j);
-      if ((int64_t)back < 0 || back * gridDim.x > g) continue;
-      const uint64_t gg = g - back * gridDim.x;
+      if ((int64_t)back < 0 || back * gstep > g) continue;
+      const uint64_t gg = g - back * gstep;
       const uint64_t r0 = gg * W, r1 = r0 + W < nranges ? r0 + W : nranges;
       const uint64_t e0 = e_of(r0, wq16), e1 = e_of(r1, wq16);
       if (STORE == 1 && loader) {
@@ -229,6 +234,8 @@ int main(int argc, char** argv) {
                          {"rw16b8", split_kernel<16, 1, false, false, 8>, true},
                          {"rw16b16", split_kernel<16, 1, false, false, 16>, true},
                          {"sw15b4", split_kernel<15, 2, false, false, 4>, true},
+                         {"r16seq", split_kernel<16, 0, false, false, 1, true>, false},
+                         {"rw16seq", split_kernel<16, 1, false, false, 1, true>, true},
                          // buffer loads by cache policy (n: nt, p: plain, s1: sc1, s01: sc0 sc1, s01n: sc0 sc1 nt),
                          // stores non-temporal (n) or plain (p); "r" read only
                          {"rbn", pol_kernel<2, 1>, false},   {"rbp", pol_kernel<0, 1>, false},
