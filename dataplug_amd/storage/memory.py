@@ -16,7 +16,27 @@ import time
 from dataclasses import dataclass, field
 from typing import Dict, Iterator, List, Optional, Tuple
 
+import numpy as np
+
 from .errors import ClientError
+
+_GIL_FREE_COPY = 1 << 20
+
+
+def _own_copy(data):
+    """A private copy of a PUT body: ``bytes`` when small; above 1 MiB a numpy buffer filled by ``np.copyto``, which
+    copies without holding the GIL (``bytes(view)`` holds it for the whole copy, stalling every other Python thread
+    of the process -- the GET threads of a streamed index build among them)."""
+    try:
+        view = memoryview(data).cast("B")
+    except TypeError:
+        return bytes(data)
+    if len(view) < _GIL_FREE_COPY:
+        return bytes(view)
+    src = np.frombuffer(view, np.uint8)
+    out = np.empty(len(src), np.uint8)
+    np.copyto(out, src)
+    return out
 
 
 class Segments:
@@ -61,7 +81,7 @@ class Segments:
 
 @dataclass
 class StoredObject:
-    data: object                  # bytes / bytearray, or Segments (a multipart upload's parts)
+    data: object                  # bytes / bytearray / uint8 array, or Segments (a multipart upload's parts)
     metadata: Dict[str, str] = field(default_factory=dict)
     last_modified: float = field(default_factory=time.time)
     _etag: Optional[str] = None
@@ -164,7 +184,7 @@ class MemoryStore:
             owned: bool = False) -> StoredObject:
         """Store a copy of ``data``; ``owned``: a bytes / bytearray the caller hands over (kept as it is, never
         written again: the loopback server's request bodies)."""
-        keep = data if owned and isinstance(data, (bytes, bytearray)) else bytes(data)
+        keep = data if owned and isinstance(data, (bytes, bytearray)) else _own_copy(data)
         obj = StoredObject(keep, dict(metadata or {}))
         with self._lock:
             self._bucket(bucket, "PutObject")[key] = obj
@@ -190,10 +210,10 @@ class MemoryStore:
         """Store part ``number`` (1..10000) of an upload, a copy of ``data`` unless ``owned``; returns its ETag."""
         if not 1 <= int(number) <= 10000:
             raise ClientError("InvalidArgument", "UploadPart", f"part number {number}", 400)
-        keep = data if owned and isinstance(data, (bytes, bytearray)) else bytes(data)
+        keep = data if owned and isinstance(data, (bytes, bytearray)) else _own_copy(data)
         with self._lock:
             self._upload(bucket, key, uid, "UploadPart")[3][int(number)] = keep
-        return f'"{hashlib.md5(keep[:1 << 16]).hexdigest()}-{len(keep):x}"'
+        return f'"{hashlib.md5(memoryview(keep)[:1 << 16]).hexdigest()}-{len(keep):x}"'
 
     def complete_multipart(self, bucket: str, key: str, uid: str, numbers: List[int]) -> StoredObject:
         """The object made of the listed parts in ascending order (every one but the last >= MIN_PART)."""

@@ -189,12 +189,18 @@ class _Handler(BaseHTTPRequestHandler):
             self._error(e)
 
 
+class _Server(ThreadingHTTPServer):
+    # the listen backlog: socketserver's default of 5 drops the SYNs of a burst of parallel ranged GETs (two
+    # workers x 16 GET threads per GPU), and each dropped one costs the client a 1 s retransmit
+    request_queue_size = 1024
+
+
 class LoopbackS3Server:
     """``with LoopbackS3Server() as srv: ... srv.endpoint_url``; serves in a daemon thread."""
 
     def __init__(self, store: Optional[MemoryStore] = None, host: str = "127.0.0.1", port: int = 0):
         self.store = store if store is not None else MemoryStore()
-        self._httpd = ThreadingHTTPServer((host, port), _Handler)
+        self._httpd = _Server((host, port), _Handler)
         self._httpd.daemon_threads = True
         self._httpd.store = self.store
         self._thread: Optional[threading.Thread] = None

@@ -215,7 +215,7 @@ def test_streamed_index_equals_stored_index(client, monkeypatch, fmt):
     """verdict r5 #4: the index stored piece by piece while later pieces are scanned (multipart low bytes and
     256-byte counts, the block table at the end) is byte-identical to the merged index stored at once, and
     LineIndex reads every offset back.  Each piece's GPU scan replaced by what the kernel returns for it (host logic
-    only: the piece split, its two workers per device entry, the ordered merge and the uploads)."""
+    only: the piece split over the device entries' workers, the ordered merge and the uploads)."""
     import numpy as np
     from types import SimpleNamespace
     from test_partition_golden import byte_offsets
@@ -236,7 +236,11 @@ def test_streamed_index_equals_stored_index(client, monkeypatch, fmt):
         if lo & 0xFFFF:
             tab[0] = 0
         return (sel & np.uint64(0xFFFF)).astype(np.uint16), tab
+    def fake_run(dev, co, jobs, delim, fmt_, stop):
+        for lo, hi, fut in jobs:                       # in order, as the device worker runs them
+            fut.set_result(fake_group(dev, co, lo, hi, delim, 1, 0, fmt=fmt_))
     monkeypatch.setattr(objects, "_delim_group", fake_group)
+    monkeypatch.setattr(objects, "_delim_piece_run", fake_run)
     monkeypatch.setattr(_lines, "PART_MIN", 5 << 20)
     monkeypatch.setenv("DATAPLUG_AMD_DEVICES", "0,0")
     client.create_bucket(Bucket="ds")

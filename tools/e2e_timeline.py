@@ -1,0 +1,102 @@
+"""Timeline of one CSV ``co.preprocess()`` through the streamed index store: per piece, when its worker started and
+finished (GETs + H2D + scan + D2H), when the consumer took it; per multipart part, when its upload started and
+ended (ms from the call's start).  Memory store and/or the loopback HTTP server in a child process.
+
+    python tools/e2e_timeline.py [--gib 4] [--src memory,http] [--piece-mib 512]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gib", type=float, default=4)
+    ap.add_argument("--src", default="memory,http")
+    ap.add_argument("--piece-mib", type=int, default=512)
+    args = ap.parse_args()
+    from dataplug_amd import synth
+    from dataplug_amd.cloudobject import CloudObject
+    from dataplug_amd.formats import _lines
+    from dataplug_amd.formats.generic.csv import CSV
+    from dataplug_amd.scan import objects
+    from dataplug_amd.storage import MemoryStore
+    size = int(args.gib * (1 << 30))
+    _lines.index_object.__defaults__ = (0, "auto", args.piece_mib << 20)
+    ev = []
+    t0 = [0.0]
+    lock = threading.Lock()
+
+    def mark(what, **kw):
+        with lock:
+            ev.append(dict(t_ms=round((time.perf_counter() - t0[0]) * 1e3, 2), what=what,
+                           thread=threading.current_thread().name, **kw))
+    real_group = objects._delim_group
+
+    def group(dev, co, lo, hi, *a, **kw):
+        mark("piece_start", lo=lo)
+        r = real_group(dev, co, lo, hi, *a, **kw)
+        mark("piece_end", lo=lo)
+        return r
+    objects._delim_group = group
+    real_flush, real_close = _lines.MultipartWriter._flush, _lines.MultipartWriter.close
+
+    def flush(self):
+        mark("part_submit", key=self.key[-10:], n=len(self.futs) + 1, bytes=self.npend)
+        real_flush(self)
+        f = self.futs[-1]
+        n = len(self.futs)
+        f.add_done_callback(lambda _f, n=n, k=self.key[-10:]: mark("part_done", key=k, n=n))
+
+    def close(self):
+        mark("close_start", key=self.key[-10:])
+        r = real_close(self)
+        mark("close_end", key=self.key[-10:])
+        return r
+    _lines.MultipartWriter._flush, _lines.MultipartWriter.close = flush, close
+    real_pieces = objects.line_index_pieces
+
+    def pieces(*a, **kw):
+        for p in real_pieces(*a, **kw):
+            mark("consume", n=len(p[0]))
+            yield p
+    objects.line_index_pieces = pieces
+    bucket = "data"
+    store = MemoryStore.named("e2e_tl")
+    for b in (bucket, bucket + ".meta"):
+        store.create_bucket(b)
+    store.put(bucket, "x", synth.tiled_csv(size, seed=9).bytes_range(0, size))
+    for src in args.src.split(","):
+        cfg = {"endpoint_url": "memory://e2e_tl"}
+        srv = None
+        if src == "http":
+            from e2e_legs import _Server
+            srv = _Server(19074, [(f"{bucket}/x", "csv", size, 9)], [bucket + ".meta"])
+            srv.wait_ready()
+            cfg = {"endpoint_url": srv.url}
+        co = CloudObject.from_s3(CSV, f"s3://{bucket}/x", s3_config=cfg)
+        for i in range(3):
+            ev.clear()
+            t0[0] = time.perf_counter()
+            mark("call_start")
+            co.preprocess(force=True)
+            mark("call_end")
+            dt = ev[-1]["t_ms"]
+            print(json.dumps({"src": src, "call": i, "ms": dt, "GiB_per_s": round(size / (dt / 1e3) / (1 << 30), 2)}),
+                  flush=True)
+        for e in ev:
+            print(json.dumps(e))
+        if srv is not None:
+            srv.stop()
+
+
+if __name__ == "__main__":
+    main()
