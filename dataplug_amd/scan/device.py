@@ -424,23 +424,26 @@ def device_count() -> int:
     return _lib.device_count()
 
 
-def get_context(device: int = 0) -> ScanContext:
-    """The calling thread's context for ``device`` (created on first use)."""
+def get_context(device: int = 0, slot: int = 0) -> ScanContext:
+    """The calling thread's context for ``device`` (created on first use); ``slot`` > 0 names further contexts of
+    the thread on the same device (their own stream and buffers: a thread alternating two overlaps one's copies with
+    the other's scan)."""
     ctxs = getattr(_tls, "ctxs", None)
     if ctxs is None:
         ctxs = _tls.ctxs = {}
-    c = ctxs.get(device)
+    key = device if slot == 0 else (device, slot)
+    c = ctxs.get(key)
     if c is None:
-        c = ctxs[device] = ScanContext(device)
+        c = ctxs[key] = ScanContext(device)
     return c
 
 
 def close_context(device: int = 0) -> None:
-    """Close the calling thread's context for ``device``, if any (its stream, pinned staging and HBM workspace
-    are freed; the next ``get_context`` makes a new one)."""
-    c = getattr(_tls, "ctxs", {}).pop(device, None)
-    if c is not None:
-        c.close()
+    """Close the calling thread's contexts for ``device``, if any (their streams, pinned staging and HBM workspaces
+    are freed; the next ``get_context`` makes new ones)."""
+    ctxs = getattr(_tls, "ctxs", {})
+    for key in [k for k in ctxs if k == device or (isinstance(k, tuple) and k[0] == device)]:
+        ctxs.pop(key).close()
 
 
 def pick_device(i: int, devices: Optional[Iterable[int]] = None) -> int:

@@ -646,8 +646,8 @@ def line_index_pieces(co, begin: int = 0, end: Optional[int] = None, delim: int 
     piece k while later pieces are still being fetched and scanned (the streamed index PUT, verdict r5 #4).
 
     Pieces of at most ``piece_bytes`` (at least one per device entry) go round-robin to the device entries; each
-    entry's persistent worker runs its pieces in order, fetching piece k + 1 while piece k's scan runs
-    (``_delim_piece_run``).  (Two workers per GPU fetching side by side were slower: 41 against ~50 GiB/s of
+    entry's persistent worker runs its pieces in order on two alternating contexts, fetching piece k + 1 while piece
+    k's scan runs (``_delim_piece_run``).  (Two workers per GPU fetching side by side were slower: 41 against ~50 GiB/s of
     GETs + H2D for a 4 GiB CSV, ``profiles/r06/e2e/``.)"""
     if fmt not in ("u8s", "u16b"):
         raise ValueError(f"streamed newline index forms: u8s or u16b, not {fmt!r}")
@@ -673,22 +673,23 @@ def line_index_pieces(co, begin: int = 0, end: Optional[int] = None, delim: int 
 
 
 def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.Event) -> None:
-    """One device entry's pieces in order on its worker, each piece's GETs and H2D copies in flight while the previous
-    piece's scan runs (two device and pinned buffers alternate; at most one scan per context outstanding).  Each
-    piece's (low, table[, sub]) is set on its future; the first failure is set on every remaining one."""
-    ctx = get_context(dev)
+    """One device entry's pieces in order on its worker.  Two contexts of the worker alternate (their own streams,
+    pinned staging and HBM buffers): piece k is fetched and its scan launched on one while piece k - 1's result is
+    read back on the other, so the read-back never waits behind piece k's H2D copies and the next GETs follow at
+    once.  Each piece's (low, table[, sub]) is set on its future; the first failure on every remaining one."""
+    ctxs = (get_context(dev), get_context(dev, 1))
     mode = 4 if fmt == "u8s" else 3
     pend = None
 
-    def launch(i, lo, hi, dp):
+    def launch(ctx, lo, hi, dp):
         rg = np.asarray([lo, hi], np.uint64)
         cap = (hi - lo) // 16 + 1024
-        out = ctx.workspace(f"piece_out{i % 2}", ScanContext.out_bytes(cap, mode, rg))
+        out = ctx.workspace("out", ScanContext.out_bytes(cap, mode, rg))
         ctx.delim_ranges_async(dp, hi - lo, lo, rg, delim, 1, 0, 0, out.ptr, mode, cap)
-        return rg, cap, out, dp
+        return ctx, rg, cap, out, dp
 
     def collect(p, fut):
-        rg, cap, out, dp = p
+        ctx, rg, cap, out, dp = p
         lo, hi = int(rg[0]), int(rg[1])
         try:
             cnt = ctx.delim_ranges_result(1)[0]
@@ -703,12 +704,14 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
         for i, (lo, hi, fut) in enumerate(jobs):
             if stop.is_set():
                 raise RuntimeError("newline index stream abandoned")
-            d = ctx.workspace(f"piece{i % 2}", hi - lo + 64)
+            ctx = ctxs[i % 2]
+            d = ctx.workspace("input", hi - lo + 64)
             dp = d.ptr + (lo & 15)                   # object offset and device address congruent mod 16
-            fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp, staging=f"piece{i % 2}")
+            fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp)
+            p = (launch(ctx, lo, hi, dp), fut)
             if pend is not None:
                 collect(*pend)
-            pend = (launch(i, lo, hi, dp), fut)
+            pend = p
         if pend is not None:
             collect(*pend)
     except BaseException as e:

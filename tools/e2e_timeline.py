@@ -69,6 +69,34 @@ def main():
             mark("consume", n=len(p[0]))
             yield p
     objects.line_index_pieces = pieces
+    from dataplug_amd.formats.generic import csv as fcsv
+    from dataplug_amd.preprocessing import handler, preprocess as pre
+    from dataplug_amd import cloudobject as cob
+
+    def wrap(mod, name):
+        real = getattr(mod, name)
+
+        def w(*a, **kw):
+            mark(name + "_start")
+            try:
+                return real(*a, **kw)
+            finally:
+                mark(name + "_end")
+        setattr(mod, name, w)
+    wrap(fcsv, "index_object")
+    wrap(objects, "line_index_form")
+    for mod in (handler, pre):
+        if hasattr(mod, "upload_metadata"):
+            wrap(mod, "upload_metadata")
+    real_fetch = cob.CloudObject.fetch
+
+    def fetch(self, *a, **kw):
+        mark("fetch_start")
+        r = real_fetch(self, *a, **kw)
+        mark("fetch_end")
+        return r
+    cob.CloudObject.fetch = fetch
+    real_pcsv = fcsv.CSV.preprocessing_function if hasattr(fcsv.CSV, "preprocessing_function") else None
     bucket = "data"
     store = MemoryStore.named("e2e_tl")
     for b in (bucket, bucket + ".meta"):

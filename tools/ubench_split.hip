@@ -10,6 +10,7 @@
 // buffers, it is the memory system.  HIP events per launch, median of `reps`.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_split tools/ubench_split.hip
 //   ./tools/ubench_split [GiB per buffer=4] [buffers=6] [write bytes per read byte=0.025] [reps=5] [variants]
+//                        [output buffers=1] [allocation per input buffer: d / c, e.g. dcdc]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -196,10 +197,15 @@ int main(int argc, char** argv) {
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, 0);
   const int grid = prop.multiProcessorCount;
+  // argv[7]: per input buffer its allocation, d = hipMalloc, c = hipExtMallocWithFlags(hipDeviceMallocContiguous)
+  const char* kinds = argc > 7 ? argv[7] : "";
   std::vector<uint4*> bufs(nbuf);
   for (int i = 0; i < nbuf; ++i) {
-    if (hipMalloc(&bufs[i], bytes) != hipSuccess) {
-      printf("alloc failed\n");
+    const char k = i < (int)strlen(kinds) ? kinds[i] : 'd';
+    const hipError_t e = k == 'c' ? hipExtMallocWithFlags((void**)&bufs[i], bytes, hipDeviceMallocContiguous)
+                                  : hipMalloc(&bufs[i], bytes);
+    if (e != hipSuccess) {
+      printf("alloc %c failed\n", k);
       return 1;
     }
     hipMemset(bufs[i], 0x41 + i, bytes);
@@ -278,8 +284,9 @@ int main(int argc, char** argv) {
       }
   for (int i = 0; i < nbuf; ++i)
   for (int o = 0; o < nout; ++o) {
-    printf("{\"buffer\": %d, \"out\": %d, \"addr_gib\": %.2f, \"out_gib\": %.3f, \"write_per_read\": %.3f", i, o,
-           (double)(uintptr_t)bufs[i] / (1ull << 30), (double)(uintptr_t)outs[o] / (1ull << 30), w);
+    printf("{\"buffer\": %d, \"alloc\": \"%c\", \"out\": %d, \"addr_gib\": %.2f, \"out_gib\": %.3f, \"write_per_read\": %.3f", i,
+           i < (int)strlen(kinds) ? kinds[i] : 'd', o, (double)(uintptr_t)bufs[i] / (1ull << 30),
+           (double)(uintptr_t)outs[o] / (1ull << 30), w);
     for (int v = 0; v < nv; ++v) {
       auto& s = t[(i * nout + o) * nv + v];
       std::sort(s.begin(), s.end());
