@@ -144,6 +144,7 @@ class MultipartWriter:
         except BaseException:
             self.abort()
             raise
+        self.uid = None                           # completed: nothing left to abort
         return self.size
 
     def abort(self) -> None:

@@ -646,8 +646,8 @@ def line_index_pieces(co, begin: int = 0, end: Optional[int] = None, delim: int 
     piece k while later pieces are still being fetched and scanned (the streamed index PUT, verdict r5 #4).
 
     Pieces of at most ``piece_bytes`` (at least one per device entry) go round-robin to the device entries; each
-    entry's persistent worker runs its pieces in order on two alternating contexts, fetching piece k + 1 while piece
-    k's scan runs (``_delim_piece_run``).  (Two workers per GPU fetching side by side were slower: 41 against ~50 GiB/s of
+    entry's persistent worker runs its pieces in order on rotating contexts, fetching piece k + 1 while piece k is
+    scanned and read back (``_delim_piece_run``).  (Two workers per GPU fetching side by side were slower: 41 against ~50 GiB/s of
     GETs + H2D for a 4 GiB CSV, ``profiles/r06/e2e/``.)"""
     if fmt not in ("u8s", "u16b"):
         raise ValueError(f"streamed newline index forms: u8s or u16b, not {fmt!r}")
@@ -672,14 +672,17 @@ def line_index_pieces(co, begin: int = 0, end: Optional[int] = None, delim: int 
         cf.wait(runs)
 
 
+_PIECE_CTXS = 3               # contexts a streamed-index worker rotates: fetch, scan, read-back in flight at once
+
+
 def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.Event) -> None:
-    """One device entry's pieces in order on its worker.  Two contexts of the worker alternate (their own streams,
-    pinned staging and HBM buffers): piece k is fetched and its scan launched on one while piece k - 1's result is
-    read back on the other, so the read-back never waits behind piece k's H2D copies and the next GETs follow at
-    once.  Each piece's (low, table[, sub]) is set on its future; the first failure on every remaining one."""
-    ctxs = (get_context(dev), get_context(dev, 1))
+    """One device entry's pieces in order on its worker.  Three contexts of the worker rotate (their own streams,
+    pinned staging and HBM buffers): piece k is fetched and its scan launched on one while a read-back thread collects
+    piece k - 1 from another, so the worker's next GETs never wait for a read-back (whose D2H may queue behind the
+    H2D copies of piece k on the same copy engine).  Each piece's (low, table[, sub]) is set on its future; the first
+    failure on every remaining one."""
+    ctxs = [get_context(dev, k) for k in range(_PIECE_CTXS)]
     mode = 4 if fmt == "u8s" else 3
-    pend = None
 
     def launch(ctx, lo, hi, dp):
         rg = np.asarray([lo, hi], np.uint64)
@@ -692,32 +695,37 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
         ctx, rg, cap, out, dp = p
         lo, hi = int(rg[0]), int(rg[1])
         try:
-            cnt = ctx.delim_ranges_result(1)[0]
-        except DPCapacityError:                      # denser than 1 per 16 bytes: again, synchronously, sized
-            r = ctx.delim_ranges(dp, hi - lo, lo, [(lo, hi)], delim=delim, out_mode=mode)
-            fut.set_result((r[0], r[3], r[4]) if mode == 4 else (r[0], r[3]))
-            return
-        low = ctx.d2h(np.empty(cnt, np.uint8 if mode == 4 else np.uint16), out.ptr)
-        tab = ctx.block_table(out.ptr, cap, rg, mode)
-        fut.set_result((low, tab, ctx.sub_table(out.ptr, cap, rg)) if mode == 4 else (low, tab))
-    try:
-        for i, (lo, hi, fut) in enumerate(jobs):
-            if stop.is_set():
-                raise RuntimeError("newline index stream abandoned")
-            ctx = ctxs[i % 2]
-            d = ctx.workspace("input", hi - lo + 64)
-            dp = d.ptr + (lo & 15)                   # object offset and device address congruent mod 16
-            fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp)
-            p = (launch(ctx, lo, hi, dp), fut)
-            if pend is not None:
-                collect(*pend)
-            pend = p
-        if pend is not None:
-            collect(*pend)
-    except BaseException as e:
-        for _, _, fut in jobs:
-            if not fut.done():
-                fut.set_exception(e)
+            try:
+                cnt = ctx.delim_ranges_result(1)[0]
+            except DPCapacityError:                  # denser than 1 per 16 bytes: again, synchronously, sized
+                r = ctx.delim_ranges(dp, hi - lo, lo, [(lo, hi)], delim=delim, out_mode=mode)
+                fut.set_result((r[0], r[3], r[4]) if mode == 4 else (r[0], r[3]))
+                return
+            low = ctx.d2h(np.empty(cnt, np.uint8 if mode == 4 else np.uint16), out.ptr)
+            tab = ctx.block_table(out.ptr, cap, rg, mode)
+            fut.set_result((low, tab, ctx.sub_table(out.ptr, cap, rg)) if mode == 4 else (low, tab))
+        except BaseException as e:
+            fut.set_exception(e)
+            raise
+    reads = []
+    with cf.ThreadPoolExecutor(1, thread_name_prefix=f"dpscan-readback{dev}") as rb:
+        try:
+            for i, (lo, hi, fut) in enumerate(jobs):
+                if stop.is_set():
+                    raise RuntimeError("newline index stream abandoned")
+                if i >= _PIECE_CTXS:
+                    reads[i - _PIECE_CTXS].result()   # that context's previous piece is read back
+                ctx = ctxs[i % _PIECE_CTXS]
+                d = ctx.workspace("input", hi - lo + 64)
+                dp = d.ptr + (lo & 15)               # object offset and device address congruent mod 16
+                fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp)
+                reads.append(rb.submit(collect, launch(ctx, lo, hi, dp), fut))
+            cf.wait(reads)
+        except BaseException as e:
+            cf.wait(reads)
+            for _, _, fut in jobs:
+                if not fut.done():
+                    fut.set_exception(e)
 
 
 def record_index_bytes(data, delim: int = 10, every_k: int = 1, emit_add: int = 0, device: int = 0,

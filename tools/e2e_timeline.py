@@ -96,6 +96,11 @@ def main():
         mark("fetch_end")
         return r
     cob.CloudObject.fetch = fetch
+    import gc
+
+    def gc_cb(phase, info):
+        mark("gc_" + phase, gen=info.get("generation"))
+    gc.callbacks.append(gc_cb)
     real_pcsv = fcsv.CSV.preprocessing_function if hasattr(fcsv.CSV, "preprocessing_function") else None
     bucket = "data"
     store = MemoryStore.named("e2e_tl")
