@@ -89,29 +89,44 @@ def fetch_to_device(ctx: ScanContext, storage, bucket: str, key: str, lo: int, h
     host = ctx.pinned(staging, max(n, 1))
     if n <= 0:
         return host
-    view = host.view(n)
-    starts = list(range(0, n, part))
-    if len(starts) == 1:
-        read_range_into(storage, bucket, key, lo, hi, view, part=part, threads=threads)
+    if n <= part:
+        read_range_into(storage, bucket, key, lo, hi, host.view(n), part=part, threads=threads)
         ctx.h2d_async(d_ptr, host.ptr, n)
         return host
+    land_gets(ctx, submit_gets(ctx.get_pool(threads), storage, bucket, key, lo, hi, host, part), d_ptr)
+    return host
+
+
+def submit_gets(pool, storage, bucket: str, key: str, lo: int, hi: int, host, part: int = _GET_PART):
+    """Queue the ranged GETs of object bytes [lo, hi) into pinned ``host`` on ``pool`` (parts of ``part`` bytes, in
+    order); ``land_gets`` copies them to the device as they land.  Queued behind another fetch's GETs on the same
+    pool, they start as its last ones finish (a continuous GET stream across pieces)."""
+    n = hi - lo
+    view = host.view(n)
 
     def one(a: int) -> int:
         read_range_into(storage, bucket, key, lo + a, lo + min(n, a + part), view[a:], part=part, threads=1)
         return a
+    return host, n, part, [pool.submit(one, a) for a in range(0, n, part)]
 
-    ex = ctx.get_pool(threads)                # the context's persistent GET threads (no pool per call)
-    futs = [ex.submit(one, a) for a in starts]
+
+def land_gets(ctx: ScanContext, gets, d_ptr: int) -> None:
+    """Each part of ``submit_gets`` copied to ``d_ptr`` on the context stream as soon as it lands (H2D issued from
+    the calling thread only); a failed GET cancels the rest, and none may still land in the staging buffer."""
+    host, n, part, futs = gets
     try:
-        for f in cf.as_completed(futs):       # H2D issued from this (the context's) thread only
+        for f in cf.as_completed(futs):
             a = f.result()
             ctx.h2d_async(d_ptr + a, host.ptr + a, min(n, a + part) - a)
     except BaseException:
-        for f in futs:                        # a failed GET: no part may still land in the staging buffer
-            f.cancel()
-        cf.wait(futs)
+        cancel_gets(gets)
         raise
-    return host
+
+
+def cancel_gets(gets) -> None:
+    for f in gets[3]:
+        f.cancel()
+    cf.wait(gets[3])
 
 
 def resolve_line_end(ctx: ScanContext, storage, bucket: str, key: str, size: int, pos: int) -> int:
@@ -679,8 +694,9 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
     """One device entry's pieces in order on its worker.  Three contexts of the worker rotate (their own streams,
     pinned staging and HBM buffers): piece k is fetched and its scan launched on one while a read-back thread collects
     piece k - 1 from another, so the worker's next GETs never wait for a read-back (whose D2H may queue behind the
-    H2D copies of piece k on the same copy engine).  Each piece's (low, table[, sub]) is set on its future; the first
-    failure on every remaining one."""
+    H2D copies of piece k on the same copy engine); piece k + 1's GETs are queued behind piece k's on one GET pool,
+    so the GET stream does not drain at piece boundaries.  Each piece's (low, table[, sub]) is set on its future;
+    the first failure on every remaining one."""
     ctxs = [get_context(dev, k) for k in range(_PIECE_CTXS)]
     mode = 4 if fmt == "u8s" else 3
 
@@ -708,20 +724,31 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
             fut.set_exception(e)
             raise
     reads = []
+    pool = ctxs[0].get_pool(_GET_THREADS)         # one GET stream for every piece of the worker
+    nxt = None                                      # the next piece's GETs, queued behind the current piece's
+
+    def queue_gets(i):
+        lo, hi, _ = jobs[i]
+        if i >= _PIECE_CTXS:
+            reads[i - _PIECE_CTXS].result()         # its context's previous piece is read back: staging is free
+        host = ctxs[i % _PIECE_CTXS].pinned("object", hi - lo)
+        return submit_gets(pool, co.storage, co.path.bucket, co.path.key, lo, hi, host)
     with cf.ThreadPoolExecutor(1, thread_name_prefix=f"dpscan-readback{dev}") as rb:
         try:
             for i, (lo, hi, fut) in enumerate(jobs):
                 if stop.is_set():
                     raise RuntimeError("newline index stream abandoned")
-                if i >= _PIECE_CTXS:
-                    reads[i - _PIECE_CTXS].result()   # that context's previous piece is read back
                 ctx = ctxs[i % _PIECE_CTXS]
+                gets = nxt if nxt is not None else queue_gets(i)
+                nxt = queue_gets(i + 1) if i + 1 < len(jobs) else None
                 d = ctx.workspace("input", hi - lo + 64)
                 dp = d.ptr + (lo & 15)               # object offset and device address congruent mod 16
-                fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp)
+                land_gets(ctx, gets, dp)
                 reads.append(rb.submit(collect, launch(ctx, lo, hi, dp), fut))
             cf.wait(reads)
         except BaseException as e:
+            if nxt is not None:
+                cancel_gets(nxt)
             cf.wait(reads)
             for _, _, fut in jobs:
                 if not fut.done():

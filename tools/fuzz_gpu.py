@@ -190,9 +190,11 @@ def csv_like(rng, size):
 
 
 def lines_mode(args, rng):
-    """The CSV newline index through co.preprocess() in a random stored form (u8s, u16b, u32p, u64), the object split
-    into 1-9 parts on this GPU (dataplug_devices=[0]*g: each part its own launch, the tables merged on the host),
-    read back through LineIndex (preloaded or block by block) against the oracle's newline offsets."""
+    """The CSV newline index through co.preprocess() in a random stored form (u8s, u16b, u32p, u64, or auto: by the
+    object's density), the object split into 1-9 parts on this GPU (dataplug_devices=[0]*g: each part its own launch,
+    the tables merged on the host) or, for half the u8s / u16b / auto cases, stored as it is produced in pieces of
+    64 KiB - 8 MiB (round 6), read back through LineIndex (preloaded or block by block) against the oracle's newline
+    offsets."""
     from dataplug_amd.cloudobject import CloudObject
     from dataplug_amd.formats import _lines
     from dataplug_amd.formats.generic.csv import CSV
@@ -203,8 +205,12 @@ def lines_mode(args, rng):
     while time.time() - t0 < args.seconds:
         size = int(math.exp(rng.uniform(math.log(64), math.log(getattr(args, "max_size", 24 << 20)))))
         a = csv_like(rng, size)
-        fmt = str(rng.choice(["u8s", "u8s", "u16b", "u32p", "u64"]))
+        fmt = str(rng.choice(["u8s", "u8s", "u16b", "u32p", "u64", "auto", "auto"]))
         groups = int(rng.integers(1, 10))
+        # (round 6) half the u8s / u16b / auto cases store the index as it is produced: pieces of 64 KiB - 8 MiB
+        streamed = fmt not in ("u32p", "u64") and rng.random() < 0.5
+        piece = int(math.exp(rng.uniform(math.log(64 << 10), math.log(8 << 20)))) if streamed else _lines.STREAM_PIECE
+        _lines.index_object.__defaults__ = (0, "auto", piece)
         name = f"fl{i}"
         MemoryStore._named.pop(name, None)
         cfg = {"endpoint_url": f"memory://{name}"}
@@ -225,7 +231,11 @@ def lines_mode(args, rng):
             _lines._PRELOAD_BYTES = saved
         exp = dpref.delim(a, 0, len(a))[0]
         MemoryStore._named.pop(name, None)
+        if fmt == "auto":
+            from dataplug_amd.scan.objects import line_index_form
+            fmt = line_index_form(co, 0, len(a))
         dtype_ok = getattr(co.attributes, "line_index_dtype", None) == (None if fmt == "u64" else fmt)
+        stats["streamed_cases"] = stats.get("streamed_cases", 0) + int(streamed and len(a) > piece)
         if not dtype_ok or not np.array_equal(np.asarray(got, np.uint64), exp):
             _save_fail(data=a, groups=groups)
             print(json.dumps({"FAIL": "lines", "size": int(len(a)), "format": fmt, "groups": groups,
