@@ -2855,6 +2855,7 @@ struct dp_ctx {
   int last_delim_form = 0;            // the kernels the last collected newline launch ran (1 or 3)
   // async call state
   int inflight = -1;                  // -1 none, kFasta, kDelim
+  bool ctrl_pending = false;          // the launch's control words are already queued for read-back (enqueue_ctrl)
   uint64_t nchunks = 0, cap = 0;
   int out_u64 = 0;
   uint32_t every_k = 1;
@@ -3245,11 +3246,24 @@ int check_ctx(dp_ctx* c) {
   return DP_OK;
 }
 
-int collect_ctrl(dp_ctx* c) {
-  // D2H of [pending (nchunks) | chunk_end (nchunks) | ctrl] and wait
+// D2H of [pending (nchunks) | chunk_end (nchunks) | ctrl], queued on the context stream right behind a launch's
+// kernels: a read-back queued only when the result is collected waits in the copy engine behind whatever other
+// streams queued meanwhile (a streamed index's next H2D pieces: tens of ms).
+int enqueue_ctrl(dp_ctx* c) {
   const uint64_t off = c->pend_off;
   const uint64_t words = c->ctrl_off + kCtrlWords - off;
   HIPCHK(hipMemcpyAsync(c->h_tab + off, c->d_tab + off, words * 8, hipMemcpyDeviceToHost, c->stream));
+  c->ctrl_pending = true;
+  return DP_OK;
+}
+
+int collect_ctrl(dp_ctx* c) {
+  // the control words (queued at launch) and wait
+  if (!c->ctrl_pending) {
+    const int rc = enqueue_ctrl(c);
+    if (rc) return rc;
+  }
+  c->ctrl_pending = false;
   HIPCHK(hipStreamSynchronize(c->stream));
   int rc = harvest_events(c);
   if (rc) return rc;
@@ -3460,7 +3474,7 @@ int dp_fasta_index_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uint
   c->nchunks = nchunks;
   c->cap = cap_pairs;
   c->out_u64 = out_u64;
-  return DP_OK;
+  return enqueue_ctrl(c);
 }
 
 int dp_fasta_result(dp_ctx* c, uint64_t* n_pairs, int64_t* pending, uint64_t* chunk_end) {
@@ -3623,7 +3637,7 @@ int dp_delim_ranges_async(dp_ctx* c, const uint8_t* d_buf, uint64_t buf_len, uin
   c->out_u64 = out_mode == 1;
   c->every_k = every_k;
   c->carry = carry;
-  return DP_OK;
+  return enqueue_ctrl(c);
 }
 
 int dp_delim_ranges_result(dp_ctx* c, uint64_t* n_out, uint64_t* n_delims, uint64_t* range_end) {

@@ -119,6 +119,11 @@ class ScanContext:
         check(self.lib.dp_sync(self.handle))   # pageable source: keep it alive until the copy is done
         del keep
 
+    def d2h_async(self, dst_ptr: int, src: int, nbytes: int) -> None:
+        """Async copy to pinned host memory on the context stream (ordered after the work enqueued before it)."""
+        if nbytes:
+            check(self.lib.dp_d2h(self.handle, ctypes.c_void_p(dst_ptr), ctypes.c_void_p(src), int(nbytes)))
+
     def d2h(self, out: np.ndarray, src: int) -> np.ndarray:
         if out.nbytes:
             check(self.lib.dp_d2h(self.handle, ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(src), out.nbytes))

@@ -702,24 +702,46 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
 
     def launch(ctx, lo, hi, dp):
         rg = np.asarray([lo, hi], np.uint64)
-        cap = (hi - lo) // 16 + 1024
-        out = ctx.workspace("out", ScanContext.out_bytes(cap, mode, rg))
+        # capacity: 1 per 16 bytes for u8s, 1 per 64 for u16b (what "auto" stores below 1 per 128); a denser piece
+        # is scanned again, sized, at its read-back
+        cap = (hi - lo) // (16 if mode == 4 else 64) + 1024
+        nbytes = ScanContext.out_bytes(cap, mode, rg)
+        out = ctx.workspace("out", nbytes)
         ctx.delim_ranges_async(dp, hi - lo, lo, rg, delim, 1, 0, 0, out.ptr, mode, cap)
-        return ctx, rg, cap, out, dp
+        # the whole output region read back right behind the scan (the entries' count is not known yet): in the
+        # copy queue ahead of the next pieces' H2D copies, where a read-back issued after the count would wait
+        hb = ctx.pinned("readback", nbytes)
+        ctx.d2h_async(hb.ptr, out.ptr, nbytes)
+        return ctx, rg, cap, out, dp, hb
 
     def collect(p, fut):
-        ctx, rg, cap, out, dp = p
+        ctx, rg, cap, out, dp, hb = p
         lo, hi = int(rg[0]), int(rg[1])
         try:
             try:
                 cnt = ctx.delim_ranges_result(1)[0]
-            except DPCapacityError:                  # denser than 1 per 16 bytes: again, synchronously, sized
+            except DPCapacityError:                  # denser than the capacity: again, synchronously, sized
+                ctx.sync()
                 r = ctx.delim_ranges(dp, hi - lo, lo, [(lo, hi)], delim=delim, out_mode=mode)
                 fut.set_result((r[0], r[3], r[4]) if mode == 4 else (r[0], r[3]))
                 return
-            low = ctx.d2h(np.empty(cnt, np.uint8 if mode == 4 else np.uint16), out.ptr)
-            tab = ctx.block_table(out.ptr, cap, rg, mode)
-            fut.set_result((low, tab, ctx.sub_table(out.ptr, cap, rg)) if mode == 4 else (low, tab))
+            ctx.sync()                               # the read-back has landed
+            a = hb.array
+            low = a[:cnt * (1 if mode == 4 else 2)].view(np.uint8 if mode == 4 else np.uint16).copy()
+            j0, nt = ScanContext.block_table_size(rg)
+            t0 = ScanContext._tab_off(cap, mode)
+            tab = a[t0:t0 + 8 * nt].view(np.uint64).copy()
+            if lo & 0xFFFF:
+                tab[0] = 0                           # the boundary below the first byte (ScanContext.block_table)
+            if mode == 3:
+                fut.set_result((low, tab))
+                return
+            s0, ns = ScanContext.sub_table_size(rg)
+            u0 = ScanContext._sub_off(cap, rg)
+            sub = a[u0:u0 + 2 * ns].view(np.uint16).copy()
+            if lo & 0xFF:
+                sub[0] = 0
+            fut.set_result((low, tab, sub))
         except BaseException as e:
             fut.set_exception(e)
             raise

@@ -97,6 +97,22 @@ def main():
         return r
     cob.CloudObject.fetch = fetch
     import gc
+    from dataplug_amd.storage import client as stc
+    for cls in (stc.LocalS3Client, stc.HTTPS3Client):
+        for meth in ("put_object", "complete_multipart_upload", "get_object", "head_object"):
+            real_m = getattr(cls, meth)
+
+            def m(self, *a, _real=real_m, _meth=meth, **kw):
+                big = _meth != "get_object" or kw.get("Range") is None
+                if big:
+                    mark(_meth + "_start", key=str(kw.get("Key", ""))[-12:])
+                try:
+                    return _real(self, *a, **kw)
+                finally:
+                    if big:
+                        mark(_meth + "_end", key=str(kw.get("Key", ""))[-12:])
+            setattr(cls, meth, m)
+    wrap(_lines, "store_line_index_stream")
 
     def gc_cb(phase, info):
         mark("gc_" + phase, gen=info.get("generation"))
