@@ -113,6 +113,22 @@ def main():
                         mark(_meth + "_end", key=str(kw.get("Key", ""))[-12:])
             setattr(cls, meth, m)
     wrap(_lines, "store_line_index_stream")
+    # a sampler of the main thread's stack every 0.5 ms while a call runs: what it does in the gaps between marks
+    samples = []
+    sampling = threading.Event()
+    main_id = threading.main_thread().ident
+
+    def sampler():
+        import traceback
+        while True:
+            sampling.wait()
+            f = sys._current_frames().get(main_id)
+            if f is not None:
+                st = traceback.extract_stack(f)[-3:]
+                samples.append((round((time.perf_counter() - t0[0]) * 1e3, 2),
+                                " < ".join(f"{os.path.basename(x.filename)}:{x.lineno}:{x.name}" for x in reversed(st))))
+            time.sleep(0.0005)
+    threading.Thread(target=sampler, daemon=True).start()
 
     def gc_cb(phase, info):
         mark("gc_" + phase, gen=info.get("generation"))
@@ -134,15 +150,23 @@ def main():
         co = CloudObject.from_s3(CSV, f"s3://{bucket}/x", s3_config=cfg)
         for i in range(3):
             ev.clear()
+            samples.clear()
             t0[0] = time.perf_counter()
             mark("call_start")
+            sampling.set()
             co.preprocess(force=True)
+            sampling.clear()
             mark("call_end")
             dt = ev[-1]["t_ms"]
             print(json.dumps({"src": src, "call": i, "ms": dt, "GiB_per_s": round(size / (dt / 1e3) / (1 << 30), 2)}),
                   flush=True)
         for e in ev:
             print(json.dumps(e))
+        last = None
+        for t, where in samples:                  # the main thread's stack, one line per change
+            if where != last:
+                print(json.dumps({"sample_ms": t, "main": where}))
+                last = where
         if srv is not None:
             srv.stop()
 
