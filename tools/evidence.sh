@@ -1,6 +1,7 @@
 #!/bin/bash
 # Evidence pass (on the GPU box): size sweep, newline form sweep, rocprofv3 trace + PMC of each bench leg, the bench
 # line.   bash tools/evidence.sh <tag> [legs]      -> gpurun_out/<tag>/ (copy into profiles/rNN/)
+# (NO_SWEEPS / NO_FORM_SWEEP / NO_BENCH skip those steps)
 set -o pipefail
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 T=${1:-ev}; O=gpurun_out/$T; mkdir -p $O
@@ -21,7 +22,9 @@ for leg in $LEGS; do
   timeout -k 10 500 bash tools/leg_prof.sh $leg $O/$leg ${T}_$leg > $O/prof_$leg.log 2>&1 || { tail -20 $O/prof_$leg.log; exit 1; }
   tail -4 $O/prof_$leg.log
 done
-step bench
-timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
-python3 tools/bench_summary.py $O/bench.json
+if [ -z "$NO_BENCH" ]; then
+  step bench
+  timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+  python3 tools/bench_summary.py $O/bench.json
+fi
 step done
