@@ -16,10 +16,6 @@
  *  4. the windows are resolved in order (the last 32 KiB of each region only), then every region's markers
  *     are replaced in parallel, and each member's CRC-32 and ISIZE are checked against its trailer, so a
  *     wrong speculative decode cannot pass silently.
- *  5. (round 6) batches overlap: batch k's marker replacement and CRC jobs run in the same parallel phase as batch
- *     k + 1's find + decode jobs (two region sets; region 0's window comes from batch k's tail, resolved through
- *     that region's own window like any other region's), so the resolution is not a separate pass of the pool.
- *     A decoded batch is resolved by the next step, or when the input or the stream ends.
  *
  * The access points are those of dpgz_stream (the first block start at least `span` inflated bytes after the
  * previous point, and every member start) with the same windows.  A batch ends at a block start or a member
@@ -873,7 +869,6 @@ void dpgz__global_for(int threads, int n, void (*fn)(void*, int), void* arg) {
   pthread_mutex_unlock(&g_pool_mu);
 }
 
-struct Batch;
 struct dpgz_par {
   uint64_t span;
   int threads;
@@ -897,21 +892,13 @@ struct dpgz_par {
   uint8_t* wins;
   uint64_t nwin, wcap;
   int failed;
-  Region* regs;               /* two sets of nregs: batch k decodes into set k & 1 while batch k - 1 resolves */
+  Region* regs;
   int nregs;
   uint64_t batches, rejected;
-  struct Batch* bt;           /* [2]: the batches of the two region sets */
-  uint64_t seq;               /* the next batch's number */
-  int pend;                   /* the set of a batch decoded but not yet resolved, or -1 */
-  const Region* prev_last;    /* the last kept region of the most recent decoded batch (its window chain) */
-  uint64_t a_since;           /* (decode side) inflated bytes of the current member before the next batch */
-  uint32_t next_wl;           /* (decode side) min(WIN, a_since): the next batch's known window length */
   uint64_t region_min;
   Pool pool;                  /* threads - 1 workers */
   uint64_t ns[5];             /* time per phase: find, decode, windows, resolve, in-order bookkeeping */
 };
-
-static struct Batch* batches_new(void);   /* the two batches (defined with struct Batch below) */
 
 int dpgz_par_new(uint64_t span, int threads, dpgz_par** out) {
   if (!out) return DPGZ_ERR_INVALID;
@@ -924,10 +911,8 @@ int dpgz_par_new(uint64_t span, int threads, dpgz_par** out) {
   s->prev = -1;
   s->crc = (uint32_t)crc32(0L, Z_NULL, 0);
   s->nregs = 2 * s->threads;                          /* regions per batch: two per thread (dynamic balance) */
-  s->regs = (Region*)calloc((size_t)(2 * s->nregs), sizeof(Region));
-  s->bt = batches_new();
-  if (!s->regs || !s->bt) { free(s->regs); free(s->bt); free(s); return DPGZ_ERR_MEMORY; }
-  s->pend = -1;
+  s->regs = (Region*)calloc((size_t)s->nregs, sizeof(Region));
+  if (!s->regs) { free(s); return DPGZ_ERR_MEMORY; }
   pool_init(&s->pool, s->threads - 1);
   *out = s;
   return DPGZ_OK;
@@ -936,12 +921,11 @@ int dpgz_par_new(uint64_t span, int threads, dpgz_par** out) {
 void dpgz_par_free(dpgz_par* s) {
   if (!s) return;
   pool_free(&s->pool);
-  for (int i = 0; i < 2 * s->nregs; ++i) {
+  for (int i = 0; i < s->nregs; ++i) {
     free(s->regs[i].o);
     free(s->regs[i].ev);
   }
   free(s->regs);
-  free(s->bt);
   free(s->cin);
   free(s->out);
   free(s->pts);
@@ -949,111 +933,80 @@ void dpgz_par_free(dpgz_par* s) {
   free(s);
 }
 
-#define MAXREG (2 * 256 + 1)
-/* One batch: its regions' decode (find + decode, in parallel), then, while the next batch decodes, their
- * resolution (markers replaced + CRC segments, in parallel) and the in-order bookkeeping. */
-typedef struct Batch {
+typedef struct {
   dpgz_par* s;
-  Region* regs;               /* this batch's region set */
   int final;
-  uint64_t nbytes;            /* compressed bytes the decode sees */
-  uint64_t start;             /* region 0's start (bit position in cin) and kind */
-  int start_kind;
-  uint32_t wl0;               /* bytes of the current member before the start (<= WIN): region 0's reach */
-  uint64_t bound[MAXREG];     /* nominal region starts (bits), nreg + 1 */
-  uint64_t found[MAXREG];     /* found starts */
-  int idx[MAXREG];            /* region slot of each kept start */
+  uint64_t nbytes;
+  uint64_t* bound;            /* nominal region starts (bits), nreg + 1 */
+  uint64_t* found;            /* found starts */
+  int* idx;                   /* region slot of each kept start */
   int nkeep;
   int nreg;
   uint64_t stop_last;         /* the last region's stop_after (NONE: the batch holds the rest of the input) */
-  uint64_t total;             /* inflated bytes of the kept regions */
-  uint64_t cbase;             /* stream byte of cin[0] while the batch decoded (its events' bit positions) */
-  int end_kind;               /* what follows the batch (K_BLOCK, K_HEADER, K_END) */
   uint8_t* dst;               /* the batch's resolved output */
   uint32_t* seg_crc;          /* per region: CRC of its output up to its first member end, then per member */
   uint64_t* seg_len;
-  uint64_t seg_off[MAXREG];   /* first segment of each region in seg_* */
+  uint64_t* seg_off;          /* first segment of each region in seg_* */
 } Batch;
-
-static struct Batch* batches_new(void) { return (struct Batch*)calloc(2, sizeof(struct Batch)); }
 
 static void job_find_decode(void* a, int i) {
   Batch* b = (Batch*)a;
   dpgz_par* s = b->s;
-  Region* r = &b->regs[i];
+  Region* r = &s->regs[i];
   r->n = 0;                                             /* the buffer is reused: only the window is kept */
   if (reserve(r, WIN + s->region_min * 5 / 2 + (1u << 16))) { r->rc = D_MEM; return; }
   if (i > 0) {
     b->found[i] = find_block(r, s->cin, b->nbytes, b->bound[i], b->bound[i + 1]);
     if (b->found[i] == NONE) { r->rc = D_OK; return; }
   }
-  r->start = i == 0 ? b->start : b->found[i];
-  r->start_kind = i == 0 ? b->start_kind : K_BLOCK;
+  r->start = i == 0 ? s->pos : b->found[i];
+  r->start_kind = i == 0 ? s->kind : K_BLOCK;
   r->stop_at = NONE;
   r->stop_after = i + 1 < b->nreg ? b->bound[i + 1] : b->stop_last;
-  /* every region's window is markers, resolved later (region 0's from the previous batch's tail, which may not be
-   * resolved yet); region 0 may reach back the wl0 bytes of its member known before it */
-  for (uint32_t j = 0; j < WIN; ++j) r->o[j] = (uint16_t)(256 + j);
-  r->floor0 = i == 0 ? WIN - b->wl0 : 0;
+  if (i == 0) {                                         /* the known window, right-aligned */
+    for (uint32_t j = 0; j < WIN; ++j) r->o[j] = j >= WIN - s->wl ? s->win[j - (WIN - s->wl)] : (uint16_t)(256 + j);
+    r->floor0 = WIN - s->wl;
+  } else {
+    for (uint32_t j = 0; j < WIN; ++j) r->o[j] = (uint16_t)(256 + j);
+    r->floor0 = 0;
+  }
   decode_region(r, s->cin, b->nbytes, b->final && i == b->nreg - 1);
 }
 
-/* Markers replaced and CRC segments computed chunk by chunk (RESOLVE_CHUNK output bytes): each chunk's CRC runs
- * while its bytes are still in the core's cache, instead of a second pass over the region's output. */
-#define RESOLVE_CHUNK (64u << 10)
 static void job_resolve(void* a, int k) {
   Batch* b = (Batch*)a;
-  Region* r = &b->regs[b->idx[k]];
+  Region* r = &b->s->regs[b->idx[k]];
   uint8_t* d = b->dst + r->out_off;
   const uint16_t* o = r->o + WIN;
   const uint64_t m = r->n - WIN;
-  /* CRC segments, split at member ends and starts (a member's CRC covers its own bytes only) */
-  uint64_t si = b->seg_off[k], from = 0, e = 0;
-  uint32_t crc = 0u;
-  for (uint64_t c0 = 0; c0 < m; c0 += RESOLVE_CHUNK) {
-    const uint64_t c1 = c0 + RESOLVE_CHUNK < m ? c0 + RESOLVE_CHUNK : m;
-    uint64_t i = c0;
-    while (i < c1) {                                    /* 32 symbols at a time while no marker is among them */
-      if (i + 32 <= c1) {
-        uint16_t any = 0;
-        for (int q = 0; q < 32; ++q) any |= o[i + q];
-        if (!(any & 0xFF00u)) {
-          for (int q = 0; q < 32; ++q) d[i + q] = (uint8_t)o[i + q];
-          i += 32;
-          continue;
-        }
-      }
-      const uint64_t ee = i + 32 < c1 ? i + 32 : c1;
-      for (; i < ee; ++i) {
-        const uint16_t v = o[i];
-        d[i] = v < 256 ? (uint8_t)v : r->win[v - 256];
+  uint64_t i = 0;
+  while (i < m) {                                       /* 32 symbols at a time while no marker is among them */
+    if (i + 32 <= m) {
+      uint16_t any = 0;
+      for (int k = 0; k < 32; ++k) any |= o[i + k];
+      if (!(any & 0xFF00u)) {
+        for (int k = 0; k < 32; ++k) d[i + k] = (uint8_t)o[i + k];
+        i += 32;
+        continue;
       }
     }
-    uint64_t p = c0;
-    for (;;) {                                          /* the chunk's CRC, cut at the member events inside it */
-      while (e < r->nev && r->ev[e].kind == EV_BLOCK) ++e;
-      const uint64_t at = e < r->nev ? r->ev[e].out - WIN : NONE;
-      if (at == NONE || at > c1) break;
-      crc = crc32_fast(crc, d + p, at - p);
-      b->seg_crc[si] = crc;
-      b->seg_len[si] = at - from;
-      ++si;
-      crc = 0u;
-      from = p = at;
-      ++e;
+    const uint64_t e = i + 32 < m ? i + 32 : m;
+    for (; i < e; ++i) {
+      const uint16_t v = o[i];
+      d[i] = v < 256 ? (uint8_t)v : r->win[v - 256];
     }
-    crc = crc32_fast(crc, d + p, c1 - p);
   }
-  for (; e < r->nev; ++e) {                             /* member events at the region's very end (or m == 0) */
+  /* CRC segments, split at member ends and starts (a member's CRC covers its own bytes only) */
+  uint64_t si = b->seg_off[k], from = 0;
+  for (uint64_t e = 0; e < r->nev; ++e) {
     if (r->ev[e].kind == EV_BLOCK) continue;
     const uint64_t at = r->ev[e].out - WIN;
-    b->seg_crc[si] = crc;
+    b->seg_crc[si] = crc32_fast(0u, d + from, at - from);
     b->seg_len[si] = at - from;
     ++si;
-    crc = 0u;
     from = at;
   }
-  b->seg_crc[si] = crc;
+  b->seg_crc[si] = crc32_fast(0u, d + from, m - from);
   b->seg_len[si] = m - from;
 }
 
@@ -1095,14 +1048,16 @@ static int add_point(dpgz_par* s, uint64_t in_byte, uint32_t bits, uint64_t out,
   return 0;
 }
 
+/* One batch over the pending compressed bytes.  Returns a DPGZ status; *progress = 1 if it moved. */
 static uint64_t now_ns(void) {
   struct timespec ts;
   clock_gettime(CLOCK_MONOTONIC, &ts);
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
-
-/* Decode side, before the parallel phase: the next batch's regions over the pending compressed bytes. */
-static void batch_prep_decode(dpgz_par* s, Batch* B, int final) {
+static int par_batch(dpgz_par* s, int final, int* progress) {
+  *progress = 0;
+  uint64_t t0 = now_ns(), t1;
+  if (s->kind == K_END) return DPGZ_OK;
   const uint64_t nbytes = s->clen;
   const uint64_t b0 = s->pos >> 3;
   /* at most two batches' worth of regions at a time (bounded memory whatever the caller feeds); the last
@@ -1114,33 +1069,34 @@ static void batch_prep_decode(dpgz_par* s, Batch* B, int final) {
   int nreg = (int)(avail / s->region_min);
   if (nreg > s->nregs) nreg = s->nregs;
   if (nreg < 1) nreg = 1;
-  B->s = s;
-  B->regs = s->regs + (size_t)(s->seq & 1u) * (size_t)s->nregs;
-  B->final = final;
-  B->nbytes = nbytes;
-  B->start = s->pos;
-  B->start_kind = s->kind;
-  B->wl0 = s->next_wl;
-  B->nreg = nreg;
-  for (int i = 0; i <= nreg; ++i) B->bound[i] = (b0 + avail * (uint64_t)i / (uint64_t)nreg) * 8;
-  B->bound[0] = s->pos;
-  B->found[0] = s->pos;
-  B->stop_last = whole ? NONE : (b0 + avail) * 8;
-  B->nkeep = 0;
-  B->total = 0;
-}
-
-/* Decode side, after the parallel phase: keep regions in order while each starts exactly where the previous kept
- * one stopped (a region without a block start in its range is skipped: the previous one decodes through it),
- * chain the windows, and move the decode position past the batch.  *progress = 1 if it moved. */
-static int batch_finish_decode(dpgz_par* s, Batch* B, int* progress) {
-  *progress = 0;
+  uint64_t bound[2 * 256 + 1], found[2 * 256 + 1];
+  int idx[2 * 256 + 1];
+  for (int i = 0; i <= nreg; ++i) bound[i] = (b0 + avail * (uint64_t)i / (uint64_t)nreg) * 8;
+  bound[0] = s->pos;
+  found[0] = s->pos;
+  Batch B;
+  memset(&B, 0, sizeof(B));
+  B.s = s;
+  B.final = final;
+  B.nbytes = nbytes;
+  B.bound = bound;
+  B.found = found;
+  B.idx = idx;
+  B.nreg = nreg;
+  B.stop_last = whole ? NONE : (b0 + avail) * 8;
+  /* every region: find its start (a block start in its nominal range; region 0 starts at the known position),
+   * then decode to the first block start at or past the next region's nominal start -- which is that
+   * region's found start when it is a true one.  Regions outnumber the threads (dynamic balance). */
+  pool_for(&s->pool, nreg, job_find_decode, &B);
+  t1 = now_ns(); s->ns[1] += t1 - t0; t0 = t1;
+  /* keep regions in order while each starts exactly where the previous kept one stopped (a region without
+   * a block start in its range is skipped: the previous one decodes through it) */
   int nkeep = 0;
-  for (int i = 0; i < B->nreg; ++i) {
-    Region* r = &B->regs[i];
+  for (int i = 0; i < nreg; ++i) {
+    Region* r = &s->regs[i];
     if (i > 0) {
-      if (B->found[i] == NONE) continue;
-      Region* q = &B->regs[B->idx[nkeep - 1]];
+      if (found[i] == NONE) continue;
+      Region* q = &s->regs[idx[nkeep - 1]];
       if (q->rc != D_OK || q->end != r->start) {
         if (q->rc == D_OK) s->rejected++;
         break;
@@ -1149,66 +1105,29 @@ static int batch_finish_decode(dpgz_par* s, Batch* B, int* progress) {
     if (r->rc == D_MEM) return DPGZ_ERR_MEMORY;
     if (r->rc == D_BAD) return DPGZ_ERR_ZLIB;           /* its start is a true boundary: corrupt data */
     if (r->rc == D_TRUNC) return DPGZ_ERR_TRUNCATED;
-    B->idx[nkeep++] = i;
+    idx[nkeep++] = i;
     if (r->rc == D_INPUT) break;
   }
-  B->nkeep = nkeep;
-  Region* lastr = &B->regs[B->idx[nkeep - 1]];
+  Region* lastr = &s->regs[idx[nkeep - 1]];
   uint64_t total = 0;
   for (int k = 0; k < nkeep; ++k) {
-    Region* r = &B->regs[B->idx[k]];
+    Region* r = &s->regs[idx[k]];
     r->out_off = total;
     total += r->n - WIN;
   }
-  B->total = total;
   if (total == 0 && lastr->end == s->pos && lastr->end_kind == s->kind && lastr->rc == D_INPUT) return DPGZ_OK;
-  /* windows, in order: region 0's = the previous batch's resolved tail (its last kept region's last WIN entries
-   * through that region's own window; the known window at the stream start), region k's = region k-1's */
+  /* windows, in order: region 0's is the known one; region k's = the resolved last WIN entries of k-1 */
   {
-    Region* r0 = &B->regs[B->idx[0]];
-    const Region* q = s->prev_last;
-    if (q) {
-      const uint16_t* t = q->o + q->n - WIN;
-      for (uint32_t j = 0; j < WIN; ++j) r0->win[j] = t[j] < 256 ? (uint8_t)t[j] : q->win[t[j] - 256];
-    } else {
-      memset(r0->win, 0, WIN);
-      memcpy(r0->win + (WIN - s->wl), s->win, s->wl);
-    }
+    Region* r0 = &s->regs[idx[0]];
+    memset(r0->win, 0, WIN);
+    memcpy(r0->win + (WIN - s->wl), s->win, s->wl);
     for (int k = 1; k < nkeep; ++k) {
-      const Region* p = &B->regs[B->idx[k - 1]];
-      Region* r = &B->regs[B->idx[k]];
-      const uint16_t* t = p->o + p->n - WIN;
-      for (uint32_t j = 0; j < WIN; ++j) r->win[j] = t[j] < 256 ? (uint8_t)t[j] : p->win[t[j] - 256];
+      Region* q = &s->regs[idx[k - 1]];
+      Region* r = &s->regs[idx[k]];
+      const uint16_t* t = q->o + q->n - WIN;
+      for (uint32_t j = 0; j < WIN; ++j) r->win[j] = t[j] < 256 ? (uint8_t)t[j] : q->win[t[j] - 256];
     }
   }
-  /* the current member's bytes before the next batch (its region 0's reach): since the batch's last member start,
-   * or all of the batch on top of the bytes before it */
-  uint64_t since = s->a_since + total;
-  for (int k = 0; k < nkeep; ++k) {
-    const Region* r = &B->regs[B->idx[k]];
-    for (uint64_t e = 0; e < r->nev; ++e)
-      if (r->ev[e].kind == EV_MSTART) since = total - (r->out_off + (r->ev[e].out - WIN));
-  }
-  s->a_since = since;
-  B->end_kind = lastr->end_kind;
-  s->next_wl = lastr->end_kind == K_BLOCK ? (uint32_t)(since < WIN ? since : WIN) : 0u;
-  /* drop the consumed compressed bytes (the batch's events keep their positions relative to cbase) */
-  B->cbase = s->cbase;
-  s->kind = lastr->end_kind;
-  const uint64_t endb = lastr->end >> 3;
-  memmove(s->cin, s->cin + endb, s->clen - endb);
-  s->clen -= endb;
-  s->cbase += endb;
-  s->pos = lastr->end - endb * 8;
-  s->prev_last = lastr;
-  s->batches++;
-  s->seq++;
-  *progress = 1;
-  return DPGZ_OK;
-}
-
-/* Resolve side, before the parallel phase: output space and the CRC segment arrays. */
-static int batch_prep_resolve(dpgz_par* s, Batch* B) {
   /* output space: [ohead, olen) unread + total; keep >= WIN bytes before the batch for the points' windows */
   if (s->ohead > 2 * WIN && s->ohead > s->olen / 2) {
     const uint64_t drop = s->ohead - WIN;
@@ -1216,35 +1135,33 @@ static int batch_prep_resolve(dpgz_par* s, Batch* B) {
     s->olen -= drop;
     s->ohead -= drop;
   }
-  if (grow((void**)&s->out, &s->ocap, s->olen + B->total + 1, 1)) return DPGZ_ERR_MEMORY;
+  if (grow((void**)&s->out, &s->ocap, s->olen + total + 1, 1)) return DPGZ_ERR_MEMORY;
   uint64_t nseg = 0;
-  for (int k = 0; k < B->nkeep; ++k) {
-    Region* r = &B->regs[B->idx[k]];
-    B->seg_off[k] = nseg;
+  uint64_t seg_off[257];
+  for (int k = 0; k < nkeep; ++k) {
+    Region* r = &s->regs[idx[k]];
+    seg_off[k] = nseg;
     for (uint64_t e = 0; e < r->nev; ++e) nseg += r->ev[e].kind != EV_BLOCK;
     ++nseg;
   }
-  B->seg_crc = (uint32_t*)malloc(nseg * sizeof(uint32_t));
-  B->seg_len = (uint64_t*)malloc(nseg * sizeof(uint64_t));
-  if (!B->seg_crc || !B->seg_len) {
-    free(B->seg_crc);
-    free(B->seg_len);
-    B->seg_crc = NULL;
-    B->seg_len = NULL;
-    return DPGZ_ERR_MEMORY;
-  }
-  B->dst = s->out + s->olen;
-  return DPGZ_OK;
-}
-
-/* Resolve side, after the parallel phase, in order: CRC / ISIZE per member, access points with their windows. */
-static int batch_finish_resolve(dpgz_par* s, Batch* B) {
+  uint32_t* seg_crc = (uint32_t*)malloc(nseg * sizeof(uint32_t));
+  uint64_t* seg_len = (uint64_t*)malloc(nseg * sizeof(uint64_t));
+  if (!seg_crc || !seg_len) { free(seg_crc); free(seg_len); return DPGZ_ERR_MEMORY; }
+  B.dst = s->out + s->olen;
+  B.seg_crc = seg_crc;
+  B.seg_len = seg_len;
+  B.seg_off = seg_off;
+  B.nkeep = nkeep;
+  t1 = now_ns(); s->ns[2] += t1 - t0; t0 = t1;
+  pool_for(&s->pool, nkeep, job_resolve, &B);
+  t1 = now_ns(); s->ns[3] += t1 - t0; t0 = t1;
+  /* in order: CRC / ISIZE per member, access points with their windows */
   int rc = DPGZ_OK;
   const uint8_t* hist = s->out;                         /* output offset of hist[0]: */
   const uint64_t hist_base = s->out_total - s->olen;
-  for (int k = 0; k < B->nkeep && rc == DPGZ_OK; ++k) {
-    Region* r = &B->regs[B->idx[k]];
-    uint64_t si = B->seg_off[k];
+  for (int k = 0; k < nkeep && rc == DPGZ_OK; ++k) {
+    Region* r = &s->regs[idx[k]];
+    uint64_t si = seg_off[k];
     const uint64_t rbase = s->out_total + r->out_off;   /* output offset of the region's first byte */
     for (uint64_t e = 0; e < r->nev && rc == DPGZ_OK; ++e) {
       const Ev* ev = &r->ev[e];
@@ -1252,13 +1169,13 @@ static int batch_finish_resolve(dpgz_par* s, Batch* B) {
       if (ev->kind == EV_BLOCK) {
         if (at - s->last >= s->span && at > s->mstart_out) {
           const uint64_t in_byte = (ev->bit + 7) >> 3;
-          if (add_point(s, B->cbase + in_byte, (uint32_t)(in_byte * 8 - ev->bit), at, 0, hist, hist_base))
+          if (add_point(s, s->cbase + in_byte, (uint32_t)(in_byte * 8 - ev->bit), at, 0, hist, hist_base))
             rc = DPGZ_ERR_MEMORY;
         }
         continue;
       }
-      s->crc = (uint32_t)crc32_combine(s->crc, B->seg_crc[si], (z_off_t)B->seg_len[si]);
-      s->msize += B->seg_len[si];
+      s->crc = (uint32_t)crc32_combine(s->crc, seg_crc[si], (z_off_t)seg_len[si]);
+      s->msize += seg_len[si];
       ++si;
       if (ev->kind == EV_MEND) {
         if (s->crc != ev->crc || (s->msize & 0xFFFFFFFFull) != ev->isize) rc = DPGZ_ERR_ZLIB;
@@ -1267,24 +1184,21 @@ static int batch_finish_resolve(dpgz_par* s, Batch* B) {
         s->msize = 0;
         s->mstart_out = at;
         s->members++;
-        if (add_point(s, B->cbase + (ev->bit >> 3), 0, at, 1, hist, hist_base)) rc = DPGZ_ERR_MEMORY;
+        if (add_point(s, s->cbase + (ev->bit >> 3), 0, at, 1, hist, hist_base)) rc = DPGZ_ERR_MEMORY;
       }
     }
-    if (rc == DPGZ_OK) {
-      s->crc = (uint32_t)crc32_combine(s->crc, B->seg_crc[si], (z_off_t)B->seg_len[si]);
-      s->msize += B->seg_len[si];
-    }
+    s->crc = (uint32_t)crc32_combine(s->crc, seg_crc[si], (z_off_t)seg_len[si]);
+    s->msize += seg_len[si];
   }
-  free(B->seg_crc);
-  free(B->seg_len);
-  B->seg_crc = NULL;
-  B->seg_len = NULL;
+  free(seg_crc);
+  free(seg_len);
   if (rc != DPGZ_OK) return rc;
-  s->olen += B->total;
-  s->out_total += B->total;
+  s->olen += total;
+  s->out_total += total;
   if (s->olen) s->prev = s->out[s->olen - 1];
-  /* the resolved window after the batch: the current member's last WIN bytes */
-  if (B->end_kind == K_BLOCK) {
+  /* the window for the next batch: the current member's last WIN bytes */
+  s->kind = lastr->end_kind;
+  if (s->kind == K_BLOCK) {
     uint64_t w0 = s->out_total > WIN ? s->out_total - WIN : 0;
     if (w0 < s->mstart_out) w0 = s->mstart_out;
     if (w0 < hist_base) return DPGZ_ERR_INVALID;         /* >= WIN bytes of history are always kept */
@@ -1294,53 +1208,15 @@ static int batch_finish_resolve(dpgz_par* s, Batch* B) {
   } else {
     s->wl = 0;
   }
-  return DPGZ_OK;
-}
-
-/* One step: the pending batch's resolution (if any) and, when `decode`, the next batch's decode, as one parallel
- * phase of both kinds of jobs (the resolve jobs first), then each side's in-order part.  *progress = 1 if the
- * decode moved; a batch decoded here stays pending until the next step (or dpgz_par_flush_). */
-typedef struct {
-  Batch* rb;
-  int nres;
-  Batch* db;
-} Step;
-static void job_step(void* a, int i) {
-  Step* st = (Step*)a;
-  if (i < st->nres) job_resolve(st->rb, i);
-  else job_find_decode(st->db, i - st->nres);
-}
-static int par_step(dpgz_par* s, int decode, int final, int* progress) {
-  *progress = 0;
-  uint64_t t0 = now_ns(), t1;
-  Batch* P = s->pend >= 0 ? &s->bt[s->pend] : NULL;
-  Batch* N = NULL;
-  if (decode) {
-    N = &s->bt[s->seq & 1u];
-    batch_prep_decode(s, N, final);
-  }
-  if (P) {
-    const int rc = batch_prep_resolve(s, P);
-    if (rc) return rc;
-  }
-  Step st = {P, P ? P->nkeep : 0, N};
-  const int njobs = st.nres + (N ? N->nreg : 0);
-  if (njobs) pool_for(&s->pool, njobs, job_step, &st);
-  t1 = now_ns(); s->ns[1] += t1 - t0; t0 = t1;
-  int rc = DPGZ_OK;
-  if (P) {
-    rc = batch_finish_resolve(s, P);
-    s->pend = -1;
-    if (rc) return rc;
-  }
-  t1 = now_ns(); s->ns[4] += t1 - t0; t0 = t1;
-  if (N) {
-    const uint64_t set = s->seq & 1u;
-    rc = batch_finish_decode(s, N, progress);
-    if (rc) return rc;
-    if (*progress) s->pend = (int)set;
-  }
-  s->ns[2] += now_ns() - t0;
+  /* drop the consumed compressed bytes */
+  const uint64_t endb = lastr->end >> 3;
+  memmove(s->cin, s->cin + endb, s->clen - endb);
+  s->clen -= endb;
+  s->cbase += endb;
+  s->pos = lastr->end - endb * 8;
+  s->batches++;
+  *progress = 1;
+  s->ns[4] += now_ns() - t0;
   return DPGZ_OK;
 }
 
@@ -1375,21 +1251,13 @@ int dpgz_par_feed(dpgz_par* s, const uint8_t* in, uint64_t in_len, int in_final)
   s->clen += in_len;
   const uint64_t want = (uint64_t)s->nregs * s->region_min;
   for (;;) {
+    if (s->kind == K_END) break;
     const uint64_t avail = s->clen - (s->pos >> 3);
-    const int decode = s->kind != K_END && (in_final || avail >= want);
+    if (!in_final && avail < want) break;
     int progress = 0;
-    if (!decode) {
-      /* nothing more to decode now: a pending batch waits for the next one (so the two overlap), unless the
-       * input or the stream has ended */
-      if (s->pend >= 0 && (in_final || s->kind == K_END)) {
-        const int rc = par_step(s, 0, 0, &progress);
-        if (rc) return s->failed = rc;
-      }
-      break;
-    }
-    const int rc = par_step(s, 1, in_final, &progress);
+    const int rc = par_batch(s, in_final, &progress);
     if (rc) return s->failed = rc;
-    if (!progress) {                                    /* (the pending batch was resolved in that step) */
+    if (!progress) {
       if (in_final) return s->failed = DPGZ_ERR_TRUNCATED;
       break;
     }
@@ -1439,7 +1307,7 @@ int dpgz_par_state(dpgz_par* s, uint64_t* stats) {
   stats[3] = s->olen - s->ohead;              /* inflated bytes not read yet */
   stats[4] = s->npts;
   stats[5] = s->nwin;
-  stats[6] = s->kind == K_END && s->pend < 0; /* the stream ended (and every batch is resolved) */
+  stats[6] = s->kind == K_END;                /* the stream ended */
   stats[7] = s->batches;
   stats[8] = s->rejected;                     /* region starts dropped (not a block boundary) */
   for (int i = 0; i < 5; ++i) stats[9 + i] = s->ns[i];   /* ns in find, decode, windows, resolve, bookkeeping */
