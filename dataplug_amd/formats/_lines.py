@@ -135,8 +135,12 @@ class MultipartWriter:
             self.st.put_object(Body=data.data, Bucket=self.bucket, Key=self.key, Metadata=self.meta)
             return self.size
         try:
-            if self.npend:
-                self._flush()
+            if self.npend:                        # the rest, in up to _PUT_THREADS parts uploaded side by side
+                rest = np.concatenate(self.pending) if len(self.pending) > 1 else self.pending[0]
+                step = max(5 << 20, -(-len(rest) // _PUT_THREADS))
+                for a in range(0, len(rest), step):
+                    self.pending, self.npend = [rest[a:a + step]], min(step, len(rest) - a)
+                    self._flush()
             for f in self.futs:
                 f.result()
             self.st.complete_multipart_upload(Bucket=self.bucket, Key=self.key, UploadId=self.uid, MultipartUpload={

@@ -688,6 +688,9 @@ def line_index_pieces(co, begin: int = 0, end: Optional[int] = None, delim: int 
 
 
 _PIECE_CTXS = 3               # contexts a streamed-index worker rotates: fetch, scan, read-back in flight at once
+# ranged-GET part of a streamed piece: the H2D of a piece starts when its first part lands (16 threads x 32 MiB parts
+# all landed together, ~5 ms into each 512 MiB piece)
+_PIECE_GET_PART = 8 << 20
 
 
 def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.Event) -> None:
@@ -754,7 +757,7 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
         if i >= _PIECE_CTXS:
             reads[i - _PIECE_CTXS].result()         # its context's previous piece is read back: staging is free
         host = ctxs[i % _PIECE_CTXS].pinned("object", hi - lo)
-        return submit_gets(pool, co.storage, co.path.bucket, co.path.key, lo, hi, host)
+        return submit_gets(pool, co.storage, co.path.bucket, co.path.key, lo, hi, host, _PIECE_GET_PART)
     with cf.ThreadPoolExecutor(1, thread_name_prefix=f"dpscan-readback{dev}") as rb:
         try:
             for i, (lo, hi, fut) in enumerate(jobs):
