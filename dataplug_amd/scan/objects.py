@@ -688,9 +688,9 @@ def line_index_pieces(co, begin: int = 0, end: Optional[int] = None, delim: int 
 
 
 _PIECE_CTXS = 3               # contexts a streamed-index worker rotates: fetch, scan, read-back in flight at once
-# ranged-GET part of a streamed piece: the H2D of a piece starts when its first part lands (16 threads x 32 MiB parts
-# all landed together, ~5 ms into each 512 MiB piece)
-_PIECE_GET_PART = 8 << 20
+# ranged-GET part of a streamed piece: 32 MiB (8 MiB parts let a piece's H2D start sooner in memory, 99 vs ~105 ms per
+# 4 GiB, but over HTTP every GET is a request of its own: 12 vs 20 GiB/s, profiles/r06/e2e/timeline_8mib_parts.log)
+_PIECE_GET_PART = _GET_PART
 
 
 def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.Event) -> None:
