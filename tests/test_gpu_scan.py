@@ -96,6 +96,36 @@ def test_synthetic_fasta_vs_oracle(ctx, size, seed, div):
     np.testing.assert_array_equal(pairs.astype(np.uint64), exp)
 
 
+def _long_header_fasta(size: int, seed: int, hmax: int) -> np.ndarray:
+    """Headers as long as the sequences (1 B .. ``hmax``): about half of the 16 MiB placement blocks start inside
+    a header line, some of them many 16 KiB ranges before its newline."""
+    rng = np.random.default_rng(seed)
+    a = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size)]
+    a[60::61] = 10
+    pos = 0
+    while pos < size:
+        h = int(rng.integers(1, hmax))
+        a[pos] = 62
+        a[pos + 1:pos + h] = 72
+        if pos + h < size:
+            a[pos + h] = 10
+        pos += h + 1 + int(rng.integers(1, hmax))
+    return a
+
+
+@pytest.mark.parametrize("hmax", [300, 40 << 10, 400 << 10])
+@pytest.mark.parametrize("div,u64", [(1, False), (5, True), (13, False)])
+def test_blocks_starting_inside_headers(ctx, hmax, div, u64):
+    """The placement kernel stages a block's slots before its incoming line state is known, guessing "not in a
+    header": blocks that start inside one (written straight up to the range where the states agree, or staged
+    again) give the oracle's pairs."""
+    a = _long_header_fasta((96 << 20) + 4097, 11 + div, hmax)
+    plan = cpu_ref.chunk_plan(len(a), math.ceil(len(a) / div))
+    exp = dpref.fasta_pairs(a, plan)
+    pairs, _ = _gpu_pairs(ctx, a, plan, u64=u64, offset=3)
+    np.testing.assert_array_equal(pairs.astype(np.uint64), exp)
+
+
 def test_quirk_chunk_size_eq_num_chunks_minus_one(ctx):
     a = synth.fasta(12 * 1024 + 3, 9)
     size = len(a)

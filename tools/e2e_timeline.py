@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--gib", type=float, default=4)
     ap.add_argument("--src", default="memory,http")
     ap.add_argument("--piece-mib", type=int, default=512)
+    ap.add_argument("--detail", action="store_true", help="mark GET parts, H2D issue, launches and read-backs")
     args = ap.parse_args()
     from dataplug_amd import synth
     from dataplug_amd.cloudobject import CloudObject
@@ -113,6 +114,37 @@ def main():
                         mark(_meth + "_end", key=str(kw.get("Key", ""))[-12:])
             setattr(cls, meth, m)
     wrap(_lines, "store_line_index_stream")
+    # inside the streamed pieces: GET parts (per thread), the H2D issue loop, the scan launch, the read-back wait
+    if args.detail:
+        from dataplug_amd.scan import device as sdev
+        real_rri = objects.read_range_into
+
+        def rri(storage, bucket, key, lo, hi, *a, **kw):
+            mark("get_start", lo=lo)
+            try:
+                return real_rri(storage, bucket, key, lo, hi, *a, **kw)
+            finally:
+                mark("get_end", lo=lo)
+        objects.read_range_into = rri
+        real_land = objects.land_gets
+
+        def land(ctx, gets, dp):
+            mark("land_start", n=gets[1])
+            try:
+                return real_land(ctx, gets, dp)
+            finally:
+                mark("land_end", n=gets[1])
+        objects.land_gets = land
+        for meth in ("delim_ranges_async", "delim_ranges_result", "sync"):
+            real_m = getattr(sdev.ScanContext, meth)
+
+            def m(self, *a, _real=real_m, _meth=meth, **kw):
+                mark(_meth + "_start", slot=getattr(self, "slot", None))
+                try:
+                    return _real(self, *a, **kw)
+                finally:
+                    mark(_meth + "_end", slot=getattr(self, "slot", None))
+            setattr(sdev.ScanContext, meth, m)
     # a sampler of the main thread's stack every 0.5 ms while a call runs: what it does in the gaps between marks
     samples = []
     sampling = threading.Event()
