@@ -96,7 +96,10 @@ def store_line_index(cloud_object, offsets) -> dict:
     return attrs
 
 
-PART_MIN = 16 << 20                # streamed index: bytes per multipart part (S3's minimum is 5 MiB)
+# streamed index: least bytes per multipart part (S3's minimum is 5 MiB).  A piece's low bytes (~15 MB per 512 MiB of
+# CSV) then go up as a part of their own, by reference: no concatenation on the consuming thread (16 MiB parts
+# joined two pieces, ~3 ms of copying under the GIL each, profiles/r06/e2e/)
+PART_MIN = 8 << 20
 
 
 class MultipartWriter:
@@ -104,8 +107,9 @@ class MultipartWriter:
     least ``part_min`` bytes go up as a multipart upload from the PUT threads as they fill; an object smaller than
     one part is one ``put_object`` at ``close``.  ``abort`` (or an exception in ``close``) removes the upload."""
 
-    def __init__(self, storage, bucket: str, key: str, meta: dict, part_min: int = PART_MIN):
-        self.st, self.bucket, self.key, self.meta, self.part_min = storage, bucket, key, meta, part_min
+    def __init__(self, storage, bucket: str, key: str, meta: dict, part_min: Optional[int] = None):
+        self.st, self.bucket, self.key, self.meta = storage, bucket, key, meta
+        self.part_min = PART_MIN if part_min is None else part_min
         self.pending, self.npend, self.size = [], 0, 0
         self.uid, self.futs = None, []
 

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--src", default="memory,http")
     ap.add_argument("--piece-mib", type=int, default=512)
     ap.add_argument("--detail", action="store_true", help="mark GET parts, H2D issue, launches and read-backs")
+    ap.add_argument("--calls", type=int, default=3)
+    ap.add_argument("--all-calls", action="store_true", help="print every call's events (not only the last's)")
     args = ap.parse_args()
     from dataplug_amd import synth
     from dataplug_amd.cloudobject import CloudObject
@@ -114,6 +116,9 @@ def main():
                         mark(_meth + "_end", key=str(kw.get("Key", ""))[-12:])
             setattr(cls, meth, m)
     wrap(_lines, "store_line_index_stream")
+    import pandas as pd
+    wrap(pd, "read_csv")
+    wrap(cob, "open_object")
     # inside the streamed pieces: GET parts (per thread), the H2D issue loop, the scan launch, the read-back wait
     if args.detail:
         from dataplug_amd.scan import device as sdev
@@ -180,7 +185,10 @@ def main():
             srv.wait_ready()
             cfg = {"endpoint_url": srv.url}
         co = CloudObject.from_s3(CSV, f"s3://{bucket}/x", s3_config=cfg)
-        for i in range(3):
+        for i in range(args.calls):
+            if args.all_calls:
+                for e in ev:
+                    print(json.dumps(dict(e, call=i - 1)))
             ev.clear()
             samples.clear()
             t0[0] = time.perf_counter()
