@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--piece-mib", type=int, default=512)
     ap.add_argument("--detail", action="store_true", help="mark GET parts, H2D issue, launches and read-backs")
     ap.add_argument("--calls", type=int, default=3)
+    ap.add_argument("--profile-ms", type=float, default=0, help="profile the main thread's first ms of every call")
     ap.add_argument("--all-calls", action="store_true", help="print every call's events (not only the last's)")
     args = ap.parse_args()
     from dataplug_amd import synth
@@ -194,7 +195,22 @@ def main():
             t0[0] = time.perf_counter()
             mark("call_start")
             sampling.set()
+            prof = []
+            if args.profile_ms:
+                # the main thread's calls and returns (Python and C) over the call's first ms: a gap between two of them
+                # is time spent inside one C call or waiting for the GIL
+                def hook(frame, event, arg, _t0=t0[0], _lim=args.profile_ms / 1e3):
+                    t = time.perf_counter() - _t0
+                    if t < _lim:
+                        name = getattr(arg, "__qualname__", None) if event.startswith("c_") else frame.f_code.co_name
+                        prof.append((t, event, f"{os.path.basename(frame.f_code.co_filename)}:{frame.f_lineno}", name))
+                sys.setprofile(hook)
             co.preprocess(force=True)
+            sys.setprofile(None)
+            for (ta, ea, wa, na), (tb, eb, wb, nb) in zip(prof, prof[1:]):
+                if tb - ta > 0.5e-3:
+                    print(json.dumps({"prof_gap_ms": round((tb - ta) * 1e3, 2), "at_ms": round(ta * 1e3, 2),
+                                      "from": [ea, wa, na], "to": [eb, wb, nb]}))
             sampling.clear()
             mark("call_end")
             dt = ev[-1]["t_ms"]
