@@ -186,6 +186,15 @@ def main():
             srv.wait_ready()
             cfg = {"endpoint_url": srv.url}
         co = CloudObject.from_s3(CSV, f"s3://{bucket}/x", s3_config=cfg)
+        prof = []
+        if args.profile_ms:
+            def hook(frame, event, arg, _lim=args.profile_ms / 1e3):
+                t = time.perf_counter() - t0[0]
+                if 0 <= t < _lim:
+                    name = getattr(arg, "__qualname__", None) if event.startswith("c_") else frame.f_code.co_name
+                    prof.append((t, threading.current_thread().name, event,
+                                 f"{os.path.basename(frame.f_code.co_filename)}:{frame.f_lineno}", name))
+            threading.setprofile(hook)            # every thread started from here on (the pools start in call 0)
         for i in range(args.calls):
             if args.all_calls:
                 for e in ev:
@@ -195,22 +204,23 @@ def main():
             t0[0] = time.perf_counter()
             mark("call_start")
             sampling.set()
-            prof = []
+            prof.clear()
             if args.profile_ms:
-                # the main thread's calls and returns (Python and C) over the call's first ms: a gap between two of them
-                # is time spent inside one C call or waiting for the GIL
-                def hook(frame, event, arg, _t0=t0[0], _lim=args.profile_ms / 1e3):
-                    t = time.perf_counter() - _t0
-                    if t < _lim:
-                        name = getattr(arg, "__qualname__", None) if event.startswith("c_") else frame.f_code.co_name
-                        prof.append((t, event, f"{os.path.basename(frame.f_code.co_filename)}:{frame.f_lineno}", name))
+                # every thread's calls and returns (Python and C) over the call's first ms: a gap between two of the
+                # main thread's is time spent inside one C call or waiting for the GIL; the other threads' events in
+                # that gap show who had it
                 sys.setprofile(hook)
             co.preprocess(force=True)
             sys.setprofile(None)
-            for (ta, ea, wa, na), (tb, eb, wb, nb) in zip(prof, prof[1:]):
+            mainp = [x for x in prof if x[1] == "MainThread"]
+            for (ta, _, ea, wa, na), (tb, _, eb, wb, nb) in zip(mainp, mainp[1:]):
                 if tb - ta > 0.5e-3:
                     print(json.dumps({"prof_gap_ms": round((tb - ta) * 1e3, 2), "at_ms": round(ta * 1e3, 2),
                                       "from": [ea, wa, na], "to": [eb, wb, nb]}))
+                    if tb - ta > 3e-3:
+                        others = [x for x in prof if x[1] != "MainThread" and ta - 1e-3 <= x[0] <= tb]
+                        for x in others[:12] + (others[-12:] if len(others) > 24 else others[12:]):
+                            print(json.dumps({"in_gap": [round(x[0] * 1e3, 3)] + list(x[1:])}))
             sampling.clear()
             mark("call_end")
             dt = ev[-1]["t_ms"]
