@@ -519,7 +519,7 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
             return None
         g = sp.groups[gi]
         host = sp.obj.bytes_range(g.lo, g.buf_hi)
-        d_in = ctxs[0].workspace(f"in_{tag}", len(host) + 64)
+        d_in = ctxs[0].workspace(f"in_{tag}", len(host) + 64, placed=True)
         ctxs[0].h2d(d_in.ptr, host)
         n_buf = len(host)
         del host                        # the host copy is not kept: verify() regenerates the bytes it checks
@@ -578,6 +578,7 @@ def fasta_worker(args, team, spec: FastaSpec, strong: FastaSpec | None, k: int, 
         team.barrier()                 # no group for this worker in the strong split: keep the barriers paired
         team.barrier()
     out["verified"] = verify(spec, st, res, args.steps - 1)
+    out["placement"] = list(ctxs[0].placements)
     for c in ctxs:
         c.close()
     out["rss_gib"] = peak_rss_gib()
@@ -600,6 +601,7 @@ def leg_fasta(args, world, rank, devs, team):
 
 
 def report_fasta(args, world, team, allres, spec, strong, t_leg):
+    from dataplug_amd.scan import device as sdev
     K = args.steps
     dt_ser = max(r["dt"] for r in allres)
     dt_ov = max(r["dt_overlap"] for r in allres)
@@ -677,6 +679,8 @@ def report_fasta(args, world, team, allres, spec, strong, t_leg):
                              "worker scanning (null when workers share a GPU)"},
         "cpu_baseline": cpu,
         "verified_bit_exact": verified,
+        "input_placement": {"probes": [r.get("placement") for r in allres], "note": "per worker, per placed input buffer: read-while-writing / read-only time ratio of each candidate allocation (ScanContext.workspace(placed=True): above PLACEMENT_SLOW = the slow placement mode, another buffer tried, at most PLACEMENT_TRIES, the best kept)",
+                            "slow_above": sdev.PLACEMENT_SLOW, "tries": sdev.PLACEMENT_TRIES},
         "gen_s": round(max(r["gen_s"] for r in allres), 2),
         "leg_s": round(t_leg, 2),
         "rss_gib_max_worker": max(r["rss_gib"] for r in allres),
@@ -770,7 +774,7 @@ def delim_worker(args, team, leg, k, world, dev):
     nbytes = end - begin
     n_exp = obj.count_range(begin, end)
     ctxs = (ScanContext(dev), ScanContext(dev))
-    d_buf = ctxs[0].workspace("bench_in", nbytes + 64)
+    d_buf = ctxs[0].workspace("bench_in", nbytes + 64, placed=True)
     d_ptr = d_buf.ptr + (begin & 15)                       # object offset and device address congruent mod 16
     step = 2 << 30                                           # materialize + upload 2 GiB at a time
     stage = np.empty(min(step, max(1, nbytes)), np.uint8)
@@ -841,7 +845,7 @@ def delim_worker(args, team, leg, k, world, dev):
            "alg_bytes": nbytes + item * n_out + (8 * ScanContext.block_table_size(rg)[1] if fmt in ("u8s", "u16b") else 0)
                         + (2 * ScanContext.sub_table_size(rg)[1] if fmt == "u8s" else 0),
            "verified": verified, "verify_s": t_ver, "gen_s": gen_s, "size": size, "wpr": wpr,
-           "stream_peak": peak, "mixed_peak": mixed, "range": (begin, end)}
+           "stream_peak": peak, "mixed_peak": mixed, "range": (begin, end), "placement": list(ctxs[0].placements)}
     for c in ctxs:
         c.close()
     out["rss_gib"] = peak_rss_gib()
@@ -854,6 +858,7 @@ def leg_delim(args, world, rank, devs, team, leg):
 
 
 def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
+    from dataplug_amd.scan import device as sdev
     csv_mode = leg == "csv"
     K = args.steps
     size = allres[0]["size"]
@@ -926,6 +931,8 @@ def report_delim(args, world, team, allres, leg, t_leg, headline: bool):
                              "barrier with no worker scanning, null when workers share a GPU"},
         "cpu_baseline": cpu,
         "verified_every_offset": verified,
+        "input_placement": {"probes": [r.get("placement") for r in allres], "note": "per worker, per placed input buffer: read-while-writing / read-only time ratio of each candidate allocation (ScanContext.workspace(placed=True): above PLACEMENT_SLOW = the slow placement mode, another buffer tried, at most PLACEMENT_TRIES, the best kept)",
+                            "slow_above": sdev.PLACEMENT_SLOW, "tries": sdev.PLACEMENT_TRIES},
         "gen_s": round(max(r["gen_s"] for r in allres), 2),
         "verify_s": round(max(r["verify_s"] for r in allres), 2),
         "leg_s": round(t_leg, 2),

@@ -64,6 +64,21 @@ class PinnedBuffer:
         self.ptr = 0
 
 
+# Placement-aware input buffers (round 6, profiles/r06/placement/): about half of the large device buffers a process
+# allocates sit in a "slow mode" where a kernel reading the buffer while writing a few % of its size elsewhere runs
+# 10-16 % slower than on the other half (reads alone are not affected; the input buffer alone decides, whatever the
+# output buffer).  An input buffer of at least PLACEMENT_MIN bytes is therefore probed when it is allocated: the
+# calibration kernels read it alone and read it while writing 1/32 of it; a time ratio above PLACEMENT_SLOW marks the
+# slow mode, and another buffer is allocated (the slow one held meanwhile, so it is not handed back) -- at most
+# PLACEMENT_TRIES, the best kept (or the best of those that fit in HBM).  Eight 4 GiB buffers of one process
+# (tools/placement_probe.py, profiles/r06/placement/probe8.log): ratios 1.088-1.106 where line_kernel's u8s scan of a
+# 4 GiB CSV takes 688-700 us, 1.167-1.193 where it takes 787-792 us.
+PLACEMENT_MIN = 256 << 20
+PLACEMENT_TRIES = 5
+PLACEMENT_SLOW = 1.125
+_PROBE_WPR = 1.0 / 32
+
+
 class ScanContext:
     """A ``dp_ctx``: device, stream and scan workspace.  Not shared between threads."""
 
@@ -76,17 +91,71 @@ class ScanContext:
         self._bufs = {}
         self._pinned = {}
         self._get_pool = None
+        self._timing_on = False
+        self.placements = []                          # per placed buffer: the probe ratios of its candidates
 
     # ---------------------------------------------------------------- memory
-    def workspace(self, name: str, nbytes: int) -> DeviceBuffer:
-        """Grow-only named device buffer."""
+    def workspace(self, name: str, nbytes: int, placed: bool = False) -> DeviceBuffer:
+        """Grow-only named device buffer; ``placed``: an input buffer, probed for the slow placement mode when it is
+        allocated (``PLACEMENT_MIN``)."""
         b = self._bufs.get(name)
         if b is None or b.nbytes < nbytes:
             if b is not None:
                 b.free()
-            b = DeviceBuffer(self, max(int(nbytes), 1 << 16))
+                del self._bufs[name]
+            size = max(int(nbytes), 1 << 16)
+            b = self._placed_buffer(size) if placed and size >= PLACEMENT_MIN else DeviceBuffer(self, size)
             self._bufs[name] = b
         return b
+
+    def placement_ratio(self, buf: DeviceBuffer, nbytes: Optional[int] = None) -> float:
+        """Time of the read-while-writing calibration kernel over ``buf`` / time of the read-only one (each the
+        mean of two launches): ~1.0-1.03 on a fast buffer, ~1.08-1.16 in the slow mode."""
+        n = (buf.nbytes if nbytes is None else nbytes) // 16 * 16
+        out = DeviceBuffer(self, int(n * _PROBE_WPR) + (1 << 16))
+        was_on = self._timing_on
+        try:
+            self.stream_read(buf.ptr, n)
+            self.sync()
+            t = []
+            for rw in (False, True):
+                self.timing(True)
+                self.timing_read()
+                for _ in range(2):
+                    if rw:
+                        self.stream_rw(buf.ptr, n, out.ptr, _PROBE_WPR)
+                    else:
+                        self.stream_read(buf.ptr, n)
+                ms, k = self.timing_read()
+                t.append(ms / max(1, k))
+            return t[1] / t[0]
+        finally:
+            self.timing(was_on)
+            out.free()
+
+    def _placed_buffer(self, size: int) -> DeviceBuffer:
+        cands = []
+        try:
+            for _ in range(PLACEMENT_TRIES):
+                try:
+                    c = DeviceBuffer(self, size)
+                except _lib.DPScanError:
+                    if cands:                         # no room for another candidate: the best so far
+                        break
+                    raise
+                cands.append((self.placement_ratio(c), c))
+                if cands[-1][0] <= PLACEMENT_SLOW:
+                    break
+        except BaseException:
+            for _, c in cands:
+                c.free()
+            raise
+        best = min(cands, key=lambda rc: rc[0])
+        for rc in cands:
+            if rc is not best:
+                rc[1].free()
+        self.placements.append([round(r, 4) for r, _ in cands])
+        return best[1]
 
     def pinned(self, name: str, nbytes: int) -> PinnedBuffer:
         """Grow-only named pinned host buffer."""
@@ -358,6 +427,7 @@ class ScanContext:
     # ---------------------------------------------------------------- timing / geometry
     def timing(self, enable: bool) -> None:
         check(self.lib.dp_timing_enable(self.handle, int(bool(enable))))
+        self._timing_on = bool(enable)
 
     def timing_read(self) -> Tuple[float, int]:
         ms = ctypes.c_double(0.0)

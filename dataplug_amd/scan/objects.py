@@ -315,7 +315,7 @@ def _fasta_group(dev: int, co, scan_plan: Sequence[Tuple[int, int]], pieces: Seq
     per_piece, first_nl = [], {}
     for p_ in fasta_passes(scan_plan, g, size, max_launch_bytes()):
         n = p_.buf_hi - p_.lo
-        d = ctx.workspace("input", n + 64)
+        d = ctx.workspace("input", n + 64, placed=True)
         fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, p_.lo, p_.buf_hi, d.ptr)
         pairs, pending, cend = ctx.fasta_index(d.ptr, n, p_.lo, size, p_.chunks(scan_plan), u64=u64)
         for p in pending[pending >= 0]:
@@ -532,7 +532,7 @@ def line_parts(begin: int, end: int, n_devices: int, part_bytes: int = 16 << 30)
 def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_add: int, fmt: str = "u64"):
     ctx = get_context(dev)
     n = hi - lo
-    d = ctx.workspace("input", n + 64)
+    d = ctx.workspace("input", n + 64, placed=True)
     dp = d.ptr + (lo & 15)                # object offset and device address congruent mod 16 (out_mode 3 grid)
     fetch_to_device(ctx, co.storage, co.path.bucket, co.path.key, lo, hi, dp)
     if fmt == "u64":
@@ -766,7 +766,7 @@ def _delim_piece_run(dev: int, co, jobs, delim: int, fmt: str, stop: threading.E
                 ctx = ctxs[i % _PIECE_CTXS]
                 gets = nxt if nxt is not None else queue_gets(i)
                 nxt = queue_gets(i + 1) if i + 1 < len(jobs) else None
-                d = ctx.workspace("input", hi - lo + 64)
+                d = ctx.workspace("input", hi - lo + 64, placed=True)
                 dp = d.ptr + (lo & 15)               # object offset and device address congruent mod 16
                 land_gets(ctx, gets, dp)
                 reads.append(rb.submit(collect, launch(ctx, lo, hi, dp), fut))
@@ -789,6 +789,6 @@ def record_index_bytes(data, delim: int = 10, every_k: int = 1, emit_add: int = 
         return np.zeros(0, np.uint64 if u64 else np.uint32), 0
     host = ctx.pinned("object", n)
     host.array[:n] = np.frombuffer(memoryview(data).cast("B"), np.uint8)
-    d = ctx.workspace("input", n + 64)
+    d = ctx.workspace("input", n + 64, placed=True)
     ctx.h2d_async(d.ptr, host.ptr, n)
     return ctx.delim_index(d.ptr, n, 0, 0, n, delim=delim, every_k=every_k, emit_add=emit_add, u64=u64)

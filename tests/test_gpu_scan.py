@@ -116,9 +116,9 @@ def _long_header_fasta(size: int, seed: int, hmax: int) -> np.ndarray:
 @pytest.mark.parametrize("hmax", [300, 40 << 10, 400 << 10])
 @pytest.mark.parametrize("div,u64", [(1, False), (5, True), (13, False)])
 def test_blocks_starting_inside_headers(ctx, hmax, div, u64):
-    """The placement kernel stages a block's slots before its incoming line state is known, guessing "not in a
-    header": blocks that start inside one (written straight up to the range where the states agree, or staged
-    again) give the oracle's pairs."""
+    """Placement blocks whose incoming line state is "inside a header" (about half of them here, some many 16 KiB
+    ranges before that header's newline) resolve it by the look-back and give the oracle's pairs, in uint32 and
+    uint64, with one, five and thirteen chunks."""
     a = _long_header_fasta((96 << 20) + 4097, 11 + div, hmax)
     plan = cpu_ref.chunk_plan(len(a), math.ceil(len(a) / div))
     exp = dpref.fasta_pairs(a, plan)
@@ -673,5 +673,28 @@ def test_form_follows_delimiter_density():
             assert c.last_delim_form() == want, (name, n, c.last_delim_form())
             r4 = c.delim_ranges(d.ptr, len(a), 0, [(0, n)], out_mode=4)
             assert c.last_delim_form() == 1 and r4[1] == len(r[0]), (name, n)
+    finally:
+        c.close()
+
+
+def test_placed_input_buffer_probe():
+    """A placed input workspace is probed at allocation (read-while-writing / read-only time of the calibration
+    kernels; another candidate while above PLACEMENT_SLOW), reused while large enough, and scans like any other."""
+    from dataplug_amd.scan import ScanContext
+    from dataplug_amd.scan import device as sdev
+    c = ScanContext(0)
+    try:
+        b = c.workspace("input", sdev.PLACEMENT_MIN + 123, placed=True)
+        assert len(c.placements) == 1 and 1 <= len(c.placements[0]) <= sdev.PLACEMENT_TRIES
+        assert all(0.5 < r < 3.0 for r in c.placements[0])
+        assert len(c.placements[0]) == sdev.PLACEMENT_TRIES or c.placements[0][-1] <= sdev.PLACEMENT_SLOW
+        assert c.workspace("input", 1 << 20, placed=True) is b and len(c.placements) == 1
+        a = synth.fasta(3 << 20, 5)
+        c.h2d(b.ptr, a)
+        plan = cpu_ref.chunk_plan(len(a), len(a) // 3 + 1)
+        pairs, _, _ = c.fasta_index(b.ptr, len(a), 0, len(a), plan)
+        np.testing.assert_array_equal(pairs.astype(np.uint64), dpref.fasta_pairs(a, plan))
+        c.workspace("small", 1 << 20, placed=True)        # below PLACEMENT_MIN: not probed
+        assert len(c.placements) == 1
     finally:
         c.close()

@@ -187,6 +187,47 @@ struct Variant {
   bool writes;
 };
 
+// VMM-composed input buffers (kinds 'v' and 'p'): physical chunks of UB_CHUNK_MIB (default 512) mapped into one
+// reserved VA range.  'p' probes each candidate chunk first (read-only vs read-while-writing time over the chunk,
+// through a temporary mapping) and keeps the fast ones; the slow candidates are held until the buffer is built.
+static hipMemAllocationProp vmm_prop() {
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = 0;
+  return prop;
+}
+
+static bool vmm_map(void* va, uint64_t off, uint64_t n, hipMemGenericAllocationHandle_t h) {
+  if (hipMemMap((char*)va + off, n, 0, h, 0) != hipSuccess) return false;
+  hipMemAccessDesc acc = {};
+  acc.location = vmm_prop().location;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  return hipMemSetAccess((char*)va + off, n, &acc, 1) == hipSuccess;
+}
+
+template <class KR, class KW>
+static float chunk_ratio(void* va, uint64_t n, uint4* out, uint64_t wq16, unsigned* sink, int grid, KR kr, KW kw) {
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  float t[2] = {0, 0};
+  for (int rep = 0; rep < 3; ++rep)
+    for (int v = 0; v < 2; ++v) {
+      hipEventRecord(a, 0);
+      if (v == 0) hipLaunchKernelGGL(kr, dim3(grid), dim3(1024), 0, 0, (const uint4*)va, n / kRange, nullptr, 0ull, sink);
+      else hipLaunchKernelGGL(kw, dim3(grid), dim3(1024), 0, 0, (const uint4*)va, n / kRange, out, wq16, sink);
+      hipEventRecord(b, 0);
+      hipEventSynchronize(b);
+      float ms;
+      hipEventElapsedTime(&ms, a, b);
+      if (rep > 0) t[v] += ms;
+    }
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  return t[1] / t[0];
+}
+
 int main(int argc, char** argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 4.0;
   const int nbuf = argc > 2 ? atoi(argv[2]) : 6;
@@ -200,16 +241,6 @@ int main(int argc, char** argv) {
   // argv[7]: per input buffer its allocation, d = hipMalloc, c = hipExtMallocWithFlags(hipDeviceMallocContiguous)
   const char* kinds = argc > 7 ? argv[7] : "";
   std::vector<uint4*> bufs(nbuf);
-  for (int i = 0; i < nbuf; ++i) {
-    const char k = i < (int)strlen(kinds) ? kinds[i] : 'd';
-    const hipError_t e = k == 'c' ? hipExtMallocWithFlags((void**)&bufs[i], bytes, hipDeviceMallocContiguous)
-                                  : hipMalloc(&bufs[i], bytes);
-    if (e != hipSuccess) {
-      printf("alloc %c failed\n", k);
-      return 1;
-    }
-    hipMemset(bufs[i], 0x41 + i, bytes);
-  }
   // argv[6]: output buffers (default 1); with more, every (input, output) pair is timed for each variant
   const int nout = argc > 6 ? atoi(argv[6]) : 1;
   std::vector<uint4*> outs(nout);
@@ -226,6 +257,75 @@ int main(int argc, char** argv) {
   if (hipMalloc(&sink, 64) != hipSuccess) {
     printf("alloc failed\n");
     return 1;
+  }
+  const uint64_t chunk = (uint64_t)(getenv("UB_CHUNK_MIB") ? atoi(getenv("UB_CHUNK_MIB")) : 512) << 20;
+  const double slow = getenv("UB_SLOW") ? atof(getenv("UB_SLOW")) : 1.125;
+  for (int i = 0; i < nbuf; ++i) {
+    const char k = i < (int)strlen(kinds) ? kinds[i] : 'd';
+    hipError_t e = hipSuccess;
+    if (k == 'v' || k == 'p') {
+      if (bytes % chunk) {
+        printf("size not a multiple of the chunk\n");
+        return 1;
+      }
+      void* va = nullptr;
+      const hipMemAllocationProp prop = vmm_prop();
+      if (hipMemAddressReserve(&va, bytes, 0, nullptr, 0) != hipSuccess) {
+        printf("reserve failed\n");
+        return 1;
+      }
+      std::vector<hipMemGenericAllocationHandle_t> held;
+      std::vector<float> ratios;
+      uint64_t off = 0;
+      int tries = 0;
+      while (off < bytes) {
+        hipMemGenericAllocationHandle_t h;
+        if (hipMemCreate(&h, chunk, &prop, 0) != hipSuccess) {
+          printf("create failed after %d tries\n", tries);
+          return 1;
+        }
+        ++tries;
+        bool keep = true;
+        if (k == 'p') {
+          void* tmp = nullptr;
+          hipMemAddressReserve(&tmp, chunk, 0, nullptr, 0);
+          if (!vmm_map(tmp, 0, chunk, h)) {
+            printf("temp map failed\n");
+            return 1;
+          }
+          hipMemset(tmp, 0x41, chunk);
+          const float r = chunk_ratio(tmp, chunk, outs[0], wq16, sink, grid, split_kernel<16, 0>, split_kernel<16, 1>);
+          ratios.push_back(r);
+          hipDeviceSynchronize();
+          hipMemUnmap(tmp, chunk);
+          hipMemAddressFree(tmp, chunk);
+          keep = r <= slow || tries > 4 * (int)(bytes / chunk);
+        }
+        if (keep) {
+          if (!vmm_map(va, off, chunk, h)) {
+            printf("map failed\n");
+            return 1;
+          }
+          off += chunk;
+        } else {
+          held.push_back(h);
+        }
+      }
+      for (auto h : held) hipMemRelease(h);
+      bufs[i] = (uint4*)va;
+      if (k == 'p') {
+        printf("{\"buffer\": %d, \"chunk_ratios\": [", i);
+        for (size_t j = 0; j < ratios.size(); ++j) printf("%s%.3f", j ? ", " : "", ratios[j]);
+        printf("]}\n");
+      }
+    } else {
+      e = k == 'c' ? hipExtMallocWithFlags((void**)&bufs[i], bytes, hipDeviceMallocContiguous) : hipMalloc(&bufs[i], bytes);
+    }
+    if (e != hipSuccess) {
+      printf("alloc %c failed\n", k);
+      return 1;
+    }
+    hipMemset(bufs[i], 0x41 + i, bytes);
   }
   hipDeviceSynchronize();
   const Variant all[] = {{"r16", split_kernel<16, 0>, false},  {"r15", split_kernel<15, 0>, false},
