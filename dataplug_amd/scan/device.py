@@ -72,8 +72,11 @@ class PinnedBuffer:
 # slow mode, and another buffer is allocated (the slow one held meanwhile, so it is not handed back) -- at most
 # PLACEMENT_TRIES, the best kept (or the best of those that fit in HBM).  Eight 4 GiB buffers of one process
 # (tools/placement_probe.py, profiles/r06/placement/probe8.log): ratios 1.088-1.106 where line_kernel's u8s scan of a
-# 4 GiB CSV takes 688-700 us, 1.167-1.193 where it takes 787-792 us.
+# 4 GiB CSV takes 688-700 us, 1.167-1.193 where it takes 787-792 us.  Larger buffers are mixtures (four 32 GiB
+# ones: ratios 1.055-1.108 against scans of 6,006-6,302 us, no separation; profiles/r06/placement/probe32.log), so
+# buffers above PLACEMENT_MAX are allocated once, unprobed.
 PLACEMENT_MIN = 256 << 20
+PLACEMENT_MAX = 8 << 30
 PLACEMENT_TRIES = 5
 PLACEMENT_SLOW = 1.125
 _PROBE_WPR = 1.0 / 32
@@ -97,14 +100,15 @@ class ScanContext:
     # ---------------------------------------------------------------- memory
     def workspace(self, name: str, nbytes: int, placed: bool = False) -> DeviceBuffer:
         """Grow-only named device buffer; ``placed``: an input buffer, probed for the slow placement mode when it is
-        allocated (``PLACEMENT_MIN``)."""
+        allocated (``PLACEMENT_MIN`` .. ``PLACEMENT_MAX`` bytes)."""
         b = self._bufs.get(name)
         if b is None or b.nbytes < nbytes:
             if b is not None:
                 b.free()
                 del self._bufs[name]
             size = max(int(nbytes), 1 << 16)
-            b = self._placed_buffer(size) if placed and size >= PLACEMENT_MIN else DeviceBuffer(self, size)
+            b = (self._placed_buffer(size) if placed and PLACEMENT_MIN <= size <= PLACEMENT_MAX
+                 else DeviceBuffer(self, size))
             self._bufs[name] = b
         return b
 

@@ -696,5 +696,6 @@ def test_placed_input_buffer_probe():
         np.testing.assert_array_equal(pairs.astype(np.uint64), dpref.fasta_pairs(a, plan))
         c.workspace("small", 1 << 20, placed=True)        # below PLACEMENT_MIN: not probed
         assert len(c.placements) == 1
+        assert sdev.PLACEMENT_MIN <= 4 << 30 <= sdev.PLACEMENT_MAX   # the FASTA headline's 4 GiB input is placed
     finally:
         c.close()

@@ -8,7 +8,7 @@
 //   sw15  15 loading waves; wave 15 alone stores the run (no loading wave ever has a store in its vmcnt)
 // If the slow buffers of rw16 / rw15 are fast under sw15, it is the shared counter; if sw15 is slow on the same
 // buffers, it is the memory system.  HIP events per launch, median of `reps`.
-//   hipcc --offload-arch=gfx950 -O3 -o tools/ubench_split tools/ubench_split.hip
+//   hipcc --offload-arch=gfx950 -O3 -Wno-unused-result -Wno-unused-value -o tools/ubench_split tools/ubench_split.hip
 //   ./tools/ubench_split [GiB per buffer=4] [buffers=6] [write bytes per read byte=0.025] [reps=5] [variants]
 //                        [output buffers=1] [allocation per input buffer: d / c, e.g. dcdc]
 #include <hip/hip_runtime.h>
@@ -190,6 +190,8 @@ struct Variant {
 // VMM-composed input buffers (kinds 'v' and 'p'): physical chunks of UB_CHUNK_MIB (default 512) mapped into one
 // reserved VA range.  'p' probes each candidate chunk first (read-only vs read-while-writing time over the chunk,
 // through a temporary mapping) and keeps the fast ones; the slow candidates are held until the buffer is built.
+// (Round 6: 'v' works -- 4 GiB buffers of 512 MiB chunks read-while-write in 679-757 us, mixtures like large
+// hipMalloc buffers; 'p' ran at 1 GiB but crashed in the host runtime at 4 GiB after a few temporary mappings.)
 static hipMemAllocationProp vmm_prop() {
   hipMemAllocationProp prop = {};
   prop.type = hipMemAllocationTypePinned;
@@ -270,7 +272,12 @@ int main(int argc, char** argv) {
       }
       void* va = nullptr;
       const hipMemAllocationProp prop = vmm_prop();
-      if (hipMemAddressReserve(&va, bytes, 0, nullptr, 0) != hipSuccess) {
+      size_t gran = 0;
+      hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum);
+      int vmm = 0;
+      hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, 0);
+      fprintf(stderr, "vmm supported %d granularity %zu\n", vmm, gran);
+      if (!vmm || hipMemAddressReserve(&va, bytes, 0, nullptr, 0) != hipSuccess) {
         printf("reserve failed\n");
         return 1;
       }
@@ -285,6 +292,7 @@ int main(int argc, char** argv) {
           return 1;
         }
         ++tries;
+        fprintf(stderr, "chunk %d created\n", tries);
         bool keep = true;
         if (k == 'p') {
           void* tmp = nullptr;
@@ -302,6 +310,7 @@ int main(int argc, char** argv) {
           keep = r <= slow || tries > 4 * (int)(bytes / chunk);
         }
         if (keep) {
+          fprintf(stderr, "map at %llu\n", (unsigned long long)off);
           if (!vmm_map(va, off, chunk, h)) {
             printf("map failed\n");
             return 1;
@@ -313,6 +322,7 @@ int main(int argc, char** argv) {
       }
       for (auto h : held) hipMemRelease(h);
       bufs[i] = (uint4*)va;
+      fprintf(stderr, "buffer %d mapped\n", i);
       if (k == 'p') {
         printf("{\"buffer\": %d, \"chunk_ratios\": [", i);
         for (size_t j = 0; j < ratios.size(); ++j) printf("%s%.3f", j ? ", " : "", ratios[j]);
