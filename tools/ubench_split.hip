@@ -191,7 +191,8 @@ struct Variant {
 // reserved VA range.  'p' probes each candidate chunk first (read-only vs read-while-writing time over the chunk,
 // through a temporary mapping) and keeps the fast ones; the slow candidates are held until the buffer is built.
 // (Round 6: 'v' works -- 4 GiB buffers of 512 MiB chunks read-while-write in 679-757 us, mixtures like large
-// hipMalloc buffers; 'p' ran at 1 GiB but crashed in the host runtime at 4 GiB after a few temporary mappings.)
+// hipMalloc buffers.  'p' probing through temporary mappings crashed in the host runtime at 4 GiB; it now probes
+// each chunk in place, at its final offset, and unmaps a slow one.)
 static hipMemAllocationProp vmm_prop() {
   hipMemAllocationProp prop = {};
   prop.type = hipMemAllocationTypePinned;
@@ -295,19 +296,24 @@ int main(int argc, char** argv) {
         fprintf(stderr, "chunk %d created\n", tries);
         bool keep = true;
         if (k == 'p') {
-          void* tmp = nullptr;
-          hipMemAddressReserve(&tmp, chunk, 0, nullptr, 0);
-          if (!vmm_map(tmp, 0, chunk, h)) {
-            printf("temp map failed\n");
+          // probe the chunk in place (mapped at its final offset); a slow one is unmapped and held
+          if (!vmm_map(va, off, chunk, h)) {
+            printf("map failed\n");
             return 1;
           }
-          hipMemset(tmp, 0x41, chunk);
-          const float r = chunk_ratio(tmp, chunk, outs[0], wq16, sink, grid, split_kernel<16, 0>, split_kernel<16, 1>);
+          hipMemset((char*)va + off, 0x41, chunk);
+          const float r = chunk_ratio((char*)va + off, chunk, outs[0], wq16, sink, grid, split_kernel<16, 0>,
+                                      split_kernel<16, 1>);
           ratios.push_back(r);
           hipDeviceSynchronize();
-          hipMemUnmap(tmp, chunk);
-          hipMemAddressFree(tmp, chunk);
           keep = r <= slow || tries > 4 * (int)(bytes / chunk);
+          if (keep) {
+            off += chunk;
+          } else {
+            hipMemUnmap((char*)va + off, chunk);
+            held.push_back(h);
+          }
+          continue;
         }
         if (keep) {
           fprintf(stderr, "map at %llu\n", (unsigned long long)off);
