@@ -72,7 +72,8 @@ class PinnedBuffer:
 # slow mode, and another buffer is allocated (the slow one held meanwhile, so it is not handed back) -- at most
 # PLACEMENT_TRIES, the best kept (or the best of those that fit in HBM).  Eight 4 GiB buffers of one process
 # (tools/placement_probe.py, profiles/r06/placement/probe8.log): ratios 1.088-1.106 where line_kernel's u8s scan of a
-# 4 GiB CSV takes 688-700 us, 1.167-1.193 where it takes 787-792 us.  Larger buffers are mixtures (four 32 GiB
+# 4 GiB CSV takes 688-700 us, 1.167-1.193 where it takes 787-792 us (8 GiB: 1.080-1.094 / 1,352-1,356 us against
+# 1.184-1.199 / 1,567-1,569 us, probe8g.log).  Larger buffers are mixtures (four 32 GiB
 # ones: ratios 1.055-1.108 against scans of 6,006-6,302 us, no separation; profiles/r06/placement/probe32.log), so
 # buffers above PLACEMENT_MAX are allocated once, unprobed.
 PLACEMENT_MIN = 256 << 20
