@@ -549,7 +549,7 @@ def _delim_group(dev: int, co, lo: int, hi: int, delim: int, every_k: int, emit_
 
 
 def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int = 10,
-                      max_devices: Optional[int] = None, part_bytes: int = 16 << 30, fmt: str = "u64"):
+                      max_devices: Optional[int] = None, part_bytes: int = 8 << 30, fmt: str = "u64"):
     """Sorted offsets of every ``delim`` byte of object bytes [begin, end) in one of ``INDEX_FORMATS``:
     ``u64`` a uint64 array; ``u32p`` a ``PagedOffsets`` (uint32 low words + 4 GiB page counts); ``u16b`` a
     ``BlockedOffsets`` (uint16 low words + a 64 KiB block table); ``u8s`` a ``ByteOffsets`` (uint8 low bytes + the
@@ -557,7 +557,8 @@ def line_index_object(co, begin: int = 0, end: Optional[int] = None, delim: int 
     u16b by the object's delimiter density (``line_index_form``).
 
     The range is cut into independent parts (at most ``part_bytes`` each, at least one per GPU) scanned
-    round-robin on the GPUs and concatenated in order."""
+    round-robin on the GPUs and concatenated in order.  The default 8 GiB parts fit an input buffer the context
+    allocates placement-aware (``device.PLACEMENT_MAX``: larger buffers are not probed)."""
     if fmt != "auto" and fmt not in INDEX_FORMATS:
         raise ValueError(f"index format must be 'auto' or one of {INDEX_FORMATS}, not {fmt!r}")
     end = co.size if end is None else end
